@@ -1,0 +1,119 @@
+"""ctypes binding of libdora_gpu.so (include/dora_gpu.h).
+
+The library is built in-tree (dora_amd/lib/, `python -m dora_amd.build`).  There is no CPU
+fallback: if the library is missing, importing the data plane raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8, c_uint64,
+                    c_void_p)
+
+from .arrow_c import ArrowArray, ArrowSchema
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libdora_gpu.so")
+
+ARROW_DEVICE_CPU = 1
+ARROW_DEVICE_ROCM = 10
+ARROW_DEVICE_ROCM_HOST = 11
+
+DORA_OK = 0
+ERRORS = {-1: "invalid", -2: "hip", -3: "too_small", -4: "unsupported", -5: "closed",
+          -6: "timeout", -7: "not_found"}
+
+
+class DoraGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{ERRORS.get(code, code)}] {msg}")
+        self.code = code
+
+
+class UnsupportedType(DoraGpuError):
+    pass
+
+
+# name -> (restype, argtypes); `int` restype means a status code that is checked.
+_SIGS = {
+    "dora_gpu_last_error": (c_char_p, []),
+    "dora_gpu_version": (c_char_p, []),
+    "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
+    "dora_gpu_set_device": (c_int, [c_int]),
+    "dora_gpu_get_device": (c_int, [POINTER(c_int)]),
+    "dora_gpu_stream_create": (c_int, [POINTER(c_void_p)]),
+    "dora_gpu_stream_destroy": (c_int, [c_void_p]),
+    "dora_gpu_stream_sync": (c_int, [c_void_p]),
+    "dora_gpu_device_sync": (c_int, []),
+    "dora_gpu_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
+    "dora_gpu_free": (c_int, [c_void_p]),
+    "dora_gpu_host_alloc": (c_int, [POINTER(c_void_p), c_size_t]),
+    "dora_gpu_host_free": (c_int, [c_void_p]),
+    "dora_gpu_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dora_gpu_memset_async": (c_int, [c_void_p, c_int, c_size_t, c_void_p]),
+    "dora_gpu_event_create": (c_int, [POINTER(c_void_p)]),
+    "dora_gpu_event_destroy": (c_int, [c_void_p]),
+    "dora_gpu_event_record": (c_int, [c_void_p, c_void_p]),
+    "dora_gpu_event_sync": (c_int, [c_void_p]),
+    "dora_gpu_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "dora_gpu_plan": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema), c_int32,
+                              POINTER(c_void_p)]),
+    "dora_gpu_plan_bytes": (c_int, [c_void_p, c_size_t, c_int32, POINTER(c_void_p)]),
+    "dora_gpu_plan_free": (None, [c_void_p]),
+    "dora_gpu_plan_size": (c_size_t, [c_void_p]),
+    "dora_gpu_plan_num_segments": (c_size_t, [c_void_p]),
+    "dora_gpu_plan_segment": (c_int, [c_void_p, c_size_t, POINTER(c_void_p), POINTER(c_uint64),
+                                      POINTER(c_uint64)]),
+    "dora_gpu_plan_type_info": (c_int, [c_void_p, POINTER(c_uint8), c_size_t,
+                                        POINTER(c_size_t)]),
+    "dora_gpu_pack": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dora_gpu_array_upload": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema),
+                                      POINTER(ArrowArray)]),
+    "dora_gpu_array_download": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema),
+                                        POINTER(ArrowArray)]),
+    "dora_gpu_sample_import": (c_int, [c_void_p, c_size_t, POINTER(c_uint8), c_size_t,
+                                       POINTER(ArrowArray), POINTER(ArrowSchema)]),
+    "dora_gpu_type_info_schema": (c_int, [POINTER(c_uint8), c_size_t, POINTER(ArrowSchema)]),
+    "dora_gpu_array_release": (None, [POINTER(ArrowArray)]),
+    "dora_gpu_schema_release": (None, [POINTER(ArrowSchema)]),
+    "dora_gpu_csum64": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
+    "dora_gpu_csum64_sync": (c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_uint64)]),
+    "dora_gpu_fill_splitmix": (c_int, [c_void_p, c_size_t, c_uint64, c_void_p]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libdora_gpu.so and declare every signature; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -m dora_amd.build` (there is no CPU "
+            "fallback for the device data plane)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def check(rc: int) -> int:
+    if rc != DORA_OK:
+        msg = _lib.dora_gpu_last_error().decode(errors="replace")
+        cls = UnsupportedType if rc == -4 else DoraGpuError
+        raise cls(rc, msg)
+    return rc
+
+
+def call(name: str, *args):
+    lib = load()
+    return check(getattr(lib, name)(*args))

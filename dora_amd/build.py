@@ -1,0 +1,98 @@
+"""Builds the in-tree native artefacts with hipcc for gfx950 (no CMake, no JIT cache).
+
+    python -m dora_amd.build            # libdora_gpu.so + tools
+Outputs land in dora_amd/lib/ (git-ignored, but shipped to the GPU box by gpurun).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dora_amd", "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(ROOT, "dora_amd", "lib")
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ARCH = "gfx950"
+
+LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip"]
+LIB_NAME = "libdora_gpu.so"
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+            f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    hs.append(os.path.abspath(__file__))
+    return hs
+
+
+def _compile(src, obj, verbose):
+    if src.endswith(".hip"):
+        cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", *CXXFLAGS, "-c", src, "-o", obj]
+    else:
+        cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", *CXXFLAGS, "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _compile_all(sources, verbose):
+    os.makedirs(OBJ, exist_ok=True)
+    heads = _headers()
+    objs = []
+    for s in sources:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s.replace("/", "_") + ".o")
+        if _newer(obj, [src, *heads]):
+            _compile(src, obj, verbose)
+        objs.append(obj)
+    return objs
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(LIB, exist_ok=True)
+    objs = _compile_all(LIB_SOURCES, verbose)
+    out = os.path.join(LIB, LIB_NAME)
+    if _newer(out, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
+               "-Wl,-soname," + LIB_NAME, "-lpthread", "-lrt"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return out
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))
+
+
+TOOLS = {}  # binary name -> list of sources (filled as native tools land)
+
+
+def build_tools(verbose: bool = False):
+    out = []
+    lib = build(verbose)
+    for name, srcs in TOOLS.items():
+        objs = _compile_all(srcs, verbose)
+        exe = os.path.join(LIB, name)
+        if _newer(exe, objs + [lib]):
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-o", exe, *objs, f"-L{LIB}", "-ldora_gpu",
+                   f"-Wl,-rpath,{LIB}", "-Wl,-rpath,$ORIGIN", "-lpthread", "-lrt"]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+        out.append(exe)
+    return out

@@ -1,0 +1,330 @@
+// HIP kernels of the data plane (gfx950): the batched segmented pack that replaces
+// `copy_array_into_sample` (apis/rust/node/src/node/arrow_utils.rs:23-71), the csum64 parity
+// reduction and the splitmix64 payload generator.
+//
+// Pack = pure HBM streaming: read S bytes + write S bytes, no MFMA, no LDS.  Every chunk of a
+// segment is one 256-thread workgroup.  The destination is written with 16-byte aligned
+// `global_store_dwordx4`; the source is read with 16-byte aligned `global_load_dwordx4` and,
+// when source and destination disagree mod 16 (e.g. C3's x buffer at sample offset 68), two
+// aligned loads are funnel-shifted with v_alignbyte_b32.  The shift is uniform per segment, so
+// the per-segment loop is specialised on it and no lane diverges.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "plan.h"
+
+namespace dora {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+constexpr int kMaxSegs = 32;
+
+struct PackSeg {
+  const uint8_t* src;
+  uint64_t dst_off;
+  uint64_t len;
+};
+
+struct PackArgs {
+  uint8_t* dst;
+  uint32_t nseg;
+  uint32_t chunk_bytes;  // multiple of 16
+  uint32_t chunk_end[kMaxSegs];
+  PackSeg seg[kMaxSegs];
+};
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+  return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+// Bytes [4Q + b, 4Q + b + 16) of the 32-byte little-endian concatenation lo|hi.
+template <int Q>
+__device__ __forceinline__ uint4 funnel(uint4 lo, uint4 hi, uint32_t b) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint4 o;
+  o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], b);
+  o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], b);
+  o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], b);
+  o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], b);
+  return o;
+}
+
+// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` (any alignment).
+__device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * kUnroll) {
+    uint4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) v[u] = ld16(sp + 16 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) st16(dp + 16 * i, v[u]);
+    }
+  }
+}
+
+template <int Q>
+__device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
+                                             uint64_t nunits) {
+  // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * kUnroll) {
+    uint4 lo[kUnroll], hi[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) {
+        lo[u] = ld16(sbase + 16 * i);
+        hi[u] = ld16(sbase + 16 * i + 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) st16(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
+  const uint32_t chunk = blockIdx.x;
+  uint32_t s = 0;
+  while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
+  const PackSeg sg = args.seg[s];
+  const uint32_t c = chunk - (s ? args.chunk_end[s - 1] : 0u);
+
+  // 16-byte alignment is taken on absolute addresses (the sample base may be unaligned).
+  const uint64_t base = reinterpret_cast<uintptr_t>(args.dst);
+  const uint64_t d0 = sg.dst_off, d1 = sg.dst_off + sg.len;
+  const uint64_t A0 = (base + d0 + 15) & ~uint64_t(15);
+  const uint64_t A1 = (base + d1) & ~uint64_t(15);
+  const uint64_t a0 = A0 - base;
+  const uint64_t a1 = A1 > A0 ? A1 - base : a0;  // body [a0, a1) empty unless A1 > A0
+  uint8_t* const dst = args.dst;
+  const uint8_t* const src = sg.src;  // source byte of sample offset d is src[d - d0]
+
+  if (c == 0) {
+    // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1), byte by byte (< 16 each).
+    const uint64_t hend = a0 < d1 ? a0 : d1;
+    const uint64_t nhead = hend - d0;
+    if (threadIdx.x < nhead) dst[d0 + threadIdx.x] = src[threadIdx.x];
+    if (a0 < d1) {
+      const uint64_t t0 = a1 > a0 ? a1 : a0;
+      const uint64_t ntail = d1 - t0;
+      if (threadIdx.x >= 64 && threadIdx.x - 64 < ntail) {
+        const uint64_t d = t0 + (threadIdx.x - 64);
+        dst[d] = src[d - d0];
+      }
+    }
+  }
+  if (a0 >= a1) return;
+  const uint64_t b0 = a0 + uint64_t(c) * args.chunk_bytes;
+  if (b0 >= a1) return;
+  const uint64_t b1 = (a1 - b0) > args.chunk_bytes ? b0 + args.chunk_bytes : a1;
+  const uint64_t nunits = (b1 - b0) >> 4;
+  uint8_t* dp = dst + b0;
+  const uint8_t* sp = src + (b0 - d0);
+  const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
+  if (r == 0) {
+    copy_aligned(dp, sp, nunits);
+    return;
+  }
+  const uint8_t* sbase = sp - r;
+  const uint32_t b = r & 3;
+  switch (r >> 2) {
+    case 0: copy_shifted<0>(dp, sbase, b, nunits); break;
+    case 1: copy_shifted<1>(dp, sbase, b, nunits); break;
+    case 2: copy_shifted<2>(dp, sbase, b, nunits); break;
+    default: copy_shifted<3>(dp, sbase, b, nunits); break;
+  }
+}
+
+uint32_t choose_chunk_bytes(uint64_t body_bytes) {
+  if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
+    uint64_t v = std::strtoull(e, nullptr, 10);
+    if (v >= 16 && v % 16 == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
+  }
+  // One pass of a 256-thread block with 4 loads in flight moves 16 KiB; aim for >= ~2k
+  // workgroups on big messages (256 CUs x 8 resident) and a few passes per block beyond that.
+  const uint64_t pass = uint64_t(kThreads) * 16 * kUnroll;
+  uint64_t cb = (body_bytes / 2048 + pass - 1) / pass * pass;
+  cb = std::max<uint64_t>(cb, pass);
+  cb = std::min<uint64_t>(cb, uint64_t(1) << 22);
+  return static_cast<uint32_t>(cb);
+}
+
+// ------------------------------------------------------------------------------------------
+// csum64 (oracle/checksum_ref.py): S = sum_i fmix64(word_i ^ (i * GOLDEN + SEED)); fmix64(S+n)
+// ------------------------------------------------------------------------------------------
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kSeed = 0xD0A5D0A5D0A5D0A5ull;
+
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void csum_kernel(const uint8_t* __restrict__ p, uint64_t n,
+                                                        unsigned long long* __restrict__ acc) {
+  const uint64_t nw = (n + 7) / 8;
+  const uint64_t full = n / 8;
+  const bool aligned8 = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  uint64_t s = 0;
+  for (uint64_t i = blockIdx.x * uint64_t(kThreads) + threadIdx.x; i < nw;
+       i += uint64_t(gridDim.x) * kThreads) {
+    uint64_t w = 0;
+    if (aligned8 && i < full) {
+      w = reinterpret_cast<const uint64_t*>(p)[i];
+    } else {
+      const uint64_t lim = (i < full) ? 8 : (n - 8 * i);
+      for (uint64_t k = 0; k < lim; ++k) w |= uint64_t(p[8 * i + k]) << (8 * k);
+    }
+    s += fmix64(w ^ (i * kGolden + kSeed));
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, static_cast<unsigned long long>(s));
+}
+
+__global__ void csum_finalize(unsigned long long* acc, uint64_t n) {
+  *acc = fmix64(static_cast<uint64_t>(*acc) + n);
+}
+
+// splitmix64 payload: word k = fmix64(seed + (k + 1) * GOLDEN), little-endian bytes.
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t* __restrict__ p, uint64_t n,
+                                                        uint64_t seed) {
+  const uint64_t nw = (n + 7) / 8;
+  const bool aligned8 = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  for (uint64_t i = blockIdx.x * uint64_t(kThreads) + threadIdx.x; i < nw;
+       i += uint64_t(gridDim.x) * kThreads) {
+    const uint64_t w = fmix64(seed + (i + 1) * kGolden);
+    if (aligned8 && 8 * i + 8 <= n) {
+      reinterpret_cast<uint64_t*>(p)[i] = w;
+    } else {
+      for (uint64_t k = 0; k < 8 && 8 * i + k < n; ++k) p[8 * i + k] = uint8_t(w >> (8 * k));
+    }
+  }
+}
+
+unsigned grid_for(uint64_t items) {
+  uint64_t g = (items + kThreads - 1) / kThreads;
+  return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 4096)));
+}
+
+}  // namespace
+
+// Launch the pack of `n` segments into `dst` (device).  Segments with device sources go to
+// pack_kernel in batches of kMaxSegs; host sources are DMA'd with hipMemcpyAsync.
+int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
+                hipStream_t stream) {
+  if (dev == ARROW_DEVICE_CPU) {
+    for (size_t i = 0; i < n; ++i)
+      DORA_HIP(hipMemcpyAsync(dst + segs[i].dst_off, segs[i].src, segs[i].len,
+                              hipMemcpyHostToDevice, stream));
+    return DORA_OK;
+  }
+  size_t i = 0;
+  while (i < n) {
+    PackArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.dst = dst;
+    uint64_t body = 0;
+    const size_t m = std::min<size_t>(kMaxSegs, n - i);
+    for (size_t k = 0; k < m; ++k) body += segs[i + k].len;
+    a.chunk_bytes = choose_chunk_bytes(body);
+    uint64_t chunks = 0;
+    for (size_t k = 0; k < m; ++k) {
+      const Segment& s = segs[i + k];
+      a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
+      const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+      const uint64_t A0 = (base + s.dst_off + 15) & ~uint64_t(15);
+      const uint64_t A1 = (base + s.dst_off + s.len) & ~uint64_t(15);
+      const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
+      const uint64_t nc = std::max<uint64_t>(1, (bodyb + a.chunk_bytes - 1) / a.chunk_bytes);
+      chunks += nc;
+      if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
+      a.chunk_end[k] = static_cast<uint32_t>(chunks);
+    }
+    a.nseg = static_cast<uint32_t>(m);
+    hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
+                       stream, a);
+    DORA_HIP(hipGetLastError());
+    i += m;
+  }
+  return DORA_OK;
+}
+
+int launch_csum(const void* data, size_t len, uint64_t* out_dev, hipStream_t stream) {
+  DORA_HIP(hipMemsetAsync(out_dev, 0, sizeof(uint64_t), stream));
+  if (len) {
+    hipLaunchKernelGGL(csum_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
+                       static_cast<const uint8_t*>(data), uint64_t(len),
+                       reinterpret_cast<unsigned long long*>(out_dev));
+    DORA_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(csum_finalize, dim3(1), dim3(1), 0, stream,
+                     reinterpret_cast<unsigned long long*>(out_dev), uint64_t(len));
+  DORA_HIP(hipGetLastError());
+  return DORA_OK;
+}
+
+int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
+  if (!len) return DORA_OK;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
+                     static_cast<uint8_t*>(dst), uint64_t(len), seed);
+  DORA_HIP(hipGetLastError());
+  return DORA_OK;
+}
+
+}  // namespace dora
+
+extern "C" {
+
+int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_t stream) {
+  if (!plan) return dora::fail(DORA_ERR_INVALID, "plan is NULL");
+  if (dst_len < plan->size)
+    // arrow_utils.rs:37-42 asserts; the C ABI reports instead
+    return dora::fail(DORA_ERR_TOO_SMALL,
+                      "target buffer too small (total_len: %zu, required_len: %llu)", dst_len,
+                      static_cast<unsigned long long>(plan->size));
+  if (plan->segs.empty()) return DORA_OK;
+  if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
+  return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
+                           static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream));
+}
+
+int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream_t stream) {
+  if (!out_dev || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  return dora::launch_csum(data, len, out_dev, static_cast<hipStream_t>(stream));
+}
+
+int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uint64_t* out) {
+  if (!out || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  uint64_t* d = nullptr;
+  DORA_HIP(hipMalloc(&d, sizeof(uint64_t)));
+  int rc = dora::launch_csum(data, len, d, static_cast<hipStream_t>(stream));
+  if (rc == DORA_OK) {
+    hipError_t e = hipMemcpyAsync(out, d, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                  static_cast<hipStream_t>(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) rc = dora::fail(DORA_ERR_HIP, "csum64 readback: %s", hipGetErrorString(e));
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream) {
+  if (!dst && len) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
+  return dora::launch_fill(dst, len, seed, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,386 @@
+// Host-side planning of a pack: the a1 walk (`required_data_size_inner`,
+// apis/rust/node/src/node/arrow_utils.rs:9-21) and the ArrowTypeInfo half of
+// `copy_array_into_sample_inner` (arrow_utils.rs:28-71), over the Arrow C Data Interface.
+//
+// Restated third-party rules (arrow-rs 53.2.0, pinned by Cargo.lock, not vendored):
+//   * layout(): arrow-data `layout()` buffer specs and alignments (Rust 1.76: i128 align 8);
+//   * buffer lengths: arrow-rs FFI import `buffer_len` (offsets (len+offset+1)*w, Utf8/Binary
+//     data = last offset, everything else ceil((len+offset)*bits/8));
+//   * nulls: kept only when the null count is non-zero (ArrayDataBuilder::build filter).
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "plan.h"
+
+namespace dora {
+namespace {
+
+bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+}  // namespace
+
+// arrow-data 53.2.0 `layout()`; throws std::domain_error for types outside the parity set.
+Layout layout_of(const std::string& f) {
+  Layout l;
+  auto fixed = [&](uint32_t w, uint32_t a) { l.specs.push_back({BufSpec::Fixed, w, a}); };
+  if (f == "n") {
+    l.can_null = false;
+  } else if (f == "b") {
+    l.specs.push_back({BufSpec::Bitmap, 0, 1});
+  } else if (f == "c" || f == "C") {
+    fixed(1, 1);
+  } else if (f == "s" || f == "S" || f == "e") {
+    fixed(2, 2);
+  } else if (f == "i" || f == "I" || f == "f" || f == "tdD" || f == "tts" || f == "ttm" ||
+             f == "tiM") {
+    fixed(4, 4);
+  } else if (f == "l" || f == "L" || f == "g" || f == "tdm" || f == "ttu" || f == "ttn" ||
+             starts_with(f, "ts") || starts_with(f, "tD")) {
+    fixed(8, 8);
+  } else if (f == "tiD") {
+    fixed(8, 4);  // IntervalDayTime {i32, i32}
+  } else if (f == "tin") {
+    fixed(16, 8);  // IntervalMonthDayNano {i32, i32, i64}
+  } else if (starts_with(f, "d:")) {
+    // "d:precision,scale[,bitwidth]"; i128 / i256 have align 8 on the pinned Rust 1.76
+    int commas = 0;
+    size_t last = 0;
+    for (size_t i = 0; i < f.size(); ++i)
+      if (f[i] == ',') ++commas, last = i;
+    int bw = commas >= 2 ? std::stoi(f.substr(last + 1)) : 128;
+    if (bw != 128 && bw != 256) throw std::invalid_argument("decimal bit width " + f);
+    fixed(static_cast<uint32_t>(bw / 8), 8);
+  } else if (starts_with(f, "w:")) {
+    fixed(static_cast<uint32_t>(std::stoul(f.substr(2))), 1);
+  } else if (f == "z" || f == "u") {
+    fixed(4, 4);
+    l.specs.push_back({BufSpec::Var, 0, 1});
+    l.offsets_first = true;
+  } else if (f == "Z" || f == "U") {
+    fixed(8, 8);
+    l.specs.push_back({BufSpec::Var, 0, 1});
+    l.offsets_first = true;
+  } else if (f == "+l" || f == "+m") {
+    fixed(4, 4);
+    l.offsets_first = true;
+  } else if (f == "+L") {
+    fixed(8, 8);
+    l.offsets_first = true;
+  } else if (starts_with(f, "+w:") || f == "+s") {
+    // children only
+  } else if (f == "+r") {
+    l.can_null = false;
+  } else {
+    // views (vz/vu: the reference's zip drops variadic buffers), unions, list views
+    throw std::domain_error("arrow format '" + f + "' is outside the supported parity set");
+  }
+  return l;
+}
+
+uint64_t metadata_len(const char* meta) {
+  // Arrow C metadata: i32 n, then n × (i32 klen, key, i32 vlen, value)
+  if (!meta) return 0;
+  int32_t n;
+  std::memcpy(&n, meta, 4);
+  uint64_t off = 4;
+  for (int32_t i = 0; i < n; ++i)
+    for (int kv = 0; kv < 2; ++kv) {
+      int32_t l;
+      std::memcpy(&l, meta + off, 4);
+      off += 4 + static_cast<uint64_t>(l);
+    }
+  return off;
+}
+
+std::string schema_sig(const ArrowSchema* s) {
+  std::string fmt = s->format ? s->format : "";
+  if (s->dictionary) {
+    std::string out = "dict<" + fmt + "," + schema_sig(s->dictionary);
+    if (s->flags & ARROW_FLAG_DICTIONARY_ORDERED) out += ",ordered";
+    return out + ">";
+  }
+  std::string out = fmt;
+  if (fmt == "+m" && (s->flags & ARROW_FLAG_MAP_KEYS_SORTED)) out += "s";
+  if (s->n_children > 0) {
+    out += "[";
+    for (int64_t i = 0; i < s->n_children; ++i) {
+      const ArrowSchema* c = s->children[i];
+      if (i) out += ",";
+      out += c->name ? c->name : "";
+      out += ":";
+      out += (c->flags & ARROW_FLAG_NULLABLE) ? "?" : "!";
+      out += schema_sig(c);
+    }
+    out += "]";
+  }
+  return out;
+}
+
+namespace {
+
+void put_str(std::vector<uint8_t>& o, const char* p, uint64_t n) {
+  for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(n >> (8 * i)));
+  o.insert(o.end(), p, p + n);
+}
+
+}  // namespace
+
+void serialize_schema(const ArrowSchema* s, bool top, std::vector<uint8_t>& o) {
+  const char* f = s->format ? s->format : "";
+  put_str(o, f, std::strlen(f));
+  const char* nm = (!top && s->name) ? s->name : "";
+  put_str(o, nm, std::strlen(nm));
+  int64_t flags = s->flags;
+  if (top) flags &= (ARROW_FLAG_DICTIONARY_ORDERED | ARROW_FLAG_MAP_KEYS_SORTED);
+  for (int i = 0; i < 8; ++i) o.push_back(static_cast<uint8_t>(uint64_t(flags) >> (8 * i)));
+  const uint64_t ml = top ? 0 : metadata_len(s->metadata);
+  o.push_back(ml ? 1 : 0);
+  if (ml) put_str(o, s->metadata, ml);
+  const uint32_t nc = static_cast<uint32_t>(s->n_children);
+  for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(nc >> (8 * i)));
+  for (uint32_t i = 0; i < nc; ++i) serialize_schema(s->children[i], false, o);
+  o.push_back(s->dictionary ? 1 : 0);
+  if (s->dictionary) serialize_schema(s->dictionary, false, o);
+}
+
+namespace {
+
+struct Reader {
+  ArrowDeviceType dev;
+  void read(void* dst, const void* src, size_t n) const {
+    if (n == 0) return;
+    if (dev == ARROW_DEVICE_ROCM) {
+      hipError_t e = hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
+      if (e != hipSuccess)
+        throw std::runtime_error(std::string("hipMemcpy D2H during plan: ") +
+                                 hipGetErrorString(e));
+    } else {
+      std::memcpy(dst, src, n);
+    }
+  }
+};
+
+uint64_t count_nulls(const std::vector<uint8_t>& v, uint64_t off, uint64_t len) {
+  uint64_t n = 0;
+  for (uint64_t i = off; i < off + len; ++i) n += ((v[i >> 3] >> (i & 7)) & 1) ? 0 : 1;
+  return n;
+}
+
+uint64_t pad_to(uint64_t x, const BufSpec& sp) {
+  if (sp.kind != BufSpec::Fixed) return x;
+  return (x + sp.align - 1) / sp.align * sp.align;
+}
+
+// One ArrayData node: buffers in layout order, then children (DFS pre-order), exactly as
+// copy_array_into_sample_inner walks it.
+void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t& next,
+          std::vector<Segment>& segs, TypeInfoNode& ti) {
+  if (!a || !s || !s->format) throw std::invalid_argument("null ArrowArray/ArrowSchema node");
+  const std::string fmt = s->format;
+  const bool is_dict = s->dictionary != nullptr;
+  Layout l = layout_of(fmt);  // dictionary: layout(key type) == layout(index format)
+  if (is_dict) l.offsets_first = false;
+  if (a->length < 0 || a->offset < 0) throw std::invalid_argument("negative length/offset");
+  const uint64_t len = static_cast<uint64_t>(a->length);
+  const uint64_t off = static_cast<uint64_t>(a->offset);
+  const uint64_t total = len + off;
+  const int64_t begin = l.can_null ? 1 : 0;
+  if (a->n_buffers < begin + static_cast<int64_t>(l.specs.size()))
+    throw std::invalid_argument("ArrowArray for '" + fmt + "' has too few buffers");
+
+  ti.sig = schema_sig(s);
+  serialize_schema(s, true, ti.schema);
+  ti.len = len;
+  ti.offset = off;
+  ti.null_count = 0;
+  ti.has_validity = false;
+
+  std::vector<uint64_t> lens;
+  for (size_t k = 0; k < l.specs.size(); ++k) {
+    const BufSpec& sp = l.specs[k];
+    const void* p = a->buffers[begin + static_cast<int64_t>(k)];
+    uint64_t blen;
+    if (sp.kind == BufSpec::Var) {
+      if (len == 0) {
+        blen = 0;
+      } else {
+        const uint32_t ow = l.specs[0].width;
+        const uint64_t last = lens[0] / ow - 1;
+        const uint8_t* op = static_cast<const uint8_t*>(a->buffers[begin]) + last * ow;
+        if (ow == 4) {
+          int32_t v;
+          rd.read(&v, op, 4);
+          if (v < 0) throw std::invalid_argument("negative last offset");
+          blen = static_cast<uint64_t>(v);
+        } else {
+          int64_t v;
+          rd.read(&v, op, 8);
+          if (v < 0) throw std::invalid_argument("negative last offset");
+          blen = static_cast<uint64_t>(v);
+        }
+      }
+    } else if (k == 0 && l.offsets_first) {
+      blen = (total + 1) * sp.width;
+    } else {
+      const uint64_t bits = sp.kind == BufSpec::Bitmap ? 1 : uint64_t(sp.width) * 8;
+      blen = (total * bits + 7) / 8;
+    }
+    lens.push_back(blen);
+    if (!p && blen != 0)
+      throw std::invalid_argument("buffer " + std::to_string(begin + k) + " of '" + fmt +
+                                  "' is null but has length " + std::to_string(blen));
+    next = pad_to(next, sp);
+    ti.bufs.push_back({next, blen});
+    if (blen) segs.push_back({p, next, blen});
+    next += blen;
+  }
+
+  if (l.can_null && a->n_buffers > 0 && a->buffers[0]) {
+    std::vector<uint8_t> v((total + 7) / 8);
+    rd.read(v.data(), a->buffers[0], v.size());
+    uint64_t nc = a->null_count >= 0 ? static_cast<uint64_t>(a->null_count)
+                                     : count_nulls(v, off, len);
+    if (nc != 0) {
+      ti.has_validity = true;
+      ti.validity = std::move(v);
+      ti.null_count = nc;
+    }
+  }
+
+  if (is_dict) {
+    if (!a->dictionary) throw std::invalid_argument("dictionary schema without dictionary data");
+    ti.children.emplace_back();
+    walk(a->dictionary, s->dictionary, rd, next, segs, ti.children.back());
+  } else {
+    if (a->n_children != s->n_children)
+      throw std::invalid_argument("array/schema child count mismatch for '" + fmt + "'");
+    for (int64_t i = 0; i < a->n_children; ++i) {
+      ti.children.emplace_back();
+      walk(a->children[i], s->children[i], rd, next, segs, ti.children.back());
+    }
+  }
+}
+
+void put_u8(std::vector<uint8_t>& o, uint8_t v) { o.push_back(v); }
+void put_u32(std::vector<uint8_t>& o, uint32_t v) {
+  for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(v >> (8 * i)));
+}
+void put_u64(std::vector<uint8_t>& o, uint64_t v) {
+  for (int i = 0; i < 8; ++i) o.push_back(static_cast<uint8_t>(v >> (8 * i)));
+}
+
+}  // namespace
+
+void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& o) {
+  put_u32(o, static_cast<uint32_t>(t.schema.size()));
+  o.insert(o.end(), t.schema.begin(), t.schema.end());
+  put_u64(o, t.len);
+  put_u64(o, t.null_count);
+  put_u8(o, t.has_validity ? 1 : 0);
+  if (t.has_validity) {
+    put_u64(o, t.validity.size());
+    o.insert(o.end(), t.validity.begin(), t.validity.end());
+  }
+  put_u64(o, t.offset);
+  put_u32(o, static_cast<uint32_t>(t.bufs.size()));
+  for (auto& b : t.bufs) {
+    put_u64(o, b.first);
+    put_u64(o, b.second);
+  }
+  put_u32(o, static_cast<uint32_t>(t.children.size()));
+  for (auto& c : t.children) serialize_type_info(c, o);
+}
+
+int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
+               dora_plan** out) {
+  if (!out) return fail(DORA_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  if (dev != ARROW_DEVICE_CPU && dev != ARROW_DEVICE_ROCM && dev != ARROW_DEVICE_ROCM_HOST)
+    return fail(DORA_ERR_INVALID, "unsupported device_type %d", dev);
+  auto* p = new dora_plan();
+  p->dev = dev;
+  try {
+    Reader rd{dev};
+    uint64_t next = 0;
+    walk(array, schema, rd, next, p->segs, p->root);
+    p->size = next;
+  } catch (const std::domain_error& e) {
+    delete p;
+    return fail(DORA_ERR_UNSUPPORTED, "%s", e.what());
+  } catch (const std::exception& e) {
+    delete p;
+    return fail(DORA_ERR_INVALID, "plan: %s", e.what());
+  }
+  *out = p;
+  return DORA_OK;
+}
+
+}  // namespace dora
+
+extern "C" {
+
+int dora_gpu_plan(const struct ArrowArray* array, const struct ArrowSchema* schema,
+                  ArrowDeviceType device_type, dora_plan** out) {
+  return dora::build_plan(array, schema, device_type, out);
+}
+
+int dora_gpu_plan_bytes(const void* src, size_t len, ArrowDeviceType device_type,
+                        dora_plan** out) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  if (!src && len) return dora::fail(DORA_ERR_INVALID, "src is NULL");
+  DORA_GUARD_BEGIN
+  auto* p = new dora_plan();
+  p->dev = device_type;
+  p->size = len;
+  // ArrowTypeInfo::byte_array(len), libraries/message/src/metadata.rs:74-87
+  p->root.sig = "C";
+  {
+    ArrowSchema u8{};
+    u8.format = "C";
+    dora::serialize_schema(&u8, true, p->root.schema);
+  }
+  p->root.len = len;
+  p->root.bufs.push_back({0, len});
+  if (len) p->segs.push_back({src, 0, len});
+  *out = p;
+  return DORA_OK;
+  DORA_GUARD_END
+}
+
+void dora_gpu_plan_free(dora_plan* plan) { delete plan; }
+
+size_t dora_gpu_plan_size(const dora_plan* plan) { return plan ? plan->size : 0; }
+
+size_t dora_gpu_plan_num_segments(const dora_plan* plan) { return plan ? plan->segs.size() : 0; }
+
+int dora_gpu_plan_segment(const dora_plan* plan, size_t i, const void** src, uint64_t* dst_off,
+                          uint64_t* len) {
+  if (!plan || i >= plan->segs.size())
+    return dora::fail(DORA_ERR_INVALID, "segment index %zu out of range", i);
+  if (src) *src = plan->segs[i].src;
+  if (dst_off) *dst_off = plan->segs[i].dst_off;
+  if (len) *len = plan->segs[i].len;
+  return DORA_OK;
+}
+
+int dora_gpu_plan_type_info(const dora_plan* plan, uint8_t* buf, size_t cap, size_t* len) {
+  if (!plan || !len) return dora::fail(DORA_ERR_INVALID, "plan/len is NULL");
+  DORA_GUARD_BEGIN
+  std::vector<uint8_t> o;
+  dora::serialize_type_info(plan->root, o);
+  *len = o.size();
+  if (!buf) return DORA_OK;
+  if (cap < o.size())
+    return dora::fail(DORA_ERR_TOO_SMALL, "type info needs %zu bytes, buffer has %zu", o.size(),
+                      cap);
+  std::memcpy(buf, o.data(), o.size());
+  return DORA_OK;
+  DORA_GUARD_END
+}
+
+}  // extern "C"

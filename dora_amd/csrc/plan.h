@@ -1,0 +1,63 @@
+// Internal plan structures shared by plan.cpp and the pack launcher.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dora_gpu.h"
+
+namespace dora {
+
+struct BufSpec {
+  enum Kind { Fixed, Bitmap, Var } kind;
+  uint32_t width;  // bytes per element for Fixed
+  uint32_t align;  // FixedWidth alignment (arrow-data layout())
+};
+
+struct Layout {
+  std::vector<BufSpec> specs;
+  bool can_null = true;
+  bool offsets_first = false;  // first non-null buffer is an offsets buffer of len+1 entries
+};
+
+// ArrowTypeInfo (libraries/message/src/metadata.rs:51-59) with the data type as a signature.
+struct TypeInfoNode {
+  std::string sig;                  // canonical signature (comparison key)
+  std::vector<uint8_t> schema;      // serialized DataType (see serialize_schema)
+  uint64_t len = 0;
+  uint64_t null_count = 0;
+  bool has_validity = false;
+  std::vector<uint8_t> validity;
+  uint64_t offset = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> bufs;  // BufferOffset {offset, len}
+  std::vector<TypeInfoNode> children;
+};
+
+// One copy of `copy_array_into_sample_inner` (arrow_utils.rs:48): src -> sample[dst_off..+len].
+struct Segment {
+  const void* src;
+  uint64_t dst_off;
+  uint64_t len;
+};
+
+void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& out);
+// DataType as a schema tree: str format, str name, i64 flags, u8 has_meta [str meta],
+// u32 n_children × Schema, u8 has_dict [Schema].  The top level carries no name and only the
+// type-relevant flags (dictionary ordered / map keys sorted).
+void serialize_schema(const ArrowSchema* s, bool top, std::vector<uint8_t>& out);
+std::string schema_sig(const ArrowSchema* s);
+uint64_t metadata_len(const char* meta);
+Layout layout_of(const std::string& format);
+int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
+               dora_plan** out);
+
+}  // namespace dora
+
+struct dora_plan {
+  ArrowDeviceType dev = ARROW_DEVICE_ROCM;
+  uint64_t size = 0;
+  std::vector<dora::Segment> segs;
+  dora::TypeInfoNode root;
+};

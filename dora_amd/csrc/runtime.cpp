@@ -1,0 +1,142 @@
+// Runtime plumbing of the C ABI: errors, devices, streams, events, memory.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "common.h"
+
+namespace dora {
+
+static thread_local char g_last_error[1024] = "no error";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+void clear_error() { std::strcpy(g_last_error, "no error"); }
+
+}  // namespace dora
+
+extern "C" {
+
+const char* dora_gpu_last_error(void) { return dora::g_last_error; }
+
+const char* dora_gpu_version(void) { return "dora-gpu 0.3.6-mi355x gfx950"; }
+
+int dora_gpu_device_count(int* count) {
+  if (!count) return dora::fail(DORA_ERR_INVALID, "count is NULL");
+  DORA_HIP(hipGetDeviceCount(count));
+  return DORA_OK;
+}
+
+int dora_gpu_set_device(int ordinal) {
+  DORA_HIP(hipSetDevice(ordinal));
+  return DORA_OK;
+}
+
+int dora_gpu_get_device(int* ordinal) {
+  if (!ordinal) return dora::fail(DORA_ERR_INVALID, "ordinal is NULL");
+  DORA_HIP(hipGetDevice(ordinal));
+  return DORA_OK;
+}
+
+int dora_gpu_stream_create(dora_stream_t* out) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  hipStream_t s;
+  DORA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *out = s;
+  return DORA_OK;
+}
+
+int dora_gpu_stream_destroy(dora_stream_t stream) {
+  DORA_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+  return DORA_OK;
+}
+
+int dora_gpu_stream_sync(dora_stream_t stream) {
+  DORA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return DORA_OK;
+}
+
+int dora_gpu_device_sync(void) {
+  DORA_HIP(hipDeviceSynchronize());
+  return DORA_OK;
+}
+
+int dora_gpu_malloc(void** out, size_t nbytes) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  DORA_HIP(hipMalloc(out, nbytes ? nbytes : 1));
+  return DORA_OK;
+}
+
+int dora_gpu_free(void* ptr) {
+  DORA_HIP(hipFree(ptr));
+  return DORA_OK;
+}
+
+int dora_gpu_host_alloc(void** out, size_t nbytes) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  DORA_HIP(hipHostMalloc(out, nbytes ? nbytes : 1, hipHostMallocDefault));
+  return DORA_OK;
+}
+
+int dora_gpu_host_free(void* ptr) {
+  DORA_HIP(hipHostFree(ptr));
+  return DORA_OK;
+}
+
+int dora_gpu_memcpy_async(void* dst, const void* src, size_t nbytes, dora_stream_t stream) {
+  if (!nbytes) return DORA_OK;
+  DORA_HIP(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+  return DORA_OK;
+}
+
+int dora_gpu_memset_async(void* dst, int value, size_t nbytes, dora_stream_t stream) {
+  if (!nbytes) return DORA_OK;
+  DORA_HIP(hipMemsetAsync(dst, value, nbytes, static_cast<hipStream_t>(stream)));
+  return DORA_OK;
+}
+
+int dora_gpu_event_create(dora_event_t* out) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  hipEvent_t e;
+  DORA_HIP(hipEventCreate(&e));
+  *out = e;
+  return DORA_OK;
+}
+
+int dora_gpu_event_destroy(dora_event_t ev) {
+  DORA_HIP(hipEventDestroy(static_cast<hipEvent_t>(ev)));
+  return DORA_OK;
+}
+
+int dora_gpu_event_record(dora_event_t ev, dora_stream_t stream) {
+  DORA_HIP(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)));
+  return DORA_OK;
+}
+
+int dora_gpu_event_sync(dora_event_t ev) {
+  DORA_HIP(hipEventSynchronize(static_cast<hipEvent_t>(ev)));
+  return DORA_OK;
+}
+
+int dora_gpu_event_elapsed_ms(dora_event_t start, dora_event_t stop, float* ms) {
+  if (!ms) return dora::fail(DORA_ERR_INVALID, "ms is NULL");
+  DORA_HIP(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+  return DORA_OK;
+}
+
+}  // extern "C"
