@@ -119,7 +119,7 @@ def test_alignment_sweep(dev, src_mis):
     from oracle.checksum_ref import splitmix_bytes
     rng = np.random.default_rng(src_mis)
     data = splitmix_bytes(70000, 0xD05A + src_mis)
-    src = device.DeviceBuffer.from_bytes(b"\0" * 32 + data, dev)
+    src = device.DeviceBuffer.from_bytes(b"\0" * (16 + src_mis) + data + b"\0" * 16, dev)
     dst = device.DeviceBuffer(80000)
     try:
         for dst_off in range(16):
