@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py — node->node device data plane on MI355X (BASELINE.json metric).
+
+One rank per GPU.  Each rank runs its own local dataflow on its GPU (weak scaling: dataflow
+graphs shard by node placement, SURVEY.md §8e — no data-path collective):
+
+    node (this process, `path: dynamic`) --latency/throughput--> sink (dora-gpu-bench-sink)
+         ^------------------------------------ ack ---------------------------------'
+
+A step = one message of `--size` bytes (default 40,960,000 B, the top of the C2 ladder) sent
+with `send_output_raw` semantics: allocate a device slot (20-entry recycled cache), HIP pack
+kernel HBM->HBM from the node's device-resident source, descriptor through the daemon, IPC-mapped
+zero-copy delivery at the sink, drop token back.  The timed region is K back-to-back steps
+closed by the sink's ack of the last one, bracketed by barrier + device sync.
+
+value = total payload bytes delivered by all ranks / max-over-ranks time (GB/s).
+The JSON line also carries the per-size latency ladder (p50/p99, reference semantics: timestamp
+after the fill), the pack-kernel roofline (HIP events on the node stream) and the CPU baseline
+(C++ restatement of the reference shm path, oracle/build/shm_baseline, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LADDER = [4096, 16384, 40960, 65536, 409600, 1 << 20, 4096000, 4 << 20, 16 << 20, 40960000]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--size", type=int, default=40960000)
+    ap.add_argument("--lat-n", type=int, default=50, help="latency-mode messages per size")
+    ap.add_argument("--lat-gap-us", type=int, default=1000)
+    ap.add_argument("--no-ladder", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
+    return ap.parse_args()
+
+
+def cpu_baseline(rank_cores):
+    """Reference shm path restated in C++ (oracle/shm_baseline.cpp), bounded sample."""
+    exe = os.path.join(ROOT, "oracle", "build", "shm_baseline")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    cores = ",".join(str(c) for c in rank_cores[:3])
+    sizes = "4096,40960,409600,4096000,40960000"
+    out = subprocess.run([exe, "--sizes", sizes, "--lat-n", "20", "--lat-gap-us", "10000",
+                          "--tp-n", "40", "--cores", cores], capture_output=True, text=True,
+                         timeout=300, check=True).stdout
+    return json.loads(out)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    affinity = sorted(os.sched_getaffinity(0))
+
+    # ---- CPU-only work and process spawning first: nothing below touches HIP until Node() ----
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(affinity)
+
+    from dora_amd.dataflow import Dataflow
+    result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["latency", "throughput"],
+         "inputs": {"ack": "sink/ack"}, "_unstable_deploy": {"gpu": local_rank}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"latency": {"source": "node/latency", "queue_size": 10},
+                    "throughput": {"source": "node/throughput", "queue_size": 10}},
+         "env": {"DORA_BENCH_RESULT": result_path}, "_unstable_deploy": {"gpu": local_rank}},
+    ]}
+    df = Dataflow(desc).start()
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    from dora_amd import device
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    from dora_amd.workloads import payload_seed
+
+    node = Node("node", dataflow=df.shm, device=local_rank)
+    stream = device.Stream()
+    S = args.size
+    nsrc = args.sources or max(2, min(16, (640 << 20) // max(S, 1)))
+    srcs = []
+    for _ in range(nsrc):   # rotate > 512 MiB of sources so the Infinity Cache cannot hold them
+        b = device.DeviceBuffer(S)
+        device.fill_splitmix(b.ptr, S, payload_seed(S), stream)
+        srcs.append(b)
+    stream.sync()
+    csum = device.csum64(srcs[0].ptr, S, stream)
+
+    def wait_ack(seq, timeout=60.0):
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            ev = node.next(timeout=1.0)
+            if ev and ev["type"] == "INPUT" and ev["id"] == "ack" and \
+                    ev["metadata"].get("seq") == seq:
+                return True
+        raise RuntimeError(f"no ack for seq {seq}")
+
+    # ---- warmup (the first messages are verified bit-exact by the sink's csum kernel) ----
+    seq = 0
+    for k in range(args.warmup):
+        meta = {"seq": seq, "t_start": time.time_ns()}
+        if k < 3:
+            meta.update({"csum": to_i64(csum), "verify": True})
+        node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S, meta)
+        seq += 1
+    node.send_output("throughput", b"", {"seq": seq, "ack": True})
+    wait_ack(seq)
+    seq += 1
+
+    # ---- latency ladder (reference latency mode: spaced messages, output `latency`) ----
+    ladder_bufs = {}
+    if not args.no_ladder:
+        for size in LADDER:
+            b = device.DeviceBuffer(size)
+            device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
+            ladder_bufs[size] = b
+        stream.sync()
+        for size in LADDER:
+            for _ in range(args.lat_n):
+                node.send_output_device_bytes("latency", ladder_bufs[size].ptr, size,
+                                              {"seq": seq, "t_start": time.time_ns()})
+                seq += 1
+                time.sleep(args.lat_gap_us / 1e6)
+        node.send_output("throughput", b"", {"seq": seq, "ack": True})
+        wait_ack(seq)
+        seq += 1
+        for b in ladder_bufs.values():
+            b.free()
+
+    # ---- timed region: K back-to-back steps, closed by the sink's ack ----
+    node.set_profiling(True)
+    barrier()
+    device.set_device(local_rank)
+    from dora_amd._lib import call
+    call("dora_gpu_device_sync")
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S,
+                                      {"seq": seq, "t_start": time.time_ns()})
+        seq += 1
+    node.send_output("throughput", b"", {"seq": seq, "ack": True})
+    wait_ack(seq)
+    call("dora_gpu_device_sync")
+    elapsed = time.perf_counter() - t0
+    barrier()
+    pack = node.pack_stats()
+    stats = node.stats()
+    node.close()
+    codes = df.wait(120)
+    df.stop()
+    sink = json.load(open(result_path)) if os.path.exists(result_path) else {"series": []}
+
+    t_max = max_over_ranks(elapsed)
+    total_bytes = sum_over_ranks(float(args.steps * S))
+    value = total_bytes / t_max / 1e9
+    avg_pack_ms = pack["total_ms"] / max(pack["count"], 1)
+    achieved = 2.0 * S / (avg_pack_ms * 1e-3) / 1e9 if pack["count"] else 0.0
+
+    if rank != 0:
+        return
+    lat = {}
+    for s in sink.get("series", []):
+        if s["input"] == "latency":
+            lat[str(s["size"])] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
+                                   "p50_incl_pack_us": s["full_p50_us"],
+                                   "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
+    verified = sum(s["verified"] for s in sink.get("series", []))
+    mismatches = sum(s["mismatches"] for s in sink.get("series", []))
+    line = {
+        "metric": "node->node GB/s (40,960,000 B UInt8 samples) + p50/p99 latency per msg size",
+        "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 payloads, seed 0xD05A + size)",
+        "config": {"workload": "C2: examples/benchmark node->sink edge, device-resident UInt8 "
+                               "samples, 1 node + 1 sink per GPU",
+                   "msg_bytes": S, "parallelism": f"dp{world} (one dataflow per GPU)",
+                   "sources_rotated": nsrc},
+        "latency_us": lat,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": None, "kernel": "pack_kernel",
+                     "avg_kernel_us": round(avg_pack_ms * 1e3, 3),
+                     "algorithmic_bytes_per_launch": 2 * S},
+        "parity": {"verified_msgs": verified, "mismatches": mismatches},
+        "node_stats": stats, "exit_codes": codes,
+    }
+    if base is not None:
+        tp = [s for s in base["series"] if s["mode"] == "throughput" and s["size"] == 40960000]
+        line["cpu_baseline"] = {
+            "value": tp[0]["GBps"] if tp else None, "unit": "GB/s", "cores": 3, "kind": "port",
+            "sample": "reference shm path restated in C++ (sender/daemon/sink pinned to 3 cores,"
+                      " TCP control, F8 daemon copy): 20 latency + 40 throughput msgs per size "
+                      "in {4096, 40960, 409600, 4096000, 40960000}",
+            "latency_us": {str(s["size"]): {"p50_us": s["p50_us"], "p99_us": s["p99_us"]}
+                           for s in base["series"] if s["mode"] == "latency"},
+            "wall_s": base["wall_s"], "nproc": base["nproc"], "cores_used": base["cores"]}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -7,8 +7,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, c_char_p, c_float, c_int, c_int32, c_size_t, c_uint8, c_uint64,
-                    c_void_p)
+from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t,
+                    c_uint8, c_uint64, c_void_p)
 
 from .arrow_c import ArrowArray, ArrowSchema
 
@@ -79,6 +79,44 @@ _SIGS = {
     "dora_gpu_csum64": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
     "dora_gpu_csum64_sync": (c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_uint64)]),
     "dora_gpu_fill_splitmix": (c_int, [c_void_p, c_size_t, c_uint64, c_void_p]),
+    # node API
+    "dora_node_init": (c_int, [c_char_p, c_char_p, c_int, POINTER(c_void_p)]),
+    "dora_node_init_from_env": (c_int, [POINTER(c_void_p)]),
+    "dora_node_free": (None, [c_void_p]),
+    "dora_node_stream": (c_void_p, [c_void_p]),
+    "dora_node_allocate_data_sample": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "dora_sample_data": (c_void_p, [c_void_p]),
+    "dora_sample_len": (c_size_t, [c_void_p]),
+    "dora_sample_discard": (None, [c_void_p, c_void_p]),
+    "dora_node_send_output_sample": (c_int, [c_void_p, c_char_p, POINTER(c_uint8), c_size_t,
+                                             POINTER(c_uint8), c_size_t, c_void_p]),
+    "dora_node_send_output": (c_int, [c_void_p, c_char_p, POINTER(ArrowArray),
+                                      POINTER(ArrowSchema), c_int32, POINTER(c_uint8), c_size_t]),
+    "dora_node_send_output_bytes": (c_int, [c_void_p, c_char_p, c_void_p, c_size_t, c_int32,
+                                            POINTER(c_uint8), c_size_t]),
+    "dora_node_close_outputs": (c_int, [c_void_p, POINTER(c_char_p), c_size_t]),
+    "dora_node_next_event": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
+    "dora_event_type": (c_int, [c_void_p]),
+    "dora_event_id": (c_char_p, [c_void_p]),
+    "dora_event_error": (c_char_p, [c_void_p]),
+    "dora_event_data": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
+    "dora_event_is_device": (c_int, [c_void_p]),
+    "dora_event_type_info": (c_int, [c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
+    "dora_event_parameters": (c_int, [c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
+    "dora_event_timestamp_ns": (c_uint64, [c_void_p]),
+    "dora_event_array": (c_int, [c_void_p, POINTER(ArrowArray), POINTER(ArrowSchema)]),
+    "dora_event_free": (None, [c_void_p]),
+    "dora_node_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                POINTER(c_uint64)]),
+    "dora_node_set_profiling": (c_int, [c_void_p, c_int]),
+    "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),
+                                     POINTER(c_uint64)]),
+    # daemon
+    "dora_daemon_create": (c_int, [c_char_p, c_char_p, c_size_t, POINTER(c_void_p)]),
+    "dora_daemon_run": (c_int, [c_void_p, c_int64]),
+    "dora_daemon_request_stop": (c_int, [c_void_p]),
+    "dora_daemon_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_daemon_free": (None, [c_void_p]),
 }
 
 _lib = None

@@ -18,7 +18,8 @@ INCLUDE = os.path.join(ROOT, "include")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
-LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip"]
+LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp",
+               "wire.cpp", "daemon.cpp", "node.cpp"]
 LIB_NAME = "libdora_gpu.so"
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
@@ -75,11 +76,10 @@ def build(verbose: bool = False) -> str:
     return out
 
 
-if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
-
-
-TOOLS = {}  # binary name -> list of sources (filled as native tools land)
+TOOLS = {  # binary name -> sources (linked against libdora_gpu.so, rpath $ORIGIN)
+    "dora-gpu-daemon": ["tools/daemon_main.cpp"],
+    "dora-gpu-bench-sink": ["tools/bench_sink.cpp"],
+}
 
 
 def build_tools(verbose: bool = False):
@@ -90,9 +90,14 @@ def build_tools(verbose: bool = False):
         exe = os.path.join(LIB, name)
         if _newer(exe, objs + [lib]):
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-o", exe, *objs, f"-L{LIB}", "-ldora_gpu",
-                   f"-Wl,-rpath,{LIB}", "-Wl,-rpath,$ORIGIN", "-lpthread", "-lrt"]
+                   "-Wl,-rpath,$ORIGIN", "-lpthread", "-lrt"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
         out.append(exe)
     return out
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))
+    print(build_tools(verbose="-v" in sys.argv))

@@ -1,0 +1,411 @@
+// Local daemon: routes sample descriptors and drop tokens between the nodes of one dataflow.
+//
+// Restates the reference daemon's data-plane duties (binaries/daemon/src/lib.rs):
+//   * send_out / send_output_to_local_receivers (:955-1003, :1314-1390): clone the Input event
+//     (id, metadata, data) to every mapped receiver and register the receiver as pending on the
+//     sample's drop token;
+//   * ReportDrop (:890-917) + check_drop_token (:1642-1672): when no receiver is pending any
+//     more, send NodeDropEvent::OutputDropped to the owner;
+//   * CloseOutputs / OutputsDone -> InputClosed / AllInputsClosed;
+//   * PendingNodes: nodes get Ready once every node of the dataflow has subscribed.
+// Unlike the reference (F8, lib.rs:1361-1376) it never opens or copies a sample: device samples
+// are routed as IPC handles, so the daemon touches no payload bytes at all.
+#include <signal.h>
+#include <sys/types.h>
+
+#include <cerrno>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <set>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "dora_gpu.h"
+#include "shm.h"
+#include "wire.h"
+
+namespace dora {
+namespace {
+
+struct Receiver {
+  int node;
+  std::string input;
+};
+
+struct DNode {
+  std::string id;
+  std::set<std::string> outputs;
+  std::map<std::string, uint32_t> queue_size;  // input -> queue size
+  std::set<std::string> open_inputs;
+  bool subscribed = false;
+  bool done = false;
+  bool all_closed_sent = false;
+  std::deque<std::pair<uint32_t, std::vector<uint8_t>>> ev_overflow;    // events not yet in ring
+  std::deque<std::vector<uint8_t>> drop_overflow;
+};
+
+struct TokenInfo {
+  int owner;
+  std::set<int> pending;
+};
+
+}  // namespace
+
+class Daemon {
+ public:
+  Daemon(const std::string& shm, const std::string& spec, uint64_t ring_cap) {
+    parse(spec);
+    std::vector<std::string> ids;
+    for (auto& n : nodes_) ids.push_back(n.id);
+    region_.reset(Region::create(shm, ids, ring_cap, "dataflow"));
+    for (size_t i = 0; i < nodes_.size(); ++i) {
+      NodeEntry& e = region_->hdr()->nodes[i];
+      std::string outs, ins;
+      for (auto& o : nodes_[i].outputs) outs += (outs.empty() ? "" : ",") + o;
+      for (auto& q : nodes_[i].queue_size)
+        ins += (ins.empty() ? "" : ",") + q.first + "=" + std::to_string(q.second);
+      if (outs.size() >= kListLen || ins.size() >= kListLen)
+        throw std::invalid_argument("too many inputs/outputs on node " + nodes_[i].id);
+      std::strncpy(e.outputs, outs.c_str(), kListLen - 1);
+      std::strncpy(e.inputs, ins.c_str(), kListLen - 1);
+      req_.emplace_back(region_.get(), &e.requests);
+      ev_.emplace_back(region_.get(), &e.events);
+      drop_.emplace_back(region_.get(), &e.drops);
+    }
+  }
+
+  // Returns 0 when every node is done, DORA_ERR_TIMEOUT after timeout_ms (<0: no timeout).
+  int run(int64_t timeout_ms) {
+    const uint64_t t0 = mono_ns();
+    uint64_t idle_since = mono_ns();
+    uint64_t last_liveness = 0;
+    std::vector<uint8_t> payload;
+    RegionHdr* h = region_->hdr();
+    for (;;) {
+      bool work = false;
+      for (size_t i = 0; i < nodes_.size(); ++i) {
+        uint32_t kind;
+        int budget = 64;
+        while (budget-- > 0 && req_[i].try_pop(&kind, &payload)) {
+          handle(static_cast<int>(i), kind, payload);
+          work = true;
+        }
+      }
+      work |= flush_overflow();
+      if (all_done()) return DORA_OK;
+      if (h->shutdown.load()) return DORA_ERR_CLOSED;
+      const uint64_t now = mono_ns();
+      if (timeout_ms >= 0 && int64_t(now - t0) / 1000000 > timeout_ms) return DORA_ERR_TIMEOUT;
+      if (now - last_liveness > 200000000ull) {  // 200 ms: reap nodes whose process died
+        check_liveness();
+        last_liveness = now;
+      }
+      if (work) {
+        idle_since = now;
+        continue;
+      }
+      if (int64_t(now - idle_since) / 1000 < spin_budget_us()) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      h->daemon_sleeping.store(1, std::memory_order_seq_cst);
+      const uint32_t bell = h->doorbell.load(std::memory_order_seq_cst);
+      bool empty = true;
+      for (auto& r : req_) empty &= r.empty();
+      if (empty) futex_wait(&h->doorbell, bell, 20000);
+      h->daemon_sleeping.store(0, std::memory_order_seq_cst);
+      idle_since = mono_ns();
+    }
+  }
+
+  void request_stop() {
+    for (size_t i = 0; i < nodes_.size(); ++i) push_event(static_cast<int>(i), EV_STOP, {});
+    flush_overflow();
+  }
+
+  uint64_t routed() const { return routed_; }
+  uint64_t pending_tokens() const { return tokens_.size(); }
+
+ private:
+  void parse(const std::string& spec) {
+    // Lines: "node <id>" | "output <node> <output>" |
+    //        "input <node> <input> <src_node> <src_output> <queue_size>"
+    std::istringstream in(spec);
+    std::string line;
+    std::map<std::string, int> idx;
+    struct In {
+      std::string node, input, src, out;
+      uint32_t q;
+    };
+    std::vector<In> inputs;
+    while (std::getline(in, line)) {
+      std::istringstream ls(line);
+      std::string kw;
+      if (!(ls >> kw) || kw[0] == '#') continue;
+      if (kw == "node") {
+        DNode n;
+        ls >> n.id;
+        if (n.id.empty() || idx.count(n.id)) throw std::invalid_argument("bad node line: " + line);
+        idx[n.id] = static_cast<int>(nodes_.size());
+        nodes_.push_back(n);
+      } else if (kw == "output") {
+        std::string node, out;
+        ls >> node >> out;
+        if (!idx.count(node)) throw std::invalid_argument("unknown node in: " + line);
+        nodes_[idx[node]].outputs.insert(out);
+      } else if (kw == "input") {
+        In x;
+        ls >> x.node >> x.input >> x.src >> x.out >> x.q;
+        if (ls.fail()) throw std::invalid_argument("bad input line: " + line);
+        inputs.push_back(x);
+      } else {
+        throw std::invalid_argument("unknown spec keyword: " + kw);
+      }
+    }
+    for (auto& x : inputs) {
+      if (!idx.count(x.node) || !idx.count(x.src))
+        throw std::invalid_argument("input refers to unknown node: " + x.node + "/" + x.input);
+      DNode& n = nodes_[idx[x.node]];
+      n.queue_size[x.input] = x.q;
+      n.open_inputs.insert(x.input);
+      if (!nodes_[idx[x.src]].outputs.count(x.out))
+        throw std::invalid_argument("input " + x.node + "/" + x.input + " maps unknown output " +
+                                    x.src + "/" + x.out);
+      mappings_[{idx[x.src], x.out}].push_back({idx[x.node], x.input});
+    }
+  }
+
+  bool all_done() const {
+    for (auto& n : nodes_)
+      if (!n.done) return false;
+    return !nodes_.empty();
+  }
+
+  void push_event(int node, uint32_t kind, std::vector<uint8_t> payload) {
+    DNode& n = nodes_[node];
+    if (n.done) return;
+    if (n.ev_overflow.empty() && ev_[node].try_push(kind, payload.data(), payload.size())) return;
+    n.ev_overflow.emplace_back(kind, std::move(payload));
+  }
+
+  void push_drop(int node, const DropToken& t) {
+    DNode& n = nodes_[node];
+    if (n.done) return;
+    WBuf w;
+    w.token(t);
+    if (n.drop_overflow.empty() && drop_[node].try_push(DROP_OUTPUT_DROPPED, w.b.data(), w.b.size()))
+      return;
+    n.drop_overflow.push_back(std::move(w.b));
+  }
+
+  bool flush_overflow() {
+    bool any = false;
+    for (size_t i = 0; i < nodes_.size(); ++i) {
+      DNode& n = nodes_[i];
+      while (!n.ev_overflow.empty()) {
+        auto& f = n.ev_overflow.front();
+        if (!ev_[i].try_push(f.first, f.second.data(), f.second.size())) break;
+        n.ev_overflow.pop_front();
+        any = true;
+      }
+      while (!n.drop_overflow.empty()) {
+        auto& f = n.drop_overflow.front();
+        if (!drop_[i].try_push(DROP_OUTPUT_DROPPED, f.data(), f.size())) break;
+        n.drop_overflow.pop_front();
+        any = true;
+      }
+    }
+    return any;
+  }
+
+  void handle(int i, uint32_t kind, const std::vector<uint8_t>& payload) {
+    RBuf r(payload);
+    switch (kind) {
+      case REQ_SUBSCRIBE:
+        nodes_[i].subscribed = true;
+        region_->hdr()->nodes[i].state.store(1);
+        if (ready_sent_) {
+          push_event(i, EV_READY, {});
+        } else {
+          bool all = true;
+          for (auto& n : nodes_) all &= n.subscribed || n.done;
+          if (all) {
+            ready_sent_ = true;
+            for (size_t k = 0; k < nodes_.size(); ++k) push_event(static_cast<int>(k), EV_READY, {});
+          }
+        }
+        break;
+      case REQ_SEND_MESSAGE: {
+        const std::string output = r.str();
+        const size_t meta_start = r.pos();
+        const std::vector<uint8_t> meta = r.bytes();
+        (void)meta_start;
+        const DataMsg data = r.data();
+        send_out(i, output, meta, data);
+        break;
+      }
+      case REQ_REPORT_DROP_TOKENS: {
+        const uint32_t n = r.u32();
+        for (uint32_t k = 0; k < n; ++k) {
+          const DropToken t = r.token();
+          auto it = tokens_.find(t);
+          if (it == tokens_.end()) continue;  // unknown drop token (warned in the reference)
+          if (it->second.pending.erase(i)) check_drop_token(t);
+        }
+        break;
+      }
+      case REQ_CLOSE_OUTPUTS: {
+        const uint32_t n = r.u32();
+        for (uint32_t k = 0; k < n; ++k) close_output(i, r.str());
+        break;
+      }
+      case REQ_OUTPUTS_DONE:
+        node_done(i);
+        break;
+      default:
+        break;
+    }
+  }
+
+  // send_output_to_local_receivers (lib.rs:1314-1390), minus the F8 payload copy.
+  void send_out(int i, const std::string& output, const std::vector<uint8_t>& meta,
+                const DataMsg& data) {
+    auto it = mappings_.find({i, output});
+    ++routed_;
+    if (it != mappings_.end()) {
+      for (const Receiver& rc : it->second) {
+        DNode& rn = nodes_[rc.node];
+        if (!rn.subscribed || rn.done || !rn.open_inputs.count(rc.input)) continue;
+        WBuf w;
+        w.str(rc.input);
+        w.bytes(meta);
+        w.data(data);
+        push_event(rc.node, EV_INPUT, std::move(w.b));
+        if (data.has_token()) {
+          auto& ti = tokens_[data.ipc.token];
+          ti.owner = i;
+          ti.pending.insert(rc.node);
+        }
+      }
+    }
+    if (data.has_token()) {
+      auto& ti = tokens_[data.ipc.token];  // inserted even with no local receivers
+      ti.owner = i;
+      check_drop_token(data.ipc.token);
+    }
+  }
+
+  void check_drop_token(const DropToken& t) {
+    auto it = tokens_.find(t);
+    if (it == tokens_.end() || !it->second.pending.empty()) return;
+    const int owner = it->second.owner;
+    tokens_.erase(it);
+    push_drop(owner, t);
+  }
+
+  void close_output(int i, const std::string& output) {
+    if (!nodes_[i].outputs.erase(output)) return;
+    auto it = mappings_.find({i, output});
+    if (it == mappings_.end()) return;
+    for (const Receiver& rc : it->second) {
+      DNode& rn = nodes_[rc.node];
+      if (!rn.open_inputs.erase(rc.input)) continue;
+      WBuf w;
+      w.str(rc.input);
+      push_event(rc.node, EV_INPUT_CLOSED, std::move(w.b));
+      if (rn.open_inputs.empty() && !rn.all_closed_sent) {
+        rn.all_closed_sent = true;
+        push_event(rc.node, EV_ALL_INPUTS_CLOSED, {});
+      }
+    }
+  }
+
+  void node_done(int i) {
+    std::vector<std::string> outs(nodes_[i].outputs.begin(), nodes_[i].outputs.end());
+    for (auto& o : outs) close_output(i, o);
+    nodes_[i].done = true;
+    nodes_[i].ev_overflow.clear();
+    nodes_[i].drop_overflow.clear();
+    region_->hdr()->nodes[i].state.store(2);
+    // a finished receiver holds nothing any more: release its pending tokens
+    std::vector<DropToken> touched;
+    for (auto& kv : tokens_)
+      if (kv.second.pending.erase(i)) touched.push_back(kv.first);
+    for (auto& t : touched) check_drop_token(t);
+    if (!ready_sent_) {  // a node that exits before subscribing must not stall the others
+      bool all = true;
+      for (auto& n : nodes_) all &= n.subscribed || n.done;
+      if (all) {
+        ready_sent_ = true;
+        for (size_t k = 0; k < nodes_.size(); ++k) push_event(static_cast<int>(k), EV_READY, {});
+      }
+    }
+  }
+
+  void check_liveness() {
+    for (size_t i = 0; i < nodes_.size(); ++i) {
+      if (nodes_[i].done) continue;
+      const int32_t pid = region_->hdr()->nodes[i].pid.load();
+      if (pid > 0 && kill(pid, 0) != 0 && errno == ESRCH) node_done(static_cast<int>(i));
+    }
+  }
+
+  std::unique_ptr<Region> region_;
+  std::vector<DNode> nodes_;
+  std::map<std::pair<int, std::string>, std::vector<Receiver>> mappings_;
+  std::unordered_map<DropToken, TokenInfo, DropTokenHash> tokens_;
+  std::vector<RingReader> req_;
+  std::vector<RingWriter> ev_, drop_;
+  bool ready_sent_ = false;
+  uint64_t routed_ = 0;
+};
+
+}  // namespace dora
+
+struct dora_daemon {
+  std::unique_ptr<dora::Daemon> d;
+};
+
+extern "C" {
+
+int dora_daemon_create(const char* shm_name, const char* spec, size_t ring_bytes,
+                       dora_daemon** out) {
+  if (!shm_name || !spec || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  auto* d = new dora_daemon();
+  d->d.reset(new dora::Daemon(shm_name, spec, ring_bytes ? ring_bytes : (4u << 20)));
+  *out = d;
+  return DORA_OK;
+  DORA_GUARD_END
+}
+
+int dora_daemon_run(dora_daemon* d, int64_t timeout_ms) {
+  if (!d) return dora::fail(DORA_ERR_INVALID, "NULL daemon");
+  DORA_GUARD_BEGIN
+  int rc = d->d->run(timeout_ms);
+  if (rc == DORA_ERR_TIMEOUT) return dora::fail(rc, "daemon run timed out");
+  return rc;
+  DORA_GUARD_END
+}
+
+int dora_daemon_request_stop(dora_daemon* d) {
+  if (!d) return dora::fail(DORA_ERR_INVALID, "NULL daemon");
+  d->d->request_stop();
+  return DORA_OK;
+}
+
+int dora_daemon_stats(dora_daemon* d, uint64_t* routed, uint64_t* pending_tokens) {
+  if (!d) return dora::fail(DORA_ERR_INVALID, "NULL daemon");
+  if (routed) *routed = d->d->routed();
+  if (pending_tokens) *pending_tokens = d->d->pending_tokens();
+  return DORA_OK;
+}
+
+void dora_daemon_free(dora_daemon* d) { delete d; }
+
+}  // extern "C"

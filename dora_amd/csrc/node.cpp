@@ -1,0 +1,762 @@
+// Node API of the device data plane — the MI355X counterpart of `DoraNode` + `EventStream`
+// (apis/rust/node/src/node/mod.rs:42-503, apis/rust/node/src/event_stream/*).
+//
+// Sender (mod.rs:180-275, 303-371):
+//   allocate_data_sample -> a device slot (hipMalloc, exported once with hipIpcGetMemHandle),
+//   best-fit from a 20-entry cache of recycled slots exactly like `allocate_shared_memory`;
+//   send_output -> plan + HIP pack kernel into the slot on the node's stream; the timestamp is
+//   taken after the fill (mod.rs:258); the slot is kept in `sent_out` until its drop token
+//   returns (mod.rs:269-272, 348-371).
+// Receiver (event_stream/mod.rs:121-198, event.rs:35-126):
+//   events are drained from the node's ring into a local queue with the daemon Listener's
+//   drop-oldest-per-input policy (node_communication/mod.rs:320-359); a DeviceIpc sample is
+//   mapped with hipIpcOpenMemHandle once per slot and cached (never per message); the drop token
+//   is reported when the last reference to the input data is released, after the node's stream
+//   has drained, so the owner can reuse the slot.
+#include <hip/hip_runtime_api.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "device_array.h"
+#include "dora_gpu.h"
+#include "plan.h"
+#include "shm.h"
+#include "wire.h"
+
+namespace dora {
+
+int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
+                hipStream_t stream);
+
+namespace {
+
+constexpr size_t kMaxCacheSize = 20;          // mod.rs:365
+constexpr uint64_t kDropWaitNs = 10000000000;  // 10 s per token on drop (mod.rs:397-426)
+
+struct Slot {
+  void* ptr = nullptr;
+  uint64_t cap = 0;  // requested length (cache best-fit key, like Shmem::len)
+  uint64_t id = 0;
+  hipIpcMemHandle_t handle;
+};
+
+std::vector<std::string> split(const char* s, char sep) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (const char* p = s; *p; ++p) {
+    if (*p == sep) {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += *p;
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
+}
+
+}  // namespace
+
+// State shared between the node handle and input data that may outlive events.
+struct NodeCore {
+  std::unique_ptr<Region> region;
+  int idx = -1;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  RingWriter req;
+  RingReader ev;
+  RingReader drops;
+  std::mutex req_mu;
+  std::mutex ipc_mu;
+  std::unordered_map<std::string, void*> ipc_cache;  // handle bytes -> mapped base
+  std::unordered_map<uint64_t, Slot*> own_slots;       // for self-delivery
+  std::mutex own_mu;
+
+  void ring_doorbell() {
+    RegionHdr* h = region->hdr();
+    h->doorbell.fetch_add(1, std::memory_order_seq_cst);
+    if (h->daemon_sleeping.load(std::memory_order_seq_cst)) futex_wake(&h->doorbell);
+  }
+
+  int request(uint32_t kind, const std::vector<uint8_t>& payload) {
+    {
+      std::lock_guard<std::mutex> g(req_mu);
+      if (!req.fits(payload.size()))
+        return fail(DORA_ERR_INVALID, "message of %zu bytes exceeds the control ring",
+                    payload.size());
+      if (!req.push(kind, payload.data(), payload.size(), 30000000))
+        return fail(DORA_ERR_TIMEOUT, "daemon did not drain the request ring for 30 s");
+    }
+    ring_doorbell();
+    return DORA_OK;
+  }
+
+  void report_drop_token(const DropToken& t) {
+    WBuf w;
+    w.u32(1);
+    w.token(t);
+    (void)request(REQ_REPORT_DROP_TOKENS, w.b);
+  }
+
+  ~NodeCore() {
+    for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// The received sample of one input; reports the drop token when the last owner releases it.
+struct InputData {
+  std::shared_ptr<NodeCore> core;
+  const void* ptr = nullptr;
+  uint64_t len = 0;
+  bool has_token = false;
+  DropToken token{};
+  std::vector<uint8_t> vec;  // inline (Vec) samples stay on the host
+  ~InputData() {
+    if (has_token && core) {
+      // consumer reads on the node stream must be complete before the owner may reuse the slot
+      if (core->stream) (void)hipStreamSynchronize(core->stream);
+      core->report_drop_token(token);
+    }
+  }
+};
+
+}  // namespace dora
+
+struct dora_sample {
+  dora::Slot* slot = nullptr;
+  std::vector<uint8_t> vec;  // zero-length samples (Vec path)
+  uint64_t len = 0;
+};
+
+struct dora_event {
+  int type = 0;
+  std::string id;
+  dora::Metadata meta;
+  std::shared_ptr<dora::InputData> data;
+  std::string error;
+};
+
+struct dora_node {
+  std::shared_ptr<dora::NodeCore> core;
+  std::string id;
+  std::set<std::string> outputs;
+  std::map<std::string, uint32_t> queue_size;
+  std::deque<dora::Slot*> cache;
+  std::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out;
+  uint64_t next_slot_id = 1;
+  std::deque<std::unique_ptr<dora_event>> queue;
+  bool ended = false;
+  // profiling of the pack kernel on the node stream
+  bool profile = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint64_t pack_count = 0, pack_bytes = 0;
+  double pack_ms = 0;
+  uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
+};
+
+namespace dora {
+namespace {
+
+void free_slot(Slot* s) {
+  if (!s) return;
+  (void)hipFree(s->ptr);
+  delete s;
+}
+
+void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
+  n->cache.push_back(s);
+  while (n->cache.size() > kMaxCacheSize) {
+    Slot* old = n->cache.front();
+    n->cache.pop_front();
+    {
+      std::lock_guard<std::mutex> g(n->core->own_mu);
+      n->core->own_slots.erase(old->id);
+    }
+    free_slot(old);
+  }
+}
+
+void on_token(dora_node* n, const DropToken& t) {
+  auto it = n->sent_out.find(t);
+  if (it == n->sent_out.end()) return;  // "received unknown finished drop token"
+  Slot* s = it->second;
+  n->sent_out.erase(it);
+  add_to_cache(n, s);
+}
+
+int handle_finished_drop_tokens(dora_node* n) {  // mod.rs:348-362
+  uint32_t kind;
+  std::vector<uint8_t> p;
+  while (n->core->drops.try_pop(&kind, &p)) {
+    if (kind != DROP_OUTPUT_DROPPED) continue;
+    RBuf r(p);
+    on_token(n, r.token());
+  }
+  return DORA_OK;
+}
+
+int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
+  // best fit among cached slots, iterating newest-first like `.rev()...min_by_key`
+  int best = -1;
+  for (int i = static_cast<int>(n->cache.size()) - 1; i >= 0; --i) {
+    Slot* s = n->cache[static_cast<size_t>(i)];
+    if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) best = i;
+  }
+  if (best >= 0) {
+    *out = n->cache[static_cast<size_t>(best)];
+    n->cache.erase(n->cache.begin() + best);
+    ++n->cache_hits;
+    return DORA_OK;
+  }
+  auto* s = new Slot();
+  s->cap = len;
+  s->id = n->next_slot_id++;
+  hipError_t e = hipMalloc(&s->ptr, (len + 4095) / 4096 * 4096);
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
+  if (e != hipSuccess) {
+    if (s->ptr) (void)hipFree(s->ptr);
+    delete s;
+    return fail(DORA_ERR_HIP, "device slot of %llu bytes: %s", (unsigned long long)len,
+                hipGetErrorString(e));
+  }
+  {
+    std::lock_guard<std::mutex> g(n->core->own_mu);
+    n->core->own_slots[s->id] = s;
+  }
+  ++n->slots_created;
+  *out = s;
+  return DORA_OK;
+}
+
+void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
+  auto ev = std::make_unique<dora_event>();
+  RBuf r(p);
+  switch (kind) {
+    case EV_INPUT: {
+      ev->type = DORA_EVENT_INPUT;
+      ev->id = r.str();
+      std::vector<uint8_t> meta = r.bytes();
+      RBuf mr(meta);
+      ev->meta = mr.metadata();
+      DataMsg d = r.data();
+      auto in = std::make_shared<InputData>();
+      in->core = n->core;
+      if (d.kind == DATA_VEC) {
+        in->vec = std::move(d.vec);
+        in->ptr = in->vec.data();
+        in->len = in->vec.size();
+      } else if (d.kind == DATA_DEVICE_IPC) {
+        in->has_token = true;  // set first: a mapping failure still returns the token
+        in->token = d.ipc.token;
+        in->len = d.ipc.len;
+        void* base = nullptr;
+        if (d.ipc.owner_pid == getpid()) {
+          std::lock_guard<std::mutex> g(n->core->own_mu);
+          auto it = n->core->own_slots.find(d.ipc.slot_id);
+          if (it != n->core->own_slots.end()) base = it->second->ptr;
+        } else {
+          std::string key(reinterpret_cast<const char*>(d.ipc.handle), 64);
+          std::lock_guard<std::mutex> g(n->core->ipc_mu);
+          auto it = n->core->ipc_cache.find(key);
+          if (it != n->core->ipc_cache.end()) {
+            base = it->second;
+          } else {
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, d.ipc.handle, sizeof(h));
+            hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+              ev->type = DORA_EVENT_ERROR;
+              ev->error = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e);
+              base = nullptr;
+            } else {
+              n->core->ipc_cache[key] = base;
+            }
+          }
+        }
+        if (base) in->ptr = static_cast<uint8_t*>(base) + d.ipc.offset;
+      }
+      ev->data = std::move(in);
+      break;
+    }
+    case EV_INPUT_CLOSED:
+      ev->type = DORA_EVENT_INPUT_CLOSED;
+      ev->id = r.str();
+      break;
+    case EV_ALL_INPUTS_CLOSED:
+      ev->type = DORA_EVENT_ALL_INPUTS_CLOSED;
+      break;
+    case EV_STOP:
+      ev->type = DORA_EVENT_STOP;
+      break;
+    default:
+      return;  // EV_READY after init is ignored
+  }
+  n->queue.push_back(std::move(ev));
+}
+
+// drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
+void drop_oldest_inputs(dora_node* n) {
+  std::map<std::string, uint32_t> remaining = n->queue_size;
+  for (auto it = n->queue.rbegin(); it != n->queue.rend(); ++it) {
+    dora_event* e = it->get();
+    if (!e || e->type != DORA_EVENT_INPUT) continue;
+    auto q = remaining.find(e->id);
+    if (q == remaining.end()) continue;
+    if (q->second == 0) {
+      it->reset();  // releases the InputData -> drop token reported
+      ++n->dropped_inputs;
+    } else {
+      --q->second;
+    }
+  }
+  n->queue.erase(std::remove_if(n->queue.begin(), n->queue.end(),
+                                [](const std::unique_ptr<dora_event>& e) { return !e; }),
+                 n->queue.end());
+}
+
+void drain_events(dora_node* n) {
+  uint32_t kind;
+  std::vector<uint8_t> p;
+  bool got = false;
+  while (n->core->ev.try_pop(&kind, &p)) {
+    encode_event(n, kind, p);
+    got = true;
+  }
+  if (got) drop_oldest_inputs(n);
+}
+
+std::vector<uint8_t> encode_metadata(const std::vector<uint8_t>& ti, const uint8_t* params,
+                                     size_t params_len, uint64_t ts) {
+  Metadata m;
+  m.timestamp_ns = ts;
+  m.type_info = ti;
+  if (params && params_len) m.parameters.assign(params, params + params_len);
+  WBuf w;
+  w.metadata(m);
+  return w.b;
+}
+
+int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
+                const uint8_t* params, size_t params_len, dora_sample* sample) {
+  handle_finished_drop_tokens(n);
+  if (!n->outputs.count(output_id)) {
+    delete sample;  // the sample is consumed either way
+    return fail(DORA_ERR_NOT_FOUND,
+                "unknown dora node output `%s` called by `send_output`. Double-check if this "
+                "output is defined within your dataflow YAML file.",
+                output_id);
+  }
+  const uint64_t ts = now_ns();  // Metadata::from_parameters(clock.new_timestamp(), ..) mod.rs:258
+  DataMsg d;
+  Slot* slot = nullptr;
+  if (sample) {
+    if (sample->slot) {
+      slot = sample->slot;
+      d.kind = DATA_DEVICE_IPC;
+      std::memcpy(d.ipc.handle, &slot->handle, 64);
+      d.ipc.device = n->core->device;
+      d.ipc.owner_pid = getpid();
+      d.ipc.slot_id = slot->id;
+      d.ipc.offset = 0;
+      d.ipc.len = sample->len;
+      d.ipc.token = generate_drop_token();
+    } else {
+      d.kind = DATA_VEC;
+      d.vec = std::move(sample->vec);
+    }
+    delete sample;
+  }
+  WBuf w;
+  w.str(output_id);
+  w.bytes(encode_metadata(ti, params, params_len, ts));
+  w.data(d);
+  int rc = n->core->request(REQ_SEND_MESSAGE, w.b);
+  if (rc != DORA_OK) {
+    if (slot) add_to_cache(n, slot);
+    return rc;
+  }
+  if (slot) n->sent_out[d.ipc.token] = slot;
+  return DORA_OK;
+}
+
+constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
+
+int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303-319
+  if (n->core->device < 0) {
+    // host-only node (no GPU): only the reference's inline `DataMessage::Vec` path exists
+    if (len >= kZeroCopyThreshold)
+      return fail(DORA_ERR_INVALID,
+                  "host-only node cannot allocate a %llu-byte sample: samples >= %llu bytes live "
+                  "in HBM slots",
+                  (unsigned long long)len, (unsigned long long)kZeroCopyThreshold);
+    auto* s = new dora_sample();
+    s->len = len;
+    s->vec.assign(len, 0);  // AVec::__from_elem(128, 0, len)
+    *out = s;
+    return DORA_OK;
+  }
+  auto* s = new dora_sample();
+  s->len = len;
+  if (len > 0) {
+    handle_finished_drop_tokens(n);
+    int rc = allocate_slot(n, len, &s->slot);
+    if (rc != DORA_OK) {
+      delete s;
+      return rc;
+    }
+  }
+  *out = s;
+  return DORA_OK;
+}
+
+int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
+                  size_t params_len) {
+  dora_sample* s = nullptr;
+  int rc = alloc_sample(n, plan->size, &s);
+  if (rc != DORA_OK) return rc;
+  if (plan->size && !s->slot) {
+    // host-only node: small host payload copied into the inline Vec (arrow_utils.rs:48)
+    if (plan->dev == ARROW_DEVICE_ROCM) {
+      delete s;
+      return fail(DORA_ERR_INVALID, "host-only node cannot send device-resident data");
+    }
+    for (const Segment& g : plan->segs) std::memcpy(s->vec.data() + g.dst_off, g.src, g.len);
+  } else if (plan->size) {
+    hipStream_t st = n->core->stream;
+    if (n->profile) (void)hipEventRecord(n->ev0, st);
+    rc = launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
+                     static_cast<uint8_t*>(s->slot->ptr), st);
+    if (n->profile) (void)hipEventRecord(n->ev1, st);
+    if (rc != DORA_OK) {
+      add_to_cache(n, s->slot);
+      delete s;
+      return rc;
+    }
+    // the sample must be complete before its descriptor leaves the process
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      add_to_cache(n, s->slot);
+      delete s;
+      return fail(DORA_ERR_HIP, "pack: %s", hipGetErrorString(e));
+    }
+    if (n->profile) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, n->ev0, n->ev1) == hipSuccess) {
+        n->pack_ms += ms;
+        ++n->pack_count;
+        n->pack_bytes += plan->size;
+      }
+    }
+  }
+  std::vector<uint8_t> ti;
+  serialize_type_info(plan->root, ti);
+  return send_sample(n, output_id, ti, params, params_len, s);
+}
+
+}  // namespace
+}  // namespace dora
+
+extern "C" {
+
+int dora_node_init(const char* shm_name, const char* node_id, int device, dora_node** out) {
+  if (!shm_name || !node_id || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *out = nullptr;
+  DORA_GUARD_BEGIN
+  auto core = std::make_shared<dora::NodeCore>();
+  try {
+    core->region.reset(dora::Region::attach(shm_name));
+  } catch (const std::exception& e) {
+    return dora::fail(DORA_ERR_INVALID, "attach dataflow: %s", e.what());
+  }
+  core->idx = core->region->node_index(node_id);
+  if (core->idx < 0)
+    return dora::fail(DORA_ERR_NOT_FOUND, "node `%s` is not part of the dataflow", node_id);
+  dora::NodeEntry& e = core->region->hdr()->nodes[core->idx];
+  int32_t expected = 0;
+  if (!e.pid.compare_exchange_strong(expected, static_cast<int32_t>(getpid())))
+    return dora::fail(DORA_ERR_INVALID, "node `%s` is already running (pid %d)", node_id,
+                      expected);
+  core->req = dora::RingWriter(core->region.get(), &e.requests);
+  core->ev = dora::RingReader(core->region.get(), &e.events);
+  core->drops = dora::RingReader(core->region.get(), &e.drops);
+  core->device = device;
+  if (device >= 0) {  // device < 0: host-only node (control plane + inline Vec samples only)
+    DORA_HIP(hipSetDevice(device));
+    DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
+  }
+
+  auto* n = new dora_node();
+  n->core = core;
+  n->id = node_id;
+  for (auto& o : dora::split(e.outputs, ',')) n->outputs.insert(o);
+  for (auto& kv : dora::split(e.inputs, ',')) {
+    auto eq = kv.find('=');
+    n->queue_size[kv.substr(0, eq)] = static_cast<uint32_t>(std::stoul(kv.substr(eq + 1)));
+  }
+  const char* prof = std::getenv("DORA_GPU_PROFILE_PACK");
+  if (prof && *prof && *prof != '0') {
+    n->profile = true;
+    (void)hipEventCreate(&n->ev0);
+    (void)hipEventCreate(&n->ev1);
+  }
+  // Subscribe and wait for AllNodesReady (event_stream/mod.rs:37-118, daemon PendingNodes)
+  int rc = core->request(dora::REQ_SUBSCRIBE, {});
+  if (rc != DORA_OK) {
+    delete n;
+    return rc;
+  }
+  const uint64_t t0 = dora::mono_ns();
+  for (;;) {
+    uint32_t kind;
+    std::vector<uint8_t> p;
+    if (core->ev.try_pop(&kind, &p)) {
+      if (kind == dora::EV_READY) break;
+      dora::encode_event(n, kind, p);
+      continue;
+    }
+    if (dora::mono_ns() - t0 > 60000000000ull) {
+      delete n;
+      return dora::fail(DORA_ERR_TIMEOUT, "no AllNodesReady from the daemon within 60 s");
+    }
+    core->ev.wait(100000);
+  }
+  *out = n;
+  return DORA_OK;
+  DORA_GUARD_END
+}
+
+int dora_node_init_from_env(dora_node** out) {
+  const char* shm = std::getenv("DORA_GPU_DATAFLOW");
+  const char* id = std::getenv("DORA_NODE_ID");
+  const char* dev = std::getenv("DORA_GPU_DEVICE");
+  if (!shm || !id)
+    return dora::fail(DORA_ERR_INVALID,
+                      "env variables DORA_GPU_DATAFLOW and DORA_NODE_ID must be set. Are you sure "
+                      "the node was started by the dataflow launcher?");
+  return dora_node_init(shm, id, dev ? std::atoi(dev) : 0, out);
+}
+
+void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
+  if (!n) return;
+  std::vector<std::string> outs(n->outputs.begin(), n->outputs.end());
+  dora::WBuf w;
+  w.u32(static_cast<uint32_t>(outs.size()));
+  for (auto& o : outs) w.str(o);
+  (void)n->core->request(dora::REQ_CLOSE_OUTPUTS, w.b);
+  n->queue.clear();  // releases undelivered inputs (tokens reported)
+  uint64_t t0 = dora::mono_ns();
+  while (!n->sent_out.empty()) {
+    dora::handle_finished_drop_tokens(n);
+    if (n->sent_out.empty()) break;
+    if (dora::mono_ns() - t0 > dora::kDropWaitNs) break;  // "timeout while waiting for drop tokens"
+    n->core->drops.wait(10000);
+    if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
+  }
+  (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
+  for (auto& kv : n->sent_out) dora::free_slot(kv.second);
+  for (auto* s : n->cache) dora::free_slot(s);
+  if (n->ev0) (void)hipEventDestroy(n->ev0);
+  if (n->ev1) (void)hipEventDestroy(n->ev1);
+  delete n;
+}
+
+dora_stream_t dora_node_stream(dora_node* n) { return n ? n->core->stream : nullptr; }
+
+int dora_node_allocate_data_sample(dora_node* n, size_t len, dora_sample** out) {
+  if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  return dora::alloc_sample(n, len, out);
+  DORA_GUARD_END
+}
+
+void* dora_sample_data(dora_sample* s) {
+  if (!s) return nullptr;
+  return s->slot ? s->slot->ptr : s->vec.data();
+}
+
+size_t dora_sample_len(const dora_sample* s) { return s ? s->len : 0; }
+
+void dora_sample_discard(dora_node* n, dora_sample* s) {
+  if (!s) return;
+  if (s->slot && n) dora::add_to_cache(n, s->slot);
+  delete s;
+}
+
+int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint8_t* type_info,
+                                 size_t type_info_len, const uint8_t* params, size_t params_len,
+                                 dora_sample* sample) {
+  if (!n || !output_id || (!type_info && type_info_len))
+    return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  std::vector<uint8_t> ti(type_info, type_info + type_info_len);
+  return dora::send_sample(n, output_id, ti, params, params_len, sample);
+  DORA_GUARD_END
+}
+
+int dora_node_send_output(dora_node* n, const char* output_id, const struct ArrowArray* array,
+                          const struct ArrowSchema* schema, ArrowDeviceType device_type,
+                          const uint8_t* params, size_t params_len) {
+  if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  dora_plan* plan = nullptr;
+  int rc = dora::build_plan(array, schema, device_type, &plan);
+  if (rc != DORA_OK) return rc;
+  rc = dora::pack_and_send(n, output_id, plan, params, params_len);
+  delete plan;
+  return rc;
+  DORA_GUARD_END
+}
+
+int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void* data, size_t len,
+                                ArrowDeviceType device_type, const uint8_t* params,
+                                size_t params_len) {
+  if (!n || !output_id || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  dora_plan plan;
+  plan.dev = device_type;
+  plan.size = len;
+  plan.root.sig = "C";
+  {
+    ArrowSchema u8{};
+    u8.format = "C";
+    dora::serialize_schema(&u8, true, plan.root.schema);
+  }
+  plan.root.len = len;
+  plan.root.bufs.push_back({0, len});
+  if (len) plan.segs.push_back({data, 0, len});
+  return dora::pack_and_send(n, output_id, &plan, params, params_len);
+  DORA_GUARD_END
+}
+
+int dora_node_close_outputs(dora_node* n, const char* const* ids, size_t count) {
+  if (!n || (!ids && count)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  for (size_t i = 0; i < count; ++i)
+    if (!n->outputs.count(ids[i])) return dora::fail(DORA_ERR_NOT_FOUND, "unknown output %s", ids[i]);
+  dora::WBuf w;
+  w.u32(static_cast<uint32_t>(count));
+  for (size_t i = 0; i < count; ++i) {
+    n->outputs.erase(ids[i]);
+    w.str(ids[i]);
+  }
+  return n->core->request(dora::REQ_CLOSE_OUTPUTS, w.b);
+  DORA_GUARD_END
+}
+
+int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
+  if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *out = nullptr;
+  DORA_GUARD_BEGIN
+  const uint64_t t0 = dora::mono_ns();
+  for (;;) {
+    dora::drain_events(n);
+    if (!n->queue.empty()) {
+      *out = n->queue.front().release();
+      n->queue.pop_front();
+      return DORA_OK;
+    }
+    if (n->ended) return dora::fail(DORA_ERR_CLOSED, "event stream closed");
+    int64_t left = -1;
+    if (timeout_us >= 0) {
+      left = timeout_us - int64_t(dora::mono_ns() - t0) / 1000;
+      if (left <= 0) return dora::fail(DORA_ERR_TIMEOUT, "no event within timeout");
+    }
+    n->core->ev.wait(left < 0 ? 1000000 : left);
+  }
+  DORA_GUARD_END
+}
+
+int dora_event_type(const dora_event* e) { return e ? e->type : DORA_EVENT_ERROR; }
+
+const char* dora_event_id(const dora_event* e) { return e ? e->id.c_str() : ""; }
+
+const char* dora_event_error(const dora_event* e) { return e ? e->error.c_str() : ""; }
+
+int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
+  if (!e || !ptr || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (!e->data) return dora::fail(DORA_ERR_INVALID, "event has no data");
+  *ptr = e->data->ptr;
+  *len = e->data->len;
+  return DORA_OK;
+}
+
+int dora_event_is_device(const dora_event* e) { return e && e->data && e->data->has_token; }
+
+int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
+  if (!e || !ti || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *ti = e->meta.type_info.data();
+  *len = e->meta.type_info.size();
+  return DORA_OK;
+}
+
+int dora_event_parameters(const dora_event* e, const uint8_t** p, size_t* len) {
+  if (!e || !p || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *p = e->meta.parameters.data();
+  *len = e->meta.parameters.size();
+  return DORA_OK;
+}
+
+uint64_t dora_event_timestamp_ns(const dora_event* e) { return e ? e->meta.timestamp_ns : 0; }
+
+int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
+                     struct ArrowSchema* out_schema) {
+  if (!e || !out_array || !out_schema) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (e->type != DORA_EVENT_INPUT || !e->data)
+    return dora::fail(DORA_ERR_INVALID, "not an input event");
+  if (!e->data->ptr && e->data->len)
+    return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", e->error.c_str());
+  if (!e->data->has_token && e->data->len)
+    return dora::fail(DORA_ERR_INVALID, "inline (host Vec) sample: read it with dora_event_data");
+  std::shared_ptr<void> keep = e->data;
+  return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
+                             e->meta.type_info.size(), keep, out_array, out_schema);
+}
+
+void dora_event_free(dora_event* e) { delete e; }
+
+int dora_node_stats(dora_node* n, uint64_t* slots_created, uint64_t* cache_hits,
+                    uint64_t* in_flight, uint64_t* dropped_inputs) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (slots_created) *slots_created = n->slots_created;
+  if (cache_hits) *cache_hits = n->cache_hits;
+  if (in_flight) *in_flight = n->sent_out.size();
+  if (dropped_inputs) *dropped_inputs = n->dropped_inputs;
+  return DORA_OK;
+}
+
+int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64_t* bytes) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (count) *count = n->pack_count;
+  if (total_ms) *total_ms = n->pack_ms;
+  if (bytes) *bytes = n->pack_bytes;
+  return DORA_OK;
+}
+
+int dora_node_set_profiling(dora_node* n, int enable) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (enable && !n->ev0) {
+    DORA_HIP(hipEventCreate(&n->ev0));
+    DORA_HIP(hipEventCreate(&n->ev1));
+  }
+  n->profile = enable != 0;
+  n->pack_count = 0;
+  n->pack_ms = 0;
+  n->pack_bytes = 0;
+  return DORA_OK;
+}
+
+}  // extern "C"

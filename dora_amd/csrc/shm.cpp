@@ -1,0 +1,262 @@
+// Shared-memory region + SPSC rings + futex waits (see shm.h).
+#include "shm.h"
+
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+
+namespace dora {
+
+namespace {
+constexpr uint32_t kPadKind = 0xFFFFFFFFu;
+constexpr uint64_t kPage = 4096;
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+void init_ring(RingHdr& h, uint64_t off, uint64_t cap) {
+  new (&h.head) std::atomic<uint64_t>(0);
+  new (&h.tail) std::atomic<uint64_t>(0);
+  new (&h.seq) std::atomic<uint32_t>(0);
+  new (&h.waiters) std::atomic<uint32_t>(0);
+  h.data_off = off;
+  h.cap = cap;
+}
+}  // namespace
+
+uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+int64_t spin_budget_us() {
+  static int64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_SPIN_US");
+    return e ? std::atoll(e) : int64_t(200);
+  }();
+  return v;
+}
+
+void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us) {
+  timespec ts, *tp = nullptr;
+  if (timeout_us >= 0) {
+    ts.tv_sec = timeout_us / 1000000;
+    ts.tv_nsec = (timeout_us % 1000000) * 1000;
+    tp = &ts;
+  }
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT, expected, tp, nullptr, 0);
+}
+
+void futex_wake(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+}
+
+Region::~Region() {
+  if (hdr_) munmap(hdr_, size_);
+  if (owner_) shm_unlink(name_.c_str());
+}
+
+void Region::unlink() {
+  if (owner_) {
+    shm_unlink(name_.c_str());
+    owner_ = false;
+  }
+}
+
+Region* Region::create(const std::string& name, const std::vector<std::string>& node_ids,
+                       uint64_t ring_cap, const std::string& dataflow_id) {
+  if (node_ids.size() > kMaxNodes) throw std::invalid_argument("too many nodes");
+  if (ring_cap < 4096 || (ring_cap & (ring_cap - 1)))
+    throw std::invalid_argument("ring capacity must be a power of two >= 4096");
+  const uint64_t hdr = round_up(sizeof(RegionHdr), kPage);
+  const uint64_t total = hdr + 3 * ring_cap * node_ids.size();
+  int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
+  if (ftruncate(fd, static_cast<off_t>(total)) != 0) {
+    close(fd);
+    shm_unlink(name.c_str());
+    throw std::runtime_error(std::string("ftruncate: ") + std::strerror(errno));
+  }
+  void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    shm_unlink(name.c_str());
+    throw std::runtime_error(std::string("mmap: ") + std::strerror(errno));
+  }
+  auto* r = new Region();
+  r->hdr_ = static_cast<RegionHdr*>(p);
+  r->size_ = total;
+  r->name_ = name;
+  r->owner_ = true;
+  RegionHdr* h = r->hdr_;
+  std::memset(static_cast<void*>(h), 0, sizeof(RegionHdr));
+  h->version = kRegionVersion;
+  h->n_nodes = static_cast<uint32_t>(node_ids.size());
+  h->ring_cap = ring_cap;
+  h->total_size = total;
+  new (&h->doorbell) std::atomic<uint32_t>(0);
+  new (&h->daemon_sleeping) std::atomic<uint32_t>(0);
+  new (&h->shutdown) std::atomic<uint32_t>(0);
+  std::strncpy(h->dataflow_id, dataflow_id.c_str(), kIdLen - 1);
+  uint64_t off = hdr;
+  for (size_t i = 0; i < node_ids.size(); ++i) {
+    NodeEntry& n = h->nodes[i];
+    std::strncpy(n.id, node_ids[i].c_str(), kIdLen - 1);
+    new (&n.pid) std::atomic<int32_t>(0);
+    new (&n.state) std::atomic<uint32_t>(0);
+    init_ring(n.requests, off, ring_cap);
+    off += ring_cap;
+    init_ring(n.events, off, ring_cap);
+    off += ring_cap;
+    init_ring(n.drops, off, ring_cap);
+    off += ring_cap;
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  h->magic = kRegionMagic;
+  return r;
+}
+
+Region* Region::attach(const std::string& name) {
+  int fd = shm_open(name.c_str(), O_RDWR, 0600);
+  if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    throw std::runtime_error("fstat failed");
+  }
+  void* p = mmap(nullptr, static_cast<size_t>(st.st_size), PROT_READ | PROT_WRITE, MAP_SHARED,
+                 fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error(std::string("mmap: ") + std::strerror(errno));
+  auto* r = new Region();
+  r->hdr_ = static_cast<RegionHdr*>(p);
+  r->size_ = static_cast<size_t>(st.st_size);
+  r->name_ = name;
+  if (r->hdr_->magic != kRegionMagic || r->hdr_->version != kRegionVersion) {
+    delete r;
+    throw std::runtime_error("shm region " + name + " is not a dora-gpu dataflow region");
+  }
+  return r;
+}
+
+int Region::node_index(const std::string& id) const {
+  for (uint32_t i = 0; i < hdr_->n_nodes; ++i)
+    if (id == hdr_->nodes[i].id) return static_cast<int>(i);
+  return -1;
+}
+
+// ------------------------------------------------------------------------------------------
+bool RingWriter::fits(size_t n) const {
+  const uint64_t rec = round_up(16 + n, 8);
+  return rec <= h_->cap / 2;
+}
+
+bool RingWriter::try_push(uint32_t kind, const uint8_t* payload, size_t n) {
+  const uint64_t cap = h_->cap;
+  const uint64_t rec = round_up(16 + n, 8);
+  if (rec > cap / 2) throw std::length_error("record larger than half the ring");
+  uint64_t head = h_->head.load(std::memory_order_relaxed);
+  const uint64_t tail = h_->tail.load(std::memory_order_acquire);
+  uint64_t off = head & (cap - 1);
+  uint64_t need = rec;
+  if (off + rec > cap) need += cap - off;
+  if (cap - (head - tail) < need) return false;
+  uint8_t* data = r_->base() + h_->data_off;
+  if (off + rec > cap) {
+    const uint32_t pad = static_cast<uint32_t>(cap - off);
+    std::memcpy(data + off, &pad, 4);
+    std::memcpy(data + off + 4, &kPadKind, 4);
+    head += pad;
+    off = 0;
+  }
+  const uint32_t len = static_cast<uint32_t>(rec);
+  std::memcpy(data + off, &len, 4);
+  std::memcpy(data + off + 4, &kind, 4);
+  const uint64_t n64 = n;
+  std::memcpy(data + off + 8, &n64, 8);
+  if (n) std::memcpy(data + off + 16, payload, n);
+  h_->head.store(head + rec, std::memory_order_release);
+  h_->seq.fetch_add(1, std::memory_order_seq_cst);
+  if (h_->waiters.load(std::memory_order_seq_cst)) futex_wake(&h_->seq);
+  return true;
+}
+
+bool RingWriter::push(uint32_t kind, const uint8_t* payload, size_t n, int64_t timeout_us) {
+  const uint64_t t0 = mono_ns();
+  unsigned backoff = 1;
+  while (!try_push(kind, payload, n)) {
+    if (timeout_us >= 0 && int64_t(mono_ns() - t0) / 1000 > timeout_us) return false;
+    usleep(backoff);
+    backoff = backoff < 200 ? backoff * 2 : 200;
+  }
+  return true;
+}
+
+bool RingReader::empty() const {
+  return h_->tail.load(std::memory_order_relaxed) == h_->head.load(std::memory_order_acquire);
+}
+
+bool RingReader::try_pop(uint32_t* kind, std::vector<uint8_t>* payload) {
+  const uint64_t cap = h_->cap;
+  uint8_t* data = r_->base() + h_->data_off;
+  for (;;) {
+    uint64_t tail = h_->tail.load(std::memory_order_relaxed);
+    const uint64_t head = h_->head.load(std::memory_order_acquire);
+    if (tail == head) return false;
+    const uint64_t off = tail & (cap - 1);
+    uint32_t len, k;
+    std::memcpy(&len, data + off, 4);
+    std::memcpy(&k, data + off + 4, 4);
+    if (k == kPadKind) {
+      h_->tail.store(tail + len, std::memory_order_release);
+      continue;
+    }
+    *kind = k;
+    uint64_t n;
+    std::memcpy(&n, data + off + 8, 8);
+    payload->assign(data + off + 16, data + off + 16 + n);
+    h_->tail.store(tail + len, std::memory_order_release);
+    return true;
+  }
+}
+
+bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag) {
+  const uint64_t t0 = mono_ns();
+  const int64_t spin = spin_budget_us();
+  while (empty()) {
+    const int64_t el = int64_t(mono_ns() - t0) / 1000;
+    if (timeout_us >= 0 && el >= timeout_us) return false;
+    if (abort_flag && abort_flag->load(std::memory_order_relaxed)) return false;
+    if (el < spin) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    h_->waiters.fetch_add(1, std::memory_order_seq_cst);
+    const uint32_t s = h_->seq.load(std::memory_order_seq_cst);
+    if (empty()) {
+      int64_t slice = 20000;  // re-check abort flags periodically
+      if (timeout_us >= 0) slice = std::min<int64_t>(slice, timeout_us - el);
+      if (slice > 0) futex_wait(&h_->seq, s, slice);
+    }
+    h_->waiters.fetch_sub(1, std::memory_order_seq_cst);
+  }
+  return true;
+}
+
+}  // namespace dora

@@ -1,0 +1,124 @@
+// Shared-memory control plane of a local dataflow: one POSIX shm region created by the daemon,
+// holding, per node, three single-producer/single-consumer byte rings:
+//   requests  node   -> daemon  (DaemonRequest: SendMessage, ReportDropTokens, CloseOutputs ...)
+//   events    daemon -> node    (NodeEvent: Input, InputClosed, AllInputsClosed, Stop, Ready)
+//   drops     daemon -> node    (NodeDropEvent::OutputDropped)
+// It replaces the reference's per-node TCP/UDS/4 KiB-shmem request-reply channels
+// (apis/rust/node/src/daemon_connection/*, binaries/daemon/src/node_communication/*,
+// libraries/shared-memory-server/src/channel.rs) with rings that never block the producer on a
+// reply (SendMessage expects no reply in the reference either, node_to_daemon.rs:36-41) and are
+// sized for the type info of large nested arrays (the 4 KiB mailbox limit, F5, is gone).
+// Waiting: spin for a bounded time, then futex-wait on a sequence word.
+#pragma once
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace dora {
+
+constexpr uint64_t kRegionMagic = 0x444f5241474d5358ull;  // "DORAGMSX"
+constexpr uint32_t kRegionVersion = 1;
+constexpr uint32_t kMaxNodes = 64;
+constexpr size_t kIdLen = 64;
+
+struct RingHdr {
+  alignas(64) std::atomic<uint64_t> head;  // bytes written (producer)
+  alignas(64) std::atomic<uint64_t> tail;  // bytes consumed (consumer)
+  alignas(64) std::atomic<uint32_t> seq;   // futex word, bumped on every publish
+  std::atomic<uint32_t> waiters;
+  uint64_t data_off;  // from region base
+  uint64_t cap;       // power of two
+};
+
+constexpr size_t kListLen = 2048;
+
+struct NodeEntry {
+  char id[kIdLen];
+  char outputs[kListLen];  // "out1,out2"           (NodeRunConfig.outputs)
+  char inputs[kListLen];   // "in1=10,in2=1"        (input id = queue_size)
+  std::atomic<int32_t> pid;
+  std::atomic<uint32_t> state;  // 0 idle, 1 subscribed, 2 done
+  RingHdr requests;
+  RingHdr events;
+  RingHdr drops;
+};
+
+struct RegionHdr {
+  uint64_t magic;
+  uint32_t version;
+  uint32_t n_nodes;
+  uint64_t ring_cap;
+  uint64_t total_size;
+  alignas(64) std::atomic<uint32_t> doorbell;  // futex word the daemon sleeps on
+  std::atomic<uint32_t> daemon_sleeping;
+  std::atomic<uint32_t> shutdown;
+  char dataflow_id[kIdLen];
+  NodeEntry nodes[kMaxNodes];
+};
+
+// A mapped region (creator or attacher).
+class Region {
+ public:
+  ~Region();
+  static Region* create(const std::string& name, const std::vector<std::string>& node_ids,
+                        uint64_t ring_cap, const std::string& dataflow_id);
+  static Region* attach(const std::string& name);
+  RegionHdr* hdr() const { return hdr_; }
+  uint8_t* base() const { return reinterpret_cast<uint8_t*>(hdr_); }
+  int node_index(const std::string& id) const;
+  void unlink();
+  const std::string& name() const { return name_; }
+
+ private:
+  Region() = default;
+  RegionHdr* hdr_ = nullptr;
+  size_t size_ = 0;
+  std::string name_;
+  bool owner_ = false;
+};
+
+// Producer / consumer views of one ring.  Records: [u32 rec_len][u32 kind][u64 n][payload],
+// 8-B aligned; a record of kind 0xFFFFFFFF pads to the end of the ring.
+class RingWriter {
+ public:
+  RingWriter() = default;
+  RingWriter(Region* r, RingHdr* h) : r_(r), h_(h) {}
+  // Publish one record; returns false if it does not fit right now (caller retries / queues).
+  bool try_push(uint32_t kind, const uint8_t* payload, size_t n);
+  // Blocking push (spins, then sleeps) until space is available or `timeout_us` elapses.
+  bool push(uint32_t kind, const uint8_t* payload, size_t n, int64_t timeout_us = -1);
+  bool fits(size_t n) const;
+  RingHdr* hdr() const { return h_; }
+
+ private:
+  Region* r_ = nullptr;
+  RingHdr* h_ = nullptr;
+};
+
+class RingReader {
+ public:
+  RingReader() = default;
+  RingReader(Region* r, RingHdr* h) : r_(r), h_(h) {}
+  // Pop one record into (kind, payload).  Returns false if empty.
+  bool try_pop(uint32_t* kind, std::vector<uint8_t>* payload);
+  // Wait until a record is available or timeout (us; <0 = forever).  Returns false on timeout.
+  bool wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag = nullptr);
+  bool empty() const;
+  RingHdr* hdr() const { return h_; }
+
+ private:
+  Region* r_ = nullptr;
+  RingHdr* h_ = nullptr;
+};
+
+// futex helpers on shared (non-private) words
+void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us);
+void futex_wake(std::atomic<uint32_t>* w);
+int64_t spin_budget_us();
+uint64_t now_ns();           // CLOCK_REALTIME (timestamps that cross processes)
+uint64_t mono_ns();          // CLOCK_MONOTONIC
+
+}  // namespace dora

@@ -1,0 +1,142 @@
+// dora-gpu-bench-sink: the benchmark sink (examples/benchmark/sink/src/main.rs:6-87) on the
+// device data plane.  For every input it records the latency from the sender's metadata
+// timestamp (taken after the sample is filled, node/mod.rs:258) and, when the sender passes a
+// `t_start` parameter, the latency including allocation + pack.  With `verify` it checksums the
+// received device sample (csum64 kernel) against the sender's `csum` parameter.  Inputs with an
+// `ack` parameter are acknowledged on the `ack` output (used by the bench to close a timed burst).
+// At the end of the stream it writes one JSON document with per-(input, size) statistics.
+//   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE, DORA_BENCH_RESULT (path)
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "dora_gpu.h"
+#include "params.h"
+
+namespace {
+
+struct Series {
+  std::vector<double> lat_us, full_us;
+  uint64_t first_ns = 0, last_ns = 0, n = 0, bytes = 0, verified = 0, mismatches = 0;
+};
+
+double pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  size_t k = static_cast<size_t>(p * (v.size() - 1) + 0.5);
+  return v[std::min(k, v.size() - 1)];
+}
+
+double mean(const std::vector<double>& v) {
+  double s = 0;
+  for (double x : v) s += x;
+  return v.empty() ? 0 : s / v.size();
+}
+
+uint64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+}  // namespace
+
+int main() {
+  dora_node* node = nullptr;
+  if (dora_node_init_from_env(&node) != 0) {
+    std::fprintf(stderr, "sink: init failed: %s\n", dora_gpu_last_error());
+    return 1;
+  }
+  const char* out_path = std::getenv("DORA_BENCH_RESULT");
+  std::map<std::pair<std::string, uint64_t>, Series> stats;
+  uint64_t csum_buf_dummy = 0;
+  (void)csum_buf_dummy;
+  uint64_t* csum_dev = nullptr;
+  dora_gpu_malloc(reinterpret_cast<void**>(&csum_dev), 8);
+  dora_stream_t st = dora_node_stream(node);
+  int errors = 0;
+  for (;;) {
+    dora_event* ev = nullptr;
+    int rc = dora_node_next_event(node, -1, &ev);
+    if (rc != 0) break;
+    const int type = dora_event_type(ev);
+    if (type == DORA_EVENT_INPUT) {
+      const uint64_t t = now_ns();
+      const void* p = nullptr;
+      size_t len = 0;
+      dora_event_data(ev, &p, &len);
+      const uint8_t* pp = nullptr;
+      size_t pl = 0;
+      dora_event_parameters(ev, &pp, &pl);
+      auto params = decode_params(pp, pl);
+      Series& s = stats[{dora_event_id(ev), len}];
+      const uint64_t ts = dora_event_timestamp_ns(ev);
+      s.lat_us.push_back((double(t) - double(ts)) / 1000.0);
+      if (params.count("t_start"))
+        s.full_us.push_back((double(t) - double(params["t_start"].i)) / 1000.0);
+      if (!s.first_ns) s.first_ns = t;
+      s.last_ns = t;
+      ++s.n;
+      s.bytes += len;
+      if (params.count("csum") && params.count("verify") && dora_event_is_device(ev)) {
+        uint64_t c = 0;
+        if (dora_gpu_csum64(p, len, csum_dev, st) == 0 &&
+            dora_gpu_memcpy_async(&c, csum_dev, 8, st) == 0 && dora_gpu_stream_sync(st) == 0) {
+          ++s.verified;
+          if (c != static_cast<uint64_t>(params["csum"].i)) ++s.mismatches;
+        } else {
+          ++errors;
+        }
+      }
+      const bool ack = params.count("ack") != 0;
+      const int64_t seq = params.count("seq") ? params["seq"].i : -1;
+      dora_event_free(ev);  // zero-copy consumer done: token goes back to the sender
+      if (ack) {
+        std::map<std::string, Param> ap;
+        ap["seq"].i = seq;
+        auto enc = encode_params(ap);
+        if (dora_node_send_output_bytes(node, "ack", nullptr, 0, ARROW_DEVICE_ROCM, enc.data(),
+                                        enc.size()) != 0) {
+          std::fprintf(stderr, "sink: ack failed: %s\n", dora_gpu_last_error());
+          ++errors;
+        }
+      }
+      continue;
+    }
+    const bool end = type == DORA_EVENT_ALL_INPUTS_CLOSED || type == DORA_EVENT_STOP;
+    if (type == DORA_EVENT_ERROR) {
+      std::fprintf(stderr, "sink: error event: %s\n", dora_event_error(ev));
+      ++errors;
+    }
+    dora_event_free(ev);
+    if (end) break;
+  }
+  uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
+  dora_node_stats(node, &slots, &hits, &inflight, &dropped);
+  FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
+  std::fprintf(f, "{\"errors\": %d, \"dropped_inputs\": %llu, \"series\": [", errors,
+               (unsigned long long)dropped);
+  bool first = true;
+  for (auto& kv : stats) {
+    Series& s = kv.second;
+    std::fprintf(f,
+                 "%s\n {\"input\": \"%s\", \"size\": %llu, \"n\": %llu, \"p50_us\": %.3f, "
+                 "\"p99_us\": %.3f, \"mean_us\": %.3f, \"min_us\": %.3f, \"full_p50_us\": %.3f, "
+                 "\"full_p99_us\": %.3f, \"first_ns\": %llu, \"last_ns\": %llu, \"verified\": "
+                 "%llu, \"mismatches\": %llu}",
+                 first ? "" : ",", kv.first.first.c_str(), (unsigned long long)kv.first.second,
+                 (unsigned long long)s.n, pct(s.lat_us, 0.5), pct(s.lat_us, 0.99), mean(s.lat_us),
+                 pct(s.lat_us, 0.0), pct(s.full_us, 0.5), pct(s.full_us, 0.99),
+                 (unsigned long long)s.first_ns, (unsigned long long)s.last_ns,
+                 (unsigned long long)s.verified, (unsigned long long)s.mismatches);
+    first = false;
+  }
+  std::fprintf(f, "\n]}\n");
+  if (f != stdout) std::fclose(f);
+  dora_gpu_free(csum_dev);
+  dora_node_free(node);
+  return errors ? 1 : 0;
+}

@@ -1,0 +1,64 @@
+// dora-gpu-daemon: runs the data-plane daemon of one local dataflow (the `dora daemon
+// --run-dataflow` role of binaries/cli/src/main.rs:468-499, data plane only).
+//   dora-gpu-daemon --shm /name --spec FILE [--ring-bytes N] [--timeout-ms T]
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#include "dora_gpu.h"
+
+static volatile sig_atomic_t g_stop = 0;
+static void on_signal(int) { g_stop = 1; }
+
+int main(int argc, char** argv) {
+  std::string shm, spec_file;
+  size_t ring = 4u << 20;
+  long long timeout_ms = -1;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+    if (a == "--shm") shm = next();
+    else if (a == "--spec") spec_file = next();
+    else if (a == "--ring-bytes") ring = std::strtoull(next(), nullptr, 10);
+    else if (a == "--timeout-ms") timeout_ms = std::atoll(next());
+  }
+  if (shm.empty() || spec_file.empty()) {
+    std::fprintf(stderr, "usage: dora-gpu-daemon --shm /name --spec FILE\n");
+    return 2;
+  }
+  std::ifstream f(spec_file);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  dora_daemon* d = nullptr;
+  if (dora_daemon_create(shm.c_str(), ss.str().c_str(), ring, &d) != 0) {
+    std::fprintf(stderr, "daemon: %s\n", dora_gpu_last_error());
+    return 1;
+  }
+  std::signal(SIGTERM, on_signal);
+  std::signal(SIGINT, on_signal);
+  std::printf("{\"daemon\": \"ready\", \"shm\": \"%s\"}\n", shm.c_str());
+  std::fflush(stdout);
+  int rc;
+  long long waited = 0;
+  bool stop_sent = false;
+  for (;;) {
+    rc = dora_daemon_run(d, 200);
+    if (rc != DORA_ERR_TIMEOUT) break;
+    waited += 200;
+    if (g_stop && !stop_sent) {  // ctrl-c: Event::Stop to every node, then keep routing
+      dora_daemon_request_stop(d);
+      stop_sent = true;
+    }
+    if (timeout_ms >= 0 && waited >= timeout_ms) break;
+  }
+  uint64_t routed = 0, pending = 0;
+  dora_daemon_stats(d, &routed, &pending);
+  std::printf("{\"daemon\": \"done\", \"rc\": %d, \"routed\": %llu, \"pending_tokens\": %llu}\n", rc,
+              (unsigned long long)routed, (unsigned long long)pending);
+  dora_daemon_free(d);
+  return rc == 0 ? 0 : 1;
+}

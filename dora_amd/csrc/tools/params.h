@@ -1,0 +1,79 @@
+// MetadataParameters encoding shared by the native tools (see include/dora_gpu.h).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+struct Param {
+  uint8_t tag = 1;  // 0 bool, 1 int, 2 string
+  int64_t i = 0;
+  std::string s;
+};
+
+inline std::vector<uint8_t> encode_params(const std::map<std::string, Param>& m) {
+  std::vector<uint8_t> o;
+  auto put = [&](const void* p, size_t n) {
+    const auto* c = static_cast<const uint8_t*>(p);
+    o.insert(o.end(), c, c + n);
+  };
+  uint32_t n = static_cast<uint32_t>(m.size());
+  put(&n, 4);
+  for (auto& kv : m) {
+    uint64_t kl = kv.first.size();
+    put(&kl, 8);
+    put(kv.first.data(), kl);
+    put(&kv.second.tag, 1);
+    if (kv.second.tag == 0) {
+      uint8_t b = kv.second.i ? 1 : 0;
+      put(&b, 1);
+    } else if (kv.second.tag == 1) {
+      put(&kv.second.i, 8);
+    } else {
+      uint64_t sl = kv.second.s.size();
+      put(&sl, 8);
+      put(kv.second.s.data(), sl);
+    }
+  }
+  return o;
+}
+
+inline std::map<std::string, Param> decode_params(const uint8_t* p, size_t n) {
+  std::map<std::string, Param> m;
+  size_t i = 0;
+  auto get = [&](void* d, size_t k) {
+    if (i + k > n) throw 1;
+    std::memcpy(d, p + i, k);
+    i += k;
+  };
+  try {
+    if (n < 4) return m;
+    uint32_t cnt;
+    get(&cnt, 4);
+    for (uint32_t c = 0; c < cnt; ++c) {
+      uint64_t kl;
+      get(&kl, 8);
+      std::string key(kl, '\0');
+      get(&key[0], kl);
+      Param v;
+      get(&v.tag, 1);
+      if (v.tag == 0) {
+        uint8_t b;
+        get(&b, 1);
+        v.i = b;
+      } else if (v.tag == 1) {
+        get(&v.i, 8);
+      } else {
+        uint64_t sl;
+        get(&sl, 8);
+        v.s.assign(sl, '\0');
+        get(&v.s[0], sl);
+      }
+      m[key] = v;
+    }
+  } catch (int) {
+  }
+  return m;
+}

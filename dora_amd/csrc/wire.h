@@ -1,0 +1,206 @@
+// Wire types of the data plane (little-endian, length-prefixed) — the MI355X counterparts of
+// libraries/message: DataMessage (common.rs:135-152) with a DeviceIpc variant, DropToken
+// (common.rs:175-184), Metadata (metadata.rs:9-34), DaemonRequest / NodeEvent / NodeDropEvent
+// (node_to_daemon.rs:9-69, daemon_to_node.rs:48-77).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace dora {
+
+struct DropToken {
+  uint8_t b[16];
+  bool operator==(const DropToken& o) const { return std::memcmp(b, o.b, 16) == 0; }
+  bool operator<(const DropToken& o) const { return std::memcmp(b, o.b, 16) < 0; }
+};
+struct DropTokenHash {
+  size_t operator()(const DropToken& t) const {
+    uint64_t a, c;
+    std::memcpy(&a, t.b, 8);
+    std::memcpy(&c, t.b + 8, 8);
+    return static_cast<size_t>(a * 0x9E3779B97F4A7C15ull ^ c);
+  }
+};
+DropToken generate_drop_token();  // UUIDv7 (common.rs:181-183)
+
+// Request kinds (node -> daemon), event kinds (daemon -> node), drop kinds.
+enum : uint32_t {
+  REQ_SUBSCRIBE = 1,
+  REQ_SEND_MESSAGE = 2,
+  REQ_REPORT_DROP_TOKENS = 3,
+  REQ_CLOSE_OUTPUTS = 4,
+  REQ_OUTPUTS_DONE = 5,
+  EV_READY = 101,
+  EV_INPUT = 102,
+  EV_INPUT_CLOSED = 103,
+  EV_ALL_INPUTS_CLOSED = 104,
+  EV_STOP = 105,
+  DROP_OUTPUT_DROPPED = 201,
+};
+
+enum : uint8_t { DATA_NONE = 0, DATA_VEC = 1, DATA_DEVICE_IPC = 2 };
+
+// DataMessage::DeviceIpc — the sample lives in an exported hipMalloc slot of `owner_pid`.
+struct DeviceIpc {
+  uint8_t handle[64];  // hipIpcMemHandle_t of the slot allocation
+  int32_t device;      // GPU ordinal of the slot
+  int32_t owner_pid;
+  uint64_t slot_id;    // unique per owner process
+  uint64_t offset;     // sample offset inside the slot allocation
+  uint64_t len;
+  DropToken token;
+};
+
+struct DataMsg {
+  uint8_t kind = DATA_NONE;
+  std::vector<uint8_t> vec;  // DATA_VEC
+  DeviceIpc ipc{};           // DATA_DEVICE_IPC
+  bool has_token() const { return kind == DATA_DEVICE_IPC; }
+};
+
+struct Metadata {
+  uint16_t version = 0;
+  uint64_t timestamp_ns = 0;
+  std::vector<uint8_t> type_info;
+  std::vector<uint8_t> parameters;  // BTreeMap<String, Parameter> encoding (node.cpp)
+};
+
+class WBuf {
+ public:
+  std::vector<uint8_t> b;
+  void u8(uint8_t v) { b.push_back(v); }
+  void u16(uint16_t v) { raw(&v, 2); }
+  void u32(uint32_t v) { raw(&v, 4); }
+  void u64(uint64_t v) { raw(&v, 8); }
+  void i32(int32_t v) { raw(&v, 4); }
+  void raw(const void* p, size_t n) {
+    const auto* c = static_cast<const uint8_t*>(p);
+    b.insert(b.end(), c, c + n);
+  }
+  void bytes(const uint8_t* p, size_t n) {
+    u64(n);
+    raw(p, n);
+  }
+  void bytes(const std::vector<uint8_t>& v) { bytes(v.data(), v.size()); }
+  void str(const std::string& s) { bytes(reinterpret_cast<const uint8_t*>(s.data()), s.size()); }
+  void token(const DropToken& t) { raw(t.b, 16); }
+  void data(const DataMsg& d) {
+    u8(d.kind);
+    if (d.kind == DATA_VEC) bytes(d.vec);
+    if (d.kind == DATA_DEVICE_IPC) {
+      raw(d.ipc.handle, 64);
+      i32(d.ipc.device);
+      i32(d.ipc.owner_pid);
+      u64(d.ipc.slot_id);
+      u64(d.ipc.offset);
+      u64(d.ipc.len);
+      token(d.ipc.token);
+    }
+  }
+  void metadata(const Metadata& m) {
+    u16(m.version);
+    u64(m.timestamp_ns);
+    bytes(m.type_info);
+    bytes(m.parameters);
+  }
+};
+
+class RBuf {
+ public:
+  RBuf(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  explicit RBuf(const std::vector<uint8_t>& v) : p_(v.data()), n_(v.size()) {}
+  void need(size_t k) {
+    if (i_ + k > n_) throw std::invalid_argument("truncated message");
+  }
+  void raw(void* out, size_t k) {
+    need(k);
+    std::memcpy(out, p_ + i_, k);
+    i_ += k;
+  }
+  uint8_t u8() {
+    uint8_t v;
+    raw(&v, 1);
+    return v;
+  }
+  uint16_t u16() {
+    uint16_t v;
+    raw(&v, 2);
+    return v;
+  }
+  uint32_t u32() {
+    uint32_t v;
+    raw(&v, 4);
+    return v;
+  }
+  uint64_t u64() {
+    uint64_t v;
+    raw(&v, 8);
+    return v;
+  }
+  int32_t i32() {
+    int32_t v;
+    raw(&v, 4);
+    return v;
+  }
+  std::vector<uint8_t> bytes() {
+    const uint64_t k = u64();
+    need(k);
+    std::vector<uint8_t> v(p_ + i_, p_ + i_ + k);
+    i_ += k;
+    return v;
+  }
+  std::string str() {
+    const uint64_t k = u64();
+    need(k);
+    std::string s(reinterpret_cast<const char*>(p_ + i_), k);
+    i_ += k;
+    return s;
+  }
+  DropToken token() {
+    DropToken t;
+    raw(t.b, 16);
+    return t;
+  }
+  DataMsg data() {
+    DataMsg d;
+    d.kind = u8();
+    if (d.kind == DATA_VEC) d.vec = bytes();
+    if (d.kind == DATA_DEVICE_IPC) {
+      raw(d.ipc.handle, 64);
+      d.ipc.device = i32();
+      d.ipc.owner_pid = i32();
+      d.ipc.slot_id = u64();
+      d.ipc.offset = u64();
+      d.ipc.len = u64();
+      d.ipc.token = token();
+    }
+    if (d.kind > DATA_DEVICE_IPC) throw std::invalid_argument("unknown DataMessage kind");
+    return d;
+  }
+  Metadata metadata() {
+    Metadata m;
+    m.version = u16();
+    m.timestamp_ns = u64();
+    m.type_info = bytes();
+    m.parameters = bytes();
+    return m;
+  }
+  size_t pos() const { return i_; }
+  size_t size() const { return n_; }
+  const uint8_t* ptr() const { return p_ + i_; }
+  void skip(size_t k) {
+    need(k);
+    i_ += k;
+  }
+
+ private:
+  const uint8_t* p_;
+  size_t n_;
+  size_t i_ = 0;
+};
+
+}  // namespace dora

@@ -1,0 +1,196 @@
+"""Local dataflow launcher: descriptor -> daemon process + node processes.
+
+The descriptor follows the reference YAML (libraries/core/src/descriptor/mod.rs:25-200):
+`nodes: [{id, path, args, inputs: {in: "node/out" | {source, queue_size}}, outputs, env,
+_unstable_deploy: {gpu: N}}]`.  Input queue_size defaults to 10 (binaries/daemon/src/spawn.rs:56).
+`path: dynamic` nodes are not spawned: the caller attaches them (e.g. the benchmark process).
+GPU placement: `_unstable_deploy.gpu` (new, next to `machine`) sets DORA_GPU_DEVICE.
+
+Processes are spawned either directly (the caller has not touched the GPU yet) or through a
+`dora_amd.launcher.Launcher` started before the caller initialised HIP.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import shlex
+import subprocess
+import tempfile
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from ._lib import LIB_DIR
+
+DEFAULT_QUEUE_SIZE = 10
+_counter = itertools.count()
+
+
+@dataclass
+class NodeSpec:
+    id: str
+    path: str = "dynamic"
+    args: List[str] = field(default_factory=list)
+    inputs: Dict[str, tuple] = field(default_factory=dict)  # input -> (src_node, src_out, queue)
+    outputs: List[str] = field(default_factory=list)
+    env: Dict[str, str] = field(default_factory=dict)
+    gpu: int = 0
+
+
+def parse_descriptor(desc) -> List[NodeSpec]:
+    if isinstance(desc, str):
+        import yaml
+        with open(desc) as f:
+            desc = yaml.safe_load(f)
+    nodes = []
+    for n in desc["nodes"]:
+        spec = NodeSpec(id=n["id"], path=n.get("path", "dynamic"))
+        args = n.get("args", [])
+        spec.args = shlex.split(args) if isinstance(args, str) else list(args)
+        spec.outputs = list(n.get("outputs", []))
+        spec.env = {str(k): str(v) for k, v in (n.get("env") or {}).items()}
+        spec.gpu = int((n.get("_unstable_deploy") or {}).get("gpu", 0))
+        for inp, src in (n.get("inputs") or {}).items():
+            q = DEFAULT_QUEUE_SIZE
+            if isinstance(src, dict):
+                q = int(src.get("queue_size", DEFAULT_QUEUE_SIZE))
+                src = src["source"]
+            node, out = src.split("/", 1)
+            spec.inputs[inp] = (node, out, q)
+        nodes.append(spec)
+    ids = [n.id for n in nodes]
+    if len(set(ids)) != len(ids):
+        raise ValueError("duplicate node ids")
+    outs = {(n.id, o) for n in nodes for o in n.outputs}
+    for n in nodes:
+        for inp, (src, out, _) in n.inputs.items():
+            if (src, out) not in outs:
+                raise ValueError(f"input `{n.id}/{inp}` maps unknown output `{src}/{out}`")
+    return nodes
+
+
+def daemon_spec(nodes: List[NodeSpec]) -> str:
+    lines = [f"node {n.id}" for n in nodes]
+    for n in nodes:
+        lines += [f"output {n.id} {o}" for o in n.outputs]
+    for n in nodes:
+        lines += [f"input {n.id} {i} {s} {o} {q}" for i, (s, o, q) in n.inputs.items()]
+    return "\n".join(lines) + "\n"
+
+
+def resolve(path: str) -> str:
+    cand = os.path.join(LIB_DIR, path)
+    return cand if os.path.exists(cand) else path
+
+
+class _Proc:
+    """A spawned process, direct (Popen) or through a Launcher."""
+
+    def __init__(self, argv, env, out, launcher=None):
+        self.launcher = launcher
+        if launcher is not None:
+            self.id = launcher.spawn(argv, env, out)
+            if self.id < 0:
+                raise RuntimeError(f"launcher could not spawn {argv}")
+            self.p = None
+        else:
+            f = open(out, "w") if out else subprocess.DEVNULL
+            self.p = subprocess.Popen(argv, env=env, stdout=f,
+                                      stderr=subprocess.STDOUT if out else None)
+
+    def poll(self):
+        return self.launcher.poll(self.id) if self.p is None else self.p.poll()
+
+    def wait(self, timeout: float):
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            rc = self.poll()
+            if rc is not None:
+                return rc
+            time.sleep(0.01)
+        return None
+
+    def kill(self):
+        if self.p is None:
+            self.launcher.kill(self.id)
+        elif self.p.poll() is None:
+            self.p.kill()
+            self.p.wait()
+
+
+class Dataflow:
+    def __init__(self, descriptor, ring_bytes: int = 4 << 20, name: Optional[str] = None,
+                 launcher=None, log_dir: Optional[str] = None):
+        self.nodes = parse_descriptor(descriptor)
+        self.shm = name or f"/dora-gpu-{os.getpid()}-{next(_counter)}"
+        self.ring_bytes = ring_bytes
+        self.launcher = launcher
+        self.log_dir = log_dir or tempfile.mkdtemp(prefix="dora-gpu-logs-")
+        self.daemon: Optional[_Proc] = None
+        self.procs: Dict[str, _Proc] = {}
+        self._spec_file = None
+
+    def node_env(self, node: NodeSpec) -> dict:
+        env = dict(os.environ)
+        env.update(node.env)
+        env.update(self.dynamic_env(node.id))
+        return env
+
+    def dynamic_env(self, node_id: str) -> dict:
+        """Environment a node runs with (set it before Node() for `path: dynamic` nodes)."""
+        n = next(x for x in self.nodes if x.id == node_id)
+        return {"DORA_GPU_DATAFLOW": self.shm, "DORA_NODE_ID": n.id,
+                "DORA_GPU_DEVICE": str(n.gpu)}
+
+    def log(self, name: str) -> str:
+        p = os.path.join(self.log_dir, f"{name}.log")
+        return open(p).read() if os.path.exists(p) else ""
+
+    def start(self, timeout: float = 30.0):
+        fd, self._spec_file = tempfile.mkstemp(prefix="dora-gpu-spec-", suffix=".txt")
+        with os.fdopen(fd, "w") as f:
+            f.write(daemon_spec(self.nodes))
+        dlog = os.path.join(self.log_dir, "_daemon.log")
+        self.daemon = _Proc([resolve("dora-gpu-daemon"), "--shm", self.shm, "--spec",
+                             self._spec_file, "--ring-bytes", str(self.ring_bytes)],
+                            dict(os.environ), dlog, self.launcher)
+        deadline = time.time() + timeout
+        while '"ready"' not in self.log("_daemon"):
+            if self.daemon.poll() is not None or time.time() > deadline:
+                raise RuntimeError(f"daemon failed to start: {self.log('_daemon')!r}")
+            time.sleep(0.005)
+        for n in self.nodes:
+            if n.path == "dynamic":
+                continue
+            self.procs[n.id] = _Proc([resolve(n.path), *n.args], self.node_env(n),
+                                     os.path.join(self.log_dir, f"{n.id}.log"), self.launcher)
+        return self
+
+    def wait(self, timeout: float = 60.0) -> Dict[str, Optional[int]]:
+        deadline = time.time() + timeout
+        codes = {}
+        for nid, p in self.procs.items():
+            codes[nid] = p.wait(max(0.1, deadline - time.time()))
+            if codes[nid] is None:
+                p.kill()
+        if self.daemon:
+            codes["_daemon"] = self.daemon.wait(max(0.1, deadline - time.time()))
+        return codes
+
+    def stop(self):
+        for p in self.procs.values():
+            if p.poll() is None:
+                p.kill()
+        if self.daemon and self.daemon.poll() is None:
+            self.daemon.kill()
+        if self._spec_file and os.path.exists(self._spec_file):
+            os.unlink(self._spec_file)
+        shm_path = "/dev/shm" + self.shm
+        if os.path.exists(shm_path):
+            os.unlink(shm_path)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

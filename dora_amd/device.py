@@ -144,6 +144,12 @@ class DeviceArray:
         release_array(self.array)
         self._keepalive = None
 
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def __enter__(self):
         return self
 

@@ -1,0 +1,230 @@
+"""Python node API on the device data plane — mirrors the reference Python `Node`
+(apis/python/node/src/lib.rs:29-185) and its event dicts (apis/python/operator/src/lib.rs:81-165).
+
+    node = Node()                                   # from env (DORA_GPU_DATAFLOW, DORA_NODE_ID)
+    for event in node:                              # or node.next(timeout)
+        if event["type"] == "INPUT":
+            arr = event["value"]                    # DeviceArray: zero-copy view of the HBM sample
+            host = arr.to_pyarrow()                 # host staging for pyarrow consumers (F12)
+    node.send_output("out", pa.array([...]), {"k": 1})   # host pyarrow -> DMA into a device slot
+    node.send_output("out", device_array)                 # HBM array -> HIP pack kernel
+    node.send_output("out", b"raw bytes")                 # ArrowTypeInfo::byte_array
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+from ctypes import byref, c_double, c_size_t, c_uint8, c_uint64, c_void_p
+from typing import Optional
+
+from . import _lib
+from ._lib import ARROW_DEVICE_CPU, ARROW_DEVICE_ROCM, DoraGpuError, call, load
+from .arrow_c import ArrowArray, ArrowSchema, CArray
+from .device import DeviceArray, DeviceBuffer
+from .type_info import decode
+
+EVENT_TYPES = {0: "STOP", 1: "INPUT", 2: "INPUT_CLOSED", 3: "ERROR", 4: "ALL_INPUTS_CLOSED"}
+
+
+def encode_parameters(metadata: Optional[dict]) -> bytes:
+    """MetadataParameters encoding (pydict_to_metadata, apis/python/operator/src/lib.rs:165-186:
+    bool / int / str, anything else stringified)."""
+    if not metadata:
+        return b""
+    out = [struct.pack("<I", len(metadata))]
+    for k, v in sorted(metadata.items()):
+        kb = str(k).encode()
+        out.append(struct.pack("<Q", len(kb)) + kb)
+        if isinstance(v, bool):
+            out.append(struct.pack("<BB", 0, int(v)))
+        elif isinstance(v, int):
+            out.append(struct.pack("<Bq", 1, v))
+        else:
+            sb = (v if isinstance(v, str) else str(v)).encode()
+            out.append(struct.pack("<BQ", 2, len(sb)) + sb)
+    return b"".join(out)
+
+
+def decode_parameters(raw: bytes) -> dict:
+    if len(raw) < 4:
+        return {}
+    (n,), i, out = struct.unpack_from("<I", raw), 4, {}
+    for _ in range(n):
+        (kl,) = struct.unpack_from("<Q", raw, i)
+        i += 8
+        key = raw[i:i + kl].decode()
+        i += kl
+        tag = raw[i]
+        i += 1
+        if tag == 0:
+            out[key] = bool(raw[i])
+            i += 1
+        elif tag == 1:
+            (out[key],) = struct.unpack_from("<q", raw, i)
+            i += 8
+        else:
+            (sl,) = struct.unpack_from("<Q", raw, i)
+            i += 8
+            out[key] = raw[i:i + sl].decode()
+            i += sl
+    return out
+
+
+def _u8(b: bytes):
+    return (c_uint8 * max(len(b), 1)).from_buffer_copy(b or b"\0")
+
+
+class _EventHandle:
+    """Owns a C dora_event; freeing it (explicitly or by GC) releases the drop token once no
+    DeviceArray view references the sample any more."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+        self._lib = load()
+
+    def free(self):
+        if self.ptr:
+            self._lib.dora_event_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+class Node:
+    def __init__(self, node_id: Optional[str] = None, dataflow: Optional[str] = None,
+                 device: Optional[int] = None):
+        self._lib = load()
+        h = c_void_p()
+        if node_id is None and dataflow is None:
+            call("dora_node_init_from_env", byref(h))
+        else:
+            shm = dataflow or os.environ["DORA_GPU_DATAFLOW"]
+            dev = device if device is not None else int(os.environ.get("DORA_GPU_DEVICE", "0"))
+            call("dora_node_init", shm.encode(), node_id.encode(), dev, byref(h))
+        self.handle = h.value
+        self.id = node_id or os.environ.get("DORA_NODE_ID")
+        self.device = device if device is not None else int(os.environ.get("DORA_GPU_DEVICE", "0"))
+
+    # -------------------------------------------------------------------------------- sending
+    def send_output(self, output_id: str, data, metadata: Optional[dict] = None):
+        params = encode_parameters(metadata)
+        pb = _u8(params)
+        oid = output_id.encode()
+        if isinstance(data, (bytes, bytearray, memoryview)):
+            buf = ctypes.create_string_buffer(bytes(data), len(data))
+            call("dora_node_send_output_bytes", self.handle, oid, buf, len(data), ARROW_DEVICE_CPU,
+                 pb, len(params))
+        elif isinstance(data, DeviceArray):
+            s = data.export_schema()
+            try:
+                call("dora_node_send_output", self.handle, oid, byref(data.array), byref(s),
+                     ARROW_DEVICE_ROCM, pb, len(params))
+            finally:
+                from .arrow_c import release_schema
+                release_schema(s)
+        elif isinstance(data, DeviceBuffer):
+            call("dora_node_send_output_bytes", self.handle, oid, data.ptr, data.size,
+                 ARROW_DEVICE_ROCM, pb, len(params))
+        elif hasattr(data, "_export_to_c"):
+            with CArray.from_pyarrow(data) as c:
+                call("dora_node_send_output", self.handle, oid, byref(c.array), byref(c.schema),
+                     ARROW_DEVICE_CPU, pb, len(params))
+        else:
+            raise TypeError("data must be bytes, a pyarrow.Array, a DeviceArray or a DeviceBuffer")
+
+    def send_output_device_bytes(self, output_id: str, ptr: int, n: int,
+                                 metadata: Optional[dict] = None):
+        """send_output_raw with an HBM source: one pack kernel into a fresh device sample."""
+        params = encode_parameters(metadata)
+        call("dora_node_send_output_bytes", self.handle, output_id.encode(), ptr, n,
+             ARROW_DEVICE_ROCM, _u8(params), len(params))
+
+    def close_outputs(self, outputs):
+        arr = (ctypes.c_char_p * len(outputs))(*[o.encode() for o in outputs])
+        call("dora_node_close_outputs", self.handle, arr, len(outputs))
+
+    # ------------------------------------------------------------------------------ receiving
+    def next(self, timeout: Optional[float] = None):
+        """Next event dict, or None when the stream has ended (or on timeout)."""
+        h = c_void_p()
+        rc = self._lib.dora_node_next_event(self.handle, -1 if timeout is None
+                                            else int(timeout * 1e6), byref(h))
+        if rc in (-5, -6):   # closed / timeout
+            return None
+        _lib.check(rc)
+        ev = _EventHandle(h.value)
+        kind = EVENT_TYPES.get(self._lib.dora_event_type(ev.ptr), "UNKNOWN")
+        if kind == "ALL_INPUTS_CLOSED":
+            ev.free()
+            return None
+        out = {"type": kind, "id": self._lib.dora_event_id(ev.ptr).decode()}
+        if kind == "ERROR":
+            out["error"] = self._lib.dora_event_error(ev.ptr).decode()
+        if kind == "INPUT":
+            p, n = ctypes.POINTER(c_uint8)(), c_size_t()
+            call("dora_event_parameters", ev.ptr, byref(p), byref(n))
+            out["metadata"] = decode_parameters(ctypes.string_at(p, n.value) if n.value else b"")
+            out["timestamp_ns"] = self._lib.dora_event_timestamp_ns(ev.ptr)
+            call("dora_event_type_info", ev.ptr, byref(p), byref(n))
+            ti = decode(ctypes.string_at(p, n.value))
+            out["type_info"] = ti
+            dp, dn = c_void_p(), c_size_t()
+            call("dora_event_data", ev.ptr, byref(dp), byref(dn))
+            out["data_ptr"], out["data_len"] = dp.value, dn.value
+            out["on_device"] = bool(self._lib.dora_event_is_device(ev.ptr))
+            if dn.value == 0:       # RawData::Vec(empty) -> ArrayData::new_empty(data_type)
+                import pyarrow as pa
+                out["value"] = pa.array([], type=ti.arrow_type())
+            elif out["on_device"]:
+                a, s = ArrowArray(), ArrowSchema()
+                call("dora_event_array", ev.ptr, byref(a), byref(s))
+                import pyarrow as pa
+                t = pa.DataType._import_from_c(ctypes.addressof(s))
+                # the array keeps the input alive; the event handle can go
+                out["value"] = DeviceArray(a, t)
+            else:   # inline DataMessage::Vec sample of a host-only node
+                out["value"] = ctypes.string_at(dp.value, dn.value) if dn.value else b""
+        out["_event"] = ev
+        return out
+
+    def __iter__(self):
+        while True:
+            ev = self.next()
+            if ev is None:
+                return
+            yield ev
+
+    # -------------------------------------------------------------------------------- stats
+    @property
+    def stream(self) -> int:
+        return self._lib.dora_node_stream(self.handle)
+
+    def stats(self) -> dict:
+        v = [c_uint64() for _ in range(4)]
+        call("dora_node_stats", self.handle, *[byref(x) for x in v])
+        return dict(zip(["slots_created", "cache_hits", "in_flight", "dropped_inputs"],
+                        [x.value for x in v]))
+
+    def set_profiling(self, enable: bool = True):
+        call("dora_node_set_profiling", self.handle, int(enable))
+
+    def pack_stats(self) -> dict:
+        c, ms, b = c_uint64(), c_double(), c_uint64()
+        call("dora_node_pack_stats", self.handle, byref(c), byref(ms), byref(b))
+        return {"count": c.value, "total_ms": ms.value, "bytes": b.value}
+
+    def close(self):
+        if self.handle:
+            self._lib.dora_node_free(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+__all__ = ["Node", "encode_parameters", "decode_parameters", "DoraGpuError"]

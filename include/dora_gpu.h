@@ -188,6 +188,101 @@ int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uin
 /* Fill `len` device bytes with the splitmix64 stream of `seed` (BASELINE.md §2 payloads). */
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Node API — replaces DoraNode / EventStream (apis/rust/node/src/node/mod.rs:42-503,         */
+/* apis/rust/node/src/event_stream/mod.rs:27-235) and the C node API (apis/c/node/node_api.h) */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct dora_node dora_node;
+typedef struct dora_sample dora_sample;
+typedef struct dora_event dora_event;
+
+enum {
+  DORA_EVENT_STOP = 0,             /* Event::Stop                       (event.rs:12)     */
+  DORA_EVENT_INPUT = 1,            /* Event::Input{id, metadata, data}  (event.rs:17-21)  */
+  DORA_EVENT_INPUT_CLOSED = 2,     /* Event::InputClosed{id}            (event.rs:22-24)  */
+  DORA_EVENT_ERROR = 3,            /* Event::Error                      (event.rs:25)     */
+  DORA_EVENT_ALL_INPUTS_CLOSED = 4 /* end of the event stream (NodeEvent::AllInputsClosed) */
+};
+
+/* DoraNode::init (mod.rs:121-155): attach to the dataflow region `shm_name`, register as
+ * `node_id` on GPU `device`, subscribe and wait for every node of the dataflow to be ready. */
+int dora_node_init(const char* shm_name, const char* node_id, int device, dora_node** out);
+/* DoraNode::init_from_env (mod.rs:65-76): DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE. */
+int dora_node_init_from_env(dora_node** out);
+/* Drop for DoraNode (mod.rs:384-431): close outputs, wait <= 10 s for drop tokens, done. */
+void dora_node_free(dora_node* node);
+/* The HIP stream the node packs on; consumers must run their kernels on it so the drop token
+ * is only returned after they have read the sample. */
+dora_stream_t dora_node_stream(dora_node* node);
+
+/* allocate_data_sample (mod.rs:303-346): a device slot of `len` bytes (best-fit from the
+ * 20-entry cache of recycled slots, else a new exported hipMalloc slot); len 0 -> empty Vec. */
+int dora_node_allocate_data_sample(dora_node* node, size_t len, dora_sample** out);
+void* dora_sample_data(dora_sample* sample); /* device pointer (slot) */
+size_t dora_sample_len(const dora_sample* sample);
+void dora_sample_discard(dora_node* node, dora_sample* sample); /* unsent sample -> cache */
+/* send_output_sample (mod.rs:246-275): consumes `sample` (may be NULL = no data). The sample
+ * must be fully written (its stream synchronized) before the call. `params` is the encoded
+ * MetadataParameters (u32 n, then per entry: u64 klen, key, u8 tag 0=bool 1=int 2=string,
+ * value: u8 | i64 | u64 len + bytes). */
+int dora_node_send_output_sample(dora_node* node, const char* output_id, const uint8_t* type_info,
+                                 size_t type_info_len, const uint8_t* params, size_t params_len,
+                                 dora_sample* sample);
+/* send_output (mod.rs:198-215): plan + allocate + HIP pack + send.  `device_type` as in
+ * dora_gpu_plan. */
+int dora_node_send_output(dora_node* node, const char* output_id, const struct ArrowArray* array,
+                          const struct ArrowSchema* schema, ArrowDeviceType device_type,
+                          const uint8_t* params, size_t params_len);
+/* send_output_raw / send_output_bytes (mod.rs:180-196, 217-228): `len` bytes as
+ * ArrowTypeInfo::byte_array, copied into a device sample (kernel for HBM sources, DMA for host
+ * sources).  This is the benchmark's send path (examples/benchmark/node/src/main.rs:46-48). */
+int dora_node_send_output_bytes(dora_node* node, const char* output_id, const void* data,
+                                size_t len, ArrowDeviceType device_type, const uint8_t* params,
+                                size_t params_len);
+/* close_outputs (mod.rs:277-289). */
+int dora_node_close_outputs(dora_node* node, const char* const* output_ids, size_t count);
+
+/* EventStream::recv / recv_timeout (event_stream/mod.rs:121-140); timeout_us < 0 blocks.
+ * Returns DORA_ERR_TIMEOUT on timeout and DORA_ERR_CLOSED after the stream ended. */
+int dora_node_next_event(dora_node* node, int64_t timeout_us, dora_event** out);
+int dora_event_type(const dora_event* ev);
+const char* dora_event_id(const dora_event* ev);
+const char* dora_event_error(const dora_event* ev);
+/* Raw sample of an input: device pointer (mapped IPC slot) or host pointer for Vec data. */
+int dora_event_data(const dora_event* ev, const void** ptr, size_t* len);
+int dora_event_is_device(const dora_event* ev);
+/* Serialized ArrowTypeInfo / MetadataParameters / timestamp of the input's Metadata. */
+int dora_event_type_info(const dora_event* ev, const uint8_t** type_info, size_t* len);
+int dora_event_parameters(const dora_event* ev, const uint8_t** params, size_t* len);
+uint64_t dora_event_timestamp_ns(const dora_event* ev);
+/* RawData::into_arrow_array (event.rs:35-91): zero-copy device ArrowArray over the sample; it
+ * keeps the input (and its drop token) alive until released. */
+int dora_event_array(const dora_event* ev, struct ArrowArray* out_array,
+                     struct ArrowSchema* out_schema);
+/* Drop the event; the drop token is reported once no array references the data any more. */
+void dora_event_free(dora_event* ev);
+
+int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
+                    uint64_t* in_flight, uint64_t* dropped_inputs);
+/* Pack-kernel timing on the node stream (HIP events around every pack launch). */
+int dora_node_set_profiling(dora_node* node, int enable);
+int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Daemon — the data-plane part of binaries/daemon (send_out, drop tokens, input closing)     */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct dora_daemon dora_daemon;
+/* Create the dataflow region `shm_name` ("/name").  `spec` lines:
+ *   node <id> | output <node> <output> | input <node> <input> <src_node> <src_output> <queue> */
+int dora_daemon_create(const char* shm_name, const char* spec, size_t ring_bytes,
+                       dora_daemon** out);
+/* Route until every node is done (0), or timeout_ms elapses (DORA_ERR_TIMEOUT). */
+int dora_daemon_run(dora_daemon* daemon, int64_t timeout_ms);
+/* Send Event::Stop to every node. */
+int dora_daemon_request_stop(dora_daemon* daemon);
+int dora_daemon_stats(dora_daemon* daemon, uint64_t* routed, uint64_t* pending_tokens);
+void dora_daemon_free(dora_daemon* daemon);
+
 #ifdef __cplusplus
 }
 #endif

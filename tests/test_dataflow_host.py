@@ -1,0 +1,120 @@
+"""Control plane on the CPU (no GPU): daemon routing, AllNodesReady, drop-oldest input queues,
+InputClosed / end of stream, metadata parameters, output checks — with host-only nodes, which
+carry only the reference's inline `DataMessage::Vec` samples (< 4096 B)."""
+import ctypes
+import os
+import threading
+import time
+
+import pytest
+
+from dora_amd import _lib
+from dora_amd.dataflow import daemon_spec, parse_descriptor
+from dora_amd.node import Node, decode_parameters, encode_parameters
+
+
+class InProcessDaemon:
+    def __init__(self, desc):
+        self.lib = _lib.load()
+        self.shm = f"/dora-gpu-test-{os.getpid()}-{id(self)}"
+        h = ctypes.c_void_p()
+        _lib.call("dora_daemon_create", self.shm.encode(),
+                  daemon_spec(parse_descriptor(desc)).encode(), 1 << 20, ctypes.byref(h))
+        self.h = h.value
+        self.rc = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        self.rc = self.lib.dora_daemon_run(self.h, 20000)
+
+    def join(self):
+        self.t.join(25)
+        assert not self.t.is_alive()
+        self.lib.dora_daemon_free(self.h)
+
+
+def _start_nodes(shm, ids):
+    out = {}
+
+    def mk(i):
+        out[i] = Node(i, dataflow=shm, device=-1)
+    ts = [threading.Thread(target=mk, args=(i,)) for i in ids]
+    [t.start() for t in ts]
+    [t.join(20) for t in ts]
+    assert set(out) == set(ids)
+    return out
+
+
+DESC = {"nodes": [
+    {"id": "src", "outputs": ["out", "other"]},
+    {"id": "dst", "inputs": {"in": {"source": "src/out", "queue_size": 3}}, "outputs": []},
+]}
+
+
+def test_parameters_roundtrip():
+    p = {"a": True, "b": -5, "c": "hello", "d": 2.5}
+    assert decode_parameters(encode_parameters(p)) == {"a": True, "b": -5, "c": "hello",
+                                                       "d": "2.5"}
+    assert encode_parameters(None) == b""
+
+
+def test_descriptor_validation():
+    with pytest.raises(ValueError, match="unknown output"):
+        parse_descriptor({"nodes": [{"id": "a", "inputs": {"x": "b/y"}}, {"id": "b"}]})
+    spec = daemon_spec(parse_descriptor(DESC))
+    assert "input dst in src out 3" in spec
+
+
+def test_routing_drop_oldest_and_close():
+    d = InProcessDaemon(DESC)
+    nodes = _start_nodes(d.shm, ["src", "dst"])
+    src, dst = nodes["src"], nodes["dst"]
+    for i in range(5):
+        src.send_output("out", bytes([i]) * 10, {"seq": i})
+    time.sleep(0.2)
+    with pytest.raises(_lib.DoraGpuError, match="unknown dora node output"):
+        src.send_output("nope", b"x")
+    with pytest.raises(_lib.DoraGpuError, match="host-only"):
+        src.send_output("out", b"\0" * 5000)
+    src.close()          # closes outputs -> InputClosed + end of stream for dst
+    got = []
+    closed = []
+    while True:
+        ev = dst.next(timeout=5)
+        if ev is None:
+            break
+        if ev["type"] == "INPUT":
+            got.append((ev["metadata"]["seq"], ev["value"]))
+            assert ev["type_info"].to_json()["data_type"] == "C"
+        elif ev["type"] == "INPUT_CLOSED":
+            closed.append(ev["id"])
+    # queue_size 3: the three newest inputs survive (node_communication/mod.rs:320-359)
+    assert [s for s, _ in got] == [2, 3, 4]
+    assert got[0][1] == bytes([2]) * 10
+    assert closed == ["in"]
+    dst.close()
+    d.join()
+    assert d.rc == 0
+
+
+def test_zero_length_sample_and_ordering():
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["o"]},
+        {"id": "b", "inputs": {"i": {"source": "a/o", "queue_size": 1000}}}]})
+    nodes = _start_nodes(d.shm, ["a", "b"])
+    n = 200
+    for k in range(n):
+        nodes["a"].send_output("o", b"" if k % 2 else bytes([k % 256]) * (k % 50), {"k": k})
+    nodes["a"].close()
+    seen = []
+    for ev in nodes["b"]:
+        if ev["type"] == "INPUT":
+            seen.append(ev["metadata"]["k"])
+            if ev["metadata"]["k"] % 2:   # empty sample -> ArrayData::new_empty(UInt8)
+                assert len(ev["value"]) == 0 and str(ev["value"].type) == "uint8"
+            elif ev["metadata"]["k"] % 50:
+                assert ev["value"] == bytes([ev["metadata"]["k"] % 256]) * (ev["metadata"]["k"] % 50)
+    assert seen == list(range(n))
+    nodes["b"].close()
+    d.join()
