@@ -8,6 +8,7 @@
 // when source and destination disagree mod 16 (e.g. C3's x buffer at sample offset 68), two
 // aligned loads are funnel-shifted with v_alignbyte_b32.  The shift is uniform per segment, so
 // the per-segment loop is specialised on it and no lane diverges.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -223,9 +224,11 @@ unsigned grid_for(uint64_t items) {
 }  // namespace
 
 // Launch the pack of `n` segments into `dst` (device).  Segments with device sources go to
-// pack_kernel in batches of kMaxSegs; host sources are DMA'd with hipMemcpyAsync.
+// pack_kernel in batches of kMaxSegs; host sources are DMA'd with hipMemcpyAsync.  With timing
+// events the launches go through hipExtLaunchKernelGGL, whose dispatch packet stamps the first
+// kernel's begin into `ev_start` and the last kernel's end into `ev_stop`.
 int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
-                hipStream_t stream) {
+                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
   if (dev == ARROW_DEVICE_CPU) {
     for (size_t i = 0; i < n; ++i)
       DORA_HIP(hipMemcpyAsync(dst + segs[i].dst_off, segs[i].src, segs[i].len,
@@ -255,8 +258,14 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
       a.chunk_end[k] = static_cast<uint32_t>(chunks);
     }
     a.nseg = static_cast<uint32_t>(m);
-    hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
-                       stream, a);
+    const bool first = i == 0, last = i + m == n;
+    if (ev_start || ev_stop) {
+      hipExtLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
+                            stream, first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
+    } else {
+      hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
+                         stream, a);
+    }
     DORA_HIP(hipGetLastError());
     i += m;
   }
@@ -299,7 +308,8 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
   if (plan->segs.empty()) return DORA_OK;
   if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
   return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
-                           static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream));
+                           static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream), nullptr,
+                           nullptr);
 }
 
 int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream_t stream) {

@@ -39,7 +39,7 @@
 namespace dora {
 
 int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
-                hipStream_t stream);
+                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
 
 namespace {
 
@@ -437,10 +437,10 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     for (const Segment& g : plan->segs) std::memcpy(s->vec.data() + g.dst_off, g.src, g.len);
   } else if (plan->size) {
     hipStream_t st = n->core->stream;
-    if (n->profile) (void)hipEventRecord(n->ev0, st);
+    const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU;
     rc = launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
-                     static_cast<uint8_t*>(s->slot->ptr), st);
-    if (n->profile) (void)hipEventRecord(n->ev1, st);
+                     static_cast<uint8_t*>(s->slot->ptr), st, timed ? n->ev0 : nullptr,
+                     timed ? n->ev1 : nullptr);
     if (rc != DORA_OK) {
       add_to_cache(n, s->slot);
       delete s;
@@ -453,7 +453,7 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       delete s;
       return fail(DORA_ERR_HIP, "pack: %s", hipGetErrorString(e));
     }
-    if (n->profile) {
+    if (timed) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, n->ev0, n->ev1) == hipSuccess) {
         n->pack_ms += ms;
