@@ -12,8 +12,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -23,7 +25,6 @@ namespace dora {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;
 constexpr int kMaxSegs = 32;
 
 struct PackSeg {
@@ -40,16 +41,27 @@ struct PackArgs {
   PackSeg seg[kMaxSegs];
 };
 
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-  return *reinterpret_cast<const uint4*>(p);
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return *reinterpret_cast<const u32x4*>(p);
 }
-__device__ __forceinline__ void st16(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  } else {
+    *reinterpret_cast<u32x4*>(p) = v;
+  }
+}
 
 // Bytes [4Q + b, 4Q + b + 16) of the 32-byte little-endian concatenation lo|hi.
 template <int Q>
-__device__ __forceinline__ uint4 funnel(uint4 lo, uint4 hi, uint32_t b) {
+__device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
   const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  uint4 o;
+  u32x4 o;
   o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], b);
   o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], b);
   o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], b);
@@ -57,45 +69,48 @@ __device__ __forceinline__ uint4 funnel(uint4 lo, uint4 hi, uint32_t b) {
   return o;
 }
 
-// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` (any alignment).
+// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned.  U loads of
+// 16 B per lane in flight before the stores.
+template <int U, bool NT>
 __device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
-  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * kUnroll) {
-    uint4 v[kUnroll];
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
+    u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) v[u] = ld16(sp + 16 * i);
+      if (i < nunits) v[u] = ld16<NT>(sp + 16 * i);
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16(dp + 16 * i, v[u]);
+      if (i < nunits) st16<NT>(dp + 16 * i, v[u]);
     }
   }
 }
 
-template <int Q>
+template <int U, bool NT, int Q>
 __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
                                              uint64_t nunits) {
   // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
-  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * kUnroll) {
-    uint4 lo[kUnroll], hi[kUnroll];
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
+    u32x4 lo[U], hi[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
       if (i < nunits) {
-        lo[u] = ld16(sbase + 16 * i);
-        hi[u] = ld16(sbase + 16 * i + 16);
+        lo[u] = ld16<NT>(sbase + 16 * i);
+        hi[u] = ld16<NT>(sbase + 16 * i + 16);
       }
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
+      if (i < nunits) st16<NT>(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
     }
   }
 }
 
+template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   const uint32_t chunk = blockIdx.x;
   uint32_t s = 0;
@@ -136,29 +151,63 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   const uint8_t* sp = src + (b0 - d0);
   const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
   if (r == 0) {
-    copy_aligned(dp, sp, nunits);
+    copy_aligned<U, NT>(dp, sp, nunits);
     return;
   }
   const uint8_t* sbase = sp - r;
   const uint32_t b = r & 3;
   switch (r >> 2) {
-    case 0: copy_shifted<0>(dp, sbase, b, nunits); break;
-    case 1: copy_shifted<1>(dp, sbase, b, nunits); break;
-    case 2: copy_shifted<2>(dp, sbase, b, nunits); break;
-    default: copy_shifted<3>(dp, sbase, b, nunits); break;
+    case 0: copy_shifted<U, NT, 0>(dp, sbase, b, nunits); break;
+    case 1: copy_shifted<U, NT, 1>(dp, sbase, b, nunits); break;
+    case 2: copy_shifted<U, NT, 2>(dp, sbase, b, nunits); break;
+    default: copy_shifted<U, NT, 3>(dp, sbase, b, nunits); break;
   }
 }
 
-uint32_t choose_chunk_bytes(uint64_t body_bytes) {
+// Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
+// DORA_GPU_PACK_VARIANT = u4 | u8 | u4nt | u8nt (tuning knob; default below).
+struct Variant {
+  int unroll;
+  bool nt;
+};
+
+std::atomic<int> g_unroll{0};       // 0 = default (4) / env
+std::atomic<int> g_nt{-1};          // -1 = default (off) / env
+std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
+
+// Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
+// 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
+// cache) and are neutral below; 8 loads in flight per lane for large bodies.
+Variant pack_variant() {
+  static const Variant env = [] {
+    Variant d{0, true};
+    if (const char* e = std::getenv("DORA_GPU_PACK_VARIANT")) {
+      const std::string s(e);
+      if (s.rfind("u8", 0) == 0) d.unroll = 8;
+      if (s.rfind("u4", 0) == 0) d.unroll = 4;
+      if (s.rfind("u2", 0) == 0) d.unroll = 2;
+      d.nt = s.find("nt") != std::string::npos;
+    }
+    return d;
+  }();
+  Variant v = env;
+  if (const int u = g_unroll.load(std::memory_order_relaxed)) v.unroll = u;
+  if (const int nt = g_nt.load(std::memory_order_relaxed); nt >= 0) v.nt = nt != 0;
+  return v;
+}
+
+uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
+  if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
   if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
     uint64_t v = std::strtoull(e, nullptr, 10);
     if (v >= 16 && v % 16 == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
   }
-  // One pass of a 256-thread block with 4 loads in flight moves 16 KiB; aim for >= ~2k
-  // workgroups on big messages (256 CUs x 8 resident) and a few passes per block beyond that.
-  const uint64_t pass = uint64_t(kThreads) * 16 * kUnroll;
-  uint64_t cb = (body_bytes / 2048 + pass - 1) / pass * pass;
-  cb = std::max<uint64_t>(cb, pass);
+  // ~2k workgroups on big messages (256 CUs x 8 resident), never less than 8 KiB per
+  // workgroup (measured flat within noise from 8 KiB to 32 KiB at 4-40 MB, r01 sweep).
+  (void)unroll;
+  constexpr uint64_t kGrain = 8192;
+  uint64_t cb = (body_bytes / 2048 + kGrain - 1) / kGrain * kGrain;
+  cb = std::max<uint64_t>(cb, kGrain);
   cb = std::min<uint64_t>(cb, uint64_t(1) << 22);
   return static_cast<uint32_t>(cb);
 }
@@ -243,7 +292,9 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
     uint64_t body = 0;
     const size_t m = std::min<size_t>(kMaxSegs, n - i);
     for (size_t k = 0; k < m; ++k) body += segs[i + k].len;
-    a.chunk_bytes = choose_chunk_bytes(body);
+    Variant var = pack_variant();
+    if (var.unroll == 0) var.unroll = body >= (8u << 20) ? 8 : 4;
+    a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
     uint64_t chunks = 0;
     for (size_t k = 0; k < m; ++k) {
       const Segment& s = segs[i + k];
@@ -259,12 +310,15 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
     }
     a.nseg = static_cast<uint32_t>(m);
     const bool first = i == 0, last = i + m == n;
+    void (*kern)(PackArgs) = pack_kernel<4, false>;
+    if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;
+    else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, true> : pack_kernel<2, false>;
+    else if (var.nt) kern = pack_kernel<4, true>;
     if (ev_start || ev_stop) {
-      hipExtLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
-                            stream, first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
+      hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0, stream,
+                            first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
     } else {
-      hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0,
-                         stream, a);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0, stream, a);
     }
     DORA_HIP(hipGetLastError());
     i += m;
@@ -310,6 +364,16 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
   return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                            static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream), nullptr,
                            nullptr);
+}
+
+int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
+  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8)
+    return dora::fail(DORA_ERR_INVALID, "unroll must be 0, 2, 4 or 8");
+  if (chunk_bytes % 16) return dora::fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 16");
+  dora::g_unroll.store(unroll);
+  dora::g_nt.store(nontemporal < 0 ? -1 : (nontemporal ? 1 : 0));
+  dora::g_chunk.store(chunk_bytes);
+  return DORA_OK;
 }
 
 int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream_t stream) {

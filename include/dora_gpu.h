@@ -151,6 +151,9 @@ int dora_gpu_plan_type_info(const dora_plan* plan, uint8_t* buf, size_t cap, siz
  * `dst` (device memory, `dst_len` >= plan size) on `stream`; async.  Padding is not written.
  */
 int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_t stream);
+/* Tuning knob of the pack kernel (process-wide): 16-B loads in flight per lane (0 = default,
+ * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1), bytes per workgroup (0 = auto). */
+int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident Arrow arrays                                                               */

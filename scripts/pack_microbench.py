@@ -1,13 +1,18 @@
-"""Microbenchmark of the pack kernel vs hipMemcpyAsync D2D (the measured copy peak).
+"""Microbenchmark of the pack kernel variants vs hipMemcpyAsync D2D (the measured copy peak).
 
+Variants (unroll, non-temporal, chunk bytes) are interleaved in ONE process over several rounds
+(cdna_hip_programming.md §5.4 rule 24); kernel time comes from hipExtLaunchKernel start/stop
+stamps... here from HIP events around a batch of back-to-back launches (includes launch gaps).
 Buffers rotate over > 512 MiB so the 256 MiB Infinity Cache does not inflate HBM numbers.
-Prints one JSON line per (variant, size).  Usage: python scripts/pack_microbench.py [--iters N]
+Prints one JSON line per (variant, size) with the median over rounds.
 """
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
+import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -19,13 +24,20 @@ from dora_amd.arrow_utils import Plan  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--sizes", default="4096,65536,1048576,4096000,16777216,40960000")
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sizes", default="4096000,16777216,40960000")
     ap.add_argument("--misalign", type=int, default=0)
+    ap.add_argument("--sweep", action="store_true", help="sweep unroll x nt x chunk")
     args = ap.parse_args()
     device.set_device(0)
     s = device.Stream()
     e0, e1 = device.Event(), device.Event()
+    if args.sweep:
+        variants = [("memcpy", 0, 0, 0)] + [("pack", u, nt, ch) for u, nt, ch in itertools.product(
+            [2, 4, 8], [1], [0, 4096, 8192, 16384, 20480, 32768])]
+    else:
+        variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     for size in [int(x) for x in args.sizes.split(",")]:
         nbuf = max(2, min(64, (640 << 20) // (2 * size)))
         srcs = [device.DeviceBuffer(size + 64) for _ in range(nbuf)]
@@ -33,29 +45,36 @@ def main():
         for b in srcs:
             device.fill_splitmix(b.ptr, b.size, 7, s)
         plans = [Plan.of_bytes(b.ptr + args.misalign, size, on_device=True) for b in srcs]
-        for variant in ["pack", "memcpy"]:
-            for w in range(3):
-                k = w % nbuf
-                if variant == "pack":
-                    plans[k].pack(dsts[k].ptr, size, s)
-                else:
-                    call("dora_gpu_memcpy_async", dsts[k].ptr, srcs[k].ptr + args.misalign, size,
-                         s.handle)
-            e0.record(s)
-            for it in range(args.iters):
-                k = it % nbuf
-                if variant == "pack":
-                    plans[k].pack(dsts[k].ptr, size, s)
-                else:
-                    call("dora_gpu_memcpy_async", dsts[k].ptr, srcs[k].ptr + args.misalign, size,
-                         s.handle)
-            e1.record(s)
-            e1.sync()
-            ms = e0.elapsed_ms(e1) / args.iters
+        res = {v: [] for v in variants}
+        for _ in range(args.rounds):
+            for v in variants:
+                kind, u, nt, ch = v
+                if kind == "pack":
+                    call("dora_gpu_pack_tune", u, nt, ch)
+
+                def launch(k):
+                    if kind == "pack":
+                        plans[k].pack(dsts[k].ptr, size, s)
+                    else:
+                        call("dora_gpu_memcpy_async", dsts[k].ptr, srcs[k].ptr + args.misalign,
+                             size, s.handle)
+                for w in range(3):
+                    launch(w % nbuf)
+                e0.record(s)
+                for it in range(args.iters):
+                    launch(it % nbuf)
+                e1.record(s)
+                e1.sync()
+                res[v].append(e0.elapsed_ms(e1) / args.iters)
+        call("dora_gpu_pack_tune", 0, -1, 0)
+        for v in variants:
+            ms = statistics.median(res[v])
             gbs = 2 * size / (ms * 1e-3) / 1e9
-            print(json.dumps({"variant": variant, "size": size, "misalign": args.misalign,
-                              "us_per_launch": round(ms * 1e3, 2), "GBps_2S": round(gbs, 1),
-                              "frac_of_8TBps": round(gbs / 8000, 3)}), flush=True)
+            print(json.dumps({"variant": v[0], "unroll": v[1], "nt": v[2], "chunk": v[3],
+                              "size": size, "misalign": args.misalign,
+                              "us_per_launch": round(ms * 1e3, 2), "min_us": round(min(res[v]) * 1e3, 2),
+                              "GBps_2S": round(gbs, 1), "frac_of_8TBps": round(gbs / 8000, 3)}),
+                  flush=True)
         for p in plans:
             p.close()
         for b in srcs + dsts:
