@@ -49,6 +49,52 @@ def parse():
     return ap.parse_args()
 
 
+class Ranks:
+    """Cross-rank control for the weak-scaled replicas: barrier and max/sum of scalars over a
+    gloo (CPU) process group — the data path itself has no collective."""
+
+    def __init__(self, world: int):
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def _reduce(self, x: float, op) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.MAX) if self.dist else x
+
+    def sum(self, x: float) -> float:
+        return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist else x
+
+
+def pmc_traffic(msg_bytes: int):
+    """HBM bytes per pack launch from the newest committed PMC run for this message size
+    (profiles/*pack_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pack_pmc_traffic.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("algorithmic_bytes_per_launch") == 2 * msg_bytes:
+            best = (os.path.basename(p), d["traffic_bytes_per_launch"])
+    return best
+
+
 def cpu_baseline(rank_cores):
     """Reference shm path restated in C++ (oracle/shm_baseline.cpp), bounded sample."""
     exe = os.path.join(ROOT, "oracle", "build", "shm_baseline")
@@ -86,30 +132,8 @@ def main():
     ]}
     df = Dataflow(desc).start()
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def max_over_ranks(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum_over_ranks(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+    ranks = Ranks(world)
+    barrier, max_over_ranks, sum_over_ranks = ranks.barrier, ranks.max, ranks.sum
 
     from dora_amd import device
     from dora_amd.node import Node
@@ -200,6 +224,7 @@ def main():
 
     if rank != 0:
         return
+    traffic = pmc_traffic(S)
     lat = {}
     for s in sink.get("series", []):
         if s["input"] == "latency":
@@ -221,7 +246,8 @@ def main():
         "latency_us": lat,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "kernel": "pack_kernel",
+                     "traffic": traffic[1] if traffic else None,
+                     "traffic_source": traffic[0] if traffic else None, "kernel": "pack_kernel",
                      "avg_kernel_us": round(avg_pack_ms * 1e3, 3),
                      "algorithmic_bytes_per_launch": 2 * S},
         "parity": {"verified_msgs": verified, "mismatches": mismatches},

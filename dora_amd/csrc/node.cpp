@@ -51,7 +51,38 @@ struct Slot {
   uint64_t cap = 0;  // requested length (cache best-fit key, like Shmem::len)
   uint64_t id = 0;
   hipIpcMemHandle_t handle;
+  hipEvent_t done = nullptr;  // interprocess completion event of the slot's last fill
+  hipIpcEventHandle_t done_handle;
 };
+
+// Async sends (default): the sender records the slot's interprocess event after the pack and
+// sends at once; the receiver waits on that event before handing the input out.  Sync sends
+// synchronise the node stream before the descriptor leaves (DORA_GPU_SEND_MODE=sync).
+bool async_sends() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_SEND_MODE");
+    return !(e && std::string(e) == "sync");
+  }();
+  return v;
+}
+
+// Samples a node may have in flight (sent, token not yet back) before an allocation waits.
+size_t max_in_flight() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
+    long x = e ? std::atol(e) : 8;
+    return static_cast<size_t>(x > 0 ? x : 8);
+  }();
+  return v;
+}
+
+uint64_t slot_wait_ns() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_SLOT_WAIT_US");
+    return uint64_t(e ? std::atoll(e) : 5000) * 1000;
+  }();
+  return v;
+}
 
 std::vector<std::string> split(const char* s, char sep) {
   std::vector<std::string> out;
@@ -82,6 +113,7 @@ struct NodeCore {
   std::mutex req_mu;
   std::mutex ipc_mu;
   std::unordered_map<std::string, void*> ipc_cache;  // handle bytes -> mapped base
+  std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   std::unordered_map<uint64_t, Slot*> own_slots;       // for self-delivery
   std::mutex own_mu;
 
@@ -112,6 +144,7 @@ struct NodeCore {
   }
 
   ~NodeCore() {
+    for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -140,7 +173,17 @@ struct dora_sample {
   dora::Slot* slot = nullptr;
   std::vector<uint8_t> vec;  // zero-length samples (Vec path)
   uint64_t len = 0;
+  bool event_fill = false;  // filled by an async pack: completion = slot->done
 };
+
+namespace dora {
+// Kernel-duration stamps of async packs (hipExtLaunchKernel start/stop), harvested lazily.
+struct TimingPair {
+  hipEvent_t start = nullptr, stop = nullptr;
+  uint64_t bytes = 0;
+  bool pending = false;
+};
+}  // namespace dora
 
 struct dora_event {
   int type = 0;
@@ -162,7 +205,8 @@ struct dora_node {
   bool ended = false;
   // profiling of the pack kernel on the node stream
   bool profile = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<dora::TimingPair> timing;  // ring of kTimingPairs
+  size_t timing_next = 0;
   uint64_t pack_count = 0, pack_bytes = 0;
   double pack_ms = 0;
   uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
@@ -173,6 +217,10 @@ namespace {
 
 void free_slot(Slot* s) {
   if (!s) return;
+  if (s->done) {
+    (void)hipEventSynchronize(s->done);
+    (void)hipEventDestroy(s->done);
+  }
   (void)hipFree(s->ptr);
   delete s;
 }
@@ -227,7 +275,12 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   s->id = n->next_slot_id++;
   hipError_t e = hipMalloc(&s->ptr, (len + 4095) / 4096 * 4096);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
+  if (e == hipSuccess && async_sends()) {
+    e = hipEventCreateWithFlags(&s->done, hipEventInterprocess | hipEventDisableTiming);
+    if (e == hipSuccess) e = hipIpcGetEventHandle(&s->done_handle, s->done);
+  }
   if (e != hipSuccess) {
+    if (s->done) (void)hipEventDestroy(s->done);
     if (s->ptr) (void)hipFree(s->ptr);
     delete s;
     return fail(DORA_ERR_HIP, "device slot of %llu bytes: %s", (unsigned long long)len,
@@ -288,6 +341,38 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           }
         }
         if (base) in->ptr = static_cast<uint8_t*>(base) + d.ipc.offset;
+        if (base && d.ipc.has_event) {
+          // the producer's fill completes when its interprocess event fires
+          hipEvent_t fill = nullptr;
+          std::string key(reinterpret_cast<const char*>(d.ipc.event), 64);
+          {
+            std::lock_guard<std::mutex> g(n->core->ipc_mu);
+            auto it = n->core->ipc_events.find(key);
+            if (it != n->core->ipc_events.end()) {
+              fill = it->second;
+            } else {
+              hipIpcEventHandle_t h;
+              std::memcpy(&h, d.ipc.event, sizeof(h));
+              if (hipIpcOpenEventHandle(&fill, h) == hipSuccess) n->core->ipc_events[key] = fill;
+              else fill = nullptr;
+            }
+          }
+          // spin on the event (hipEventSynchronize sleeps in ~1 ms quanta on interprocess
+          // events that are not yet complete), then fall back to the blocking wait
+          hipError_t e = fill ? hipEventQuery(fill) : hipErrorInvalidHandle;
+          const uint64_t t0 = mono_ns();
+          while (e == hipErrorNotReady && mono_ns() - t0 < 20000000ull) {
+            __builtin_ia32_pause();
+            e = hipEventQuery(fill);
+          }
+          if (e == hipErrorNotReady) e = hipEventSynchronize(fill);
+          if (e != hipSuccess) {
+            ev->type = DORA_EVENT_ERROR;
+            ev->error = std::string("waiting for the producer's fill event: ") +
+                        hipGetErrorString(e);
+            in->ptr = nullptr;
+          }
+        }
       }
       ev->data = std::move(in);
       break;
@@ -374,6 +459,8 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.ipc.offset = 0;
       d.ipc.len = sample->len;
       d.ipc.token = generate_drop_token();
+      d.ipc.has_event = sample->event_fill ? 1 : 0;
+      if (sample->event_fill) std::memcpy(d.ipc.event, &slot->done_handle, 64);
     } else {
       d.kind = DATA_VEC;
       d.vec = std::move(sample->vec);
@@ -413,6 +500,18 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303
   s->len = len;
   if (len > 0) {
     handle_finished_drop_tokens(n);
+    // Async sends run ahead of the GPU; bound the samples in flight so the sender waits for a
+    // returned slot instead of hipMalloc-ing new ones (a device slot costs far more to create
+    // than a shm region).
+    // After `slot_wait_ns` without a returned token the slot is allocated anyway, as the
+    // reference would (a receiver may legitimately hold many inputs).
+    const uint64_t t0 = mono_ns();
+    while (async_sends() && n->sent_out.size() >= max_in_flight() &&
+           mono_ns() - t0 < slot_wait_ns()) {
+      n->core->drops.wait(1000);
+      handle_finished_drop_tokens(n);
+      if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
+    }
     int rc = allocate_slot(n, len, &s->slot);
     if (rc != DORA_OK) {
       delete s;
@@ -421,6 +520,43 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303
   }
   *out = s;
   return DORA_OK;
+}
+
+constexpr size_t kTimingPairs = 64;
+
+void harvest(dora_node* n, TimingPair& p) {
+  if (!p.pending) return;
+  float ms = 0;
+  if (hipEventSynchronize(p.stop) == hipSuccess &&
+      hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+    n->pack_ms += ms;
+    ++n->pack_count;
+    n->pack_bytes += p.bytes;
+  }
+  p.pending = false;
+}
+
+void harvest_all(dora_node* n) {
+  for (auto& p : n->timing) harvest(n, p);
+}
+
+int ensure_timing(dora_node* n) {
+  if (!n->timing.empty()) return DORA_OK;
+  n->timing.resize(kTimingPairs);
+  for (auto& p : n->timing) {
+    DORA_HIP(hipEventCreate(&p.start));
+    DORA_HIP(hipEventCreate(&p.stop));
+  }
+  return DORA_OK;
+}
+
+TimingPair* next_timing_pair(dora_node* n, uint64_t bytes) {
+  if (n->timing.empty()) return nullptr;
+  TimingPair& p = n->timing[n->timing_next++ % n->timing.size()];
+  harvest(n, p);  // normally long complete
+  p.bytes = bytes;
+  p.pending = true;
+  return &p;
 }
 
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
@@ -438,28 +574,29 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   } else if (plan->size) {
     hipStream_t st = n->core->stream;
     const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU;
+    TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
     rc = launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
-                     static_cast<uint8_t*>(s->slot->ptr), st, timed ? n->ev0 : nullptr,
-                     timed ? n->ev1 : nullptr);
+                     static_cast<uint8_t*>(s->slot->ptr), st, tp ? tp->start : nullptr,
+                     tp ? tp->stop : nullptr);
     if (rc != DORA_OK) {
+      if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
       delete s;
       return rc;
     }
-    // the sample must be complete before its descriptor leaves the process
-    hipError_t e = hipStreamSynchronize(st);
+    hipError_t e;
+    if (s->slot->done) {
+      // async: the receiver waits on the slot's interprocess event, the sender moves on
+      e = hipEventRecord(s->slot->done, st);
+      s->event_fill = true;
+    } else {
+      // sync: the sample must be complete before its descriptor leaves the process
+      e = hipStreamSynchronize(st);
+    }
     if (e != hipSuccess) {
       add_to_cache(n, s->slot);
       delete s;
       return fail(DORA_ERR_HIP, "pack: %s", hipGetErrorString(e));
-    }
-    if (timed) {
-      float ms = 0;
-      if (hipEventElapsedTime(&ms, n->ev0, n->ev1) == hipSuccess) {
-        n->pack_ms += ms;
-        ++n->pack_count;
-        n->pack_bytes += plan->size;
-      }
     }
   }
   std::vector<uint8_t> ti;
@@ -508,11 +645,8 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     n->queue_size[kv.substr(0, eq)] = static_cast<uint32_t>(std::stoul(kv.substr(eq + 1)));
   }
   const char* prof = std::getenv("DORA_GPU_PROFILE_PACK");
-  if (prof && *prof && *prof != '0') {
-    n->profile = true;
-    (void)hipEventCreate(&n->ev0);
-    (void)hipEventCreate(&n->ev1);
-  }
+  if (prof && *prof && *prof != '0' && device >= 0)
+    n->profile = dora::ensure_timing(n) == DORA_OK;
   // Subscribe and wait for AllNodesReady (event_stream/mod.rs:37-118, daemon PendingNodes)
   int rc = core->request(dora::REQ_SUBSCRIBE, {});
   if (rc != DORA_OK) {
@@ -569,8 +703,11 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
   for (auto& kv : n->sent_out) dora::free_slot(kv.second);
   for (auto* s : n->cache) dora::free_slot(s);
-  if (n->ev0) (void)hipEventDestroy(n->ev0);
-  if (n->ev1) (void)hipEventDestroy(n->ev1);
+  dora::harvest_all(n);
+  for (auto& p : n->timing) {
+    (void)hipEventDestroy(p.start);
+    (void)hipEventDestroy(p.stop);
+  }
   delete n;
 }
 
@@ -740,6 +877,7 @@ int dora_node_stats(dora_node* n, uint64_t* slots_created, uint64_t* cache_hits,
 
 int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64_t* bytes) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  dora::harvest_all(n);  // waits for the stamps of packs still in flight
   if (count) *count = n->pack_count;
   if (total_ms) *total_ms = n->pack_ms;
   if (bytes) *bytes = n->pack_bytes;
@@ -748,10 +886,12 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
 
 int dora_node_set_profiling(dora_node* n, int enable) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
-  if (enable && !n->ev0) {
-    DORA_HIP(hipEventCreate(&n->ev0));
-    DORA_HIP(hipEventCreate(&n->ev1));
+  if (enable) {
+    if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
+    int rc = dora::ensure_timing(n);
+    if (rc != DORA_OK) return rc;
   }
+  dora::harvest_all(n);
   n->profile = enable != 0;
   n->pack_count = 0;
   n->pack_ms = 0;

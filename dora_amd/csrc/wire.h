@@ -53,6 +53,8 @@ struct DeviceIpc {
   uint64_t offset;     // sample offset inside the slot allocation
   uint64_t len;
   DropToken token;
+  uint8_t has_event;     // 1: the fill completes when `event` fires (hipEventInterprocess)
+  uint8_t event[64];     // hipIpcEventHandle_t of the slot's completion event
 };
 
 struct DataMsg {
@@ -99,6 +101,8 @@ class WBuf {
       u64(d.ipc.offset);
       u64(d.ipc.len);
       token(d.ipc.token);
+      u8(d.ipc.has_event);
+      if (d.ipc.has_event) raw(d.ipc.event, 64);
     }
   }
   void metadata(const Metadata& m) {
@@ -177,6 +181,8 @@ class RBuf {
       d.ipc.offset = u64();
       d.ipc.len = u64();
       d.ipc.token = token();
+      d.ipc.has_event = u8();
+      if (d.ipc.has_event) raw(d.ipc.event, 64);
     }
     if (d.kind > DATA_DEVICE_IPC) throw std::invalid_argument("unknown DataMessage kind");
     return d;
