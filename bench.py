@@ -211,6 +211,7 @@ def main():
     barrier()
     pack = node.pack_stats()
     stats = node.stats()
+    stats["send_phase_us"] = {k: round(v, 2) for k, v in node.send_profile().items()}
     node.close()
     codes = df.wait(120)
     df.stop()
@@ -251,6 +252,7 @@ def main():
                      "avg_kernel_us": round(avg_pack_ms * 1e3, 3),
                      "algorithmic_bytes_per_launch": 2 * S},
         "parity": {"verified_msgs": verified, "mismatches": mismatches},
+        "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
         "node_stats": stats, "exit_codes": codes,
     }
     if base is not None:

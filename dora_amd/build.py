@@ -19,7 +19,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
 LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp",
-               "wire.cpp", "daemon.cpp", "node.cpp"]
+               "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp"]
 LIB_NAME = "libdora_gpu.so"
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",

@@ -27,6 +27,7 @@
 #include "common.h"
 #include "dora_gpu.h"
 #include "shm.h"
+#include "trace.h"
 #include "wire.h"
 
 namespace dora {
@@ -286,6 +287,7 @@ class Daemon {
         w.bytes(meta);
         w.data(data);
         push_event(rc.node, EV_INPUT, std::move(w.b));
+        if (data.has_token()) trace(TP_ROUTED, data.ipc.token);
         if (data.has_token()) {
           auto& ti = tokens_[data.ipc.token];
           ti.owner = i;
@@ -306,6 +308,7 @@ class Daemon {
     const int owner = it->second.owner;
     tokens_.erase(it);
     push_drop(owner, t);
+    trace(TP_TOKEN_DONE, t);
   }
 
   void close_output(int i, const std::string& output) {
@@ -379,6 +382,7 @@ int dora_daemon_create(const char* shm_name, const char* spec, size_t ring_bytes
   DORA_GUARD_BEGIN
   auto* d = new dora_daemon();
   d->d.reset(new dora::Daemon(shm_name, spec, ring_bytes ? ring_bytes : (4u << 20)));
+  dora::trace_set_name("daemon");
   *out = d;
   return DORA_OK;
   DORA_GUARD_END
@@ -406,6 +410,9 @@ int dora_daemon_stats(dora_daemon* d, uint64_t* routed, uint64_t* pending_tokens
   return DORA_OK;
 }
 
-void dora_daemon_free(dora_daemon* d) { delete d; }
+void dora_daemon_free(dora_daemon* d) {
+  delete d;
+  dora::trace_flush();
+}
 
 }  // extern "C"

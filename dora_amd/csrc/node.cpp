@@ -34,6 +34,7 @@
 #include "dora_gpu.h"
 #include "plan.h"
 #include "shm.h"
+#include "trace.h"
 #include "wire.h"
 
 namespace dora {
@@ -51,7 +52,8 @@ struct Slot {
   uint64_t cap = 0;  // requested length (cache best-fit key, like Shmem::len)
   uint64_t id = 0;
   hipIpcMemHandle_t handle;
-  hipEvent_t done = nullptr;  // interprocess completion event of the slot's last fill
+  int flag = -1;              // FillFlag index in the node's region entry (async sends)
+  hipEvent_t done = nullptr;  // fallback: interprocess completion event of the last fill
   hipIpcEventHandle_t done_handle;
 };
 
@@ -116,6 +118,15 @@ struct NodeCore {
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   std::unordered_map<uint64_t, Slot*> own_slots;       // for self-delivery
   std::mutex own_mu;
+  // fill flags: the region is host-registered so the stream can write epochs into it
+  uint8_t* region_dev = nullptr;
+  std::vector<uint32_t> free_flags;
+  uint64_t epoch = 0;
+
+  uint64_t* flag_dev(int idx) const {
+    const uint8_t* host = reinterpret_cast<const uint8_t*>(&region->hdr()->nodes[this->idx].fill[idx]);
+    return reinterpret_cast<uint64_t*>(region_dev + (host - region->base()));
+  }
 
   void ring_doorbell() {
     RegionHdr* h = region->hdr();
@@ -146,6 +157,8 @@ struct NodeCore {
   ~NodeCore() {
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (region_dev) (void)hipHostUnregister(region->base());
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -161,8 +174,10 @@ struct InputData {
   ~InputData() {
     if (has_token && core) {
       // consumer reads on the node stream must be complete before the owner may reuse the slot
-      if (core->stream) (void)hipStreamSynchronize(core->stream);
+      if (core->stream && hipStreamQuery(core->stream) != hipSuccess)
+        (void)hipStreamSynchronize(core->stream);
       core->report_drop_token(token);
+      trace(TP_RELEASED, token);
     }
   }
 };
@@ -173,7 +188,8 @@ struct dora_sample {
   dora::Slot* slot = nullptr;
   std::vector<uint8_t> vec;  // zero-length samples (Vec path)
   uint64_t len = 0;
-  bool event_fill = false;  // filled by an async pack: completion = slot->done
+  uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
+  uint64_t epoch = 0;
 };
 
 namespace dora {
@@ -210,13 +226,17 @@ struct dora_node {
   uint64_t pack_count = 0, pack_bytes = 0;
   double pack_ms = 0;
   uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
+  // host time per send phase: allocate (incl. backpressure), launch, fill sync/record, send
+  uint64_t phase_ns[4] = {0, 0, 0, 0};
+  uint64_t phase_count = 0;
 };
 
 namespace dora {
 namespace {
 
-void free_slot(Slot* s) {
+void free_slot(dora_node* n, Slot* s) {
   if (!s) return;
+  if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
   if (s->done) {
     (void)hipEventSynchronize(s->done);
     (void)hipEventDestroy(s->done);
@@ -234,11 +254,12 @@ void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
       std::lock_guard<std::mutex> g(n->core->own_mu);
       n->core->own_slots.erase(old->id);
     }
-    free_slot(old);
+    free_slot(n, old);
   }
 }
 
 void on_token(dora_node* n, const DropToken& t) {
+  trace(TP_TOKEN_BACK, t);
   auto it = n->sent_out.find(t);
   if (it == n->sent_out.end()) return;  // "received unknown finished drop token"
   Slot* s = it->second;
@@ -276,10 +297,16 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   hipError_t e = hipMalloc(&s->ptr, (len + 4095) / 4096 * 4096);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
   if (e == hipSuccess && async_sends()) {
-    e = hipEventCreateWithFlags(&s->done, hipEventInterprocess | hipEventDisableTiming);
-    if (e == hipSuccess) e = hipIpcGetEventHandle(&s->done_handle, s->done);
+    if (n->core->region_dev && !n->core->free_flags.empty()) {
+      s->flag = static_cast<int>(n->core->free_flags.back());
+      n->core->free_flags.pop_back();
+    } else {
+      e = hipEventCreateWithFlags(&s->done, hipEventInterprocess | hipEventDisableTiming);
+      if (e == hipSuccess) e = hipIpcGetEventHandle(&s->done_handle, s->done);
+    }
   }
   if (e != hipSuccess) {
+    if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
     if (s->done) (void)hipEventDestroy(s->done);
     if (s->ptr) (void)hipFree(s->ptr);
     delete s;
@@ -315,6 +342,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
       } else if (d.kind == DATA_DEVICE_IPC) {
         in->has_token = true;  // set first: a mapping failure still returns the token
         in->token = d.ipc.token;
+        trace(TP_POPPED, in->token);
         in->len = d.ipc.len;
         void* base = nullptr;
         if (d.ipc.owner_pid == getpid()) {
@@ -341,7 +369,33 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           }
         }
         if (base) in->ptr = static_cast<uint8_t*>(base) + d.ipc.offset;
-        if (base && d.ipc.has_event) {
+        if (base && d.ipc.fill == FILL_FLAG) {
+          // the producer's stream writes the epoch into its fill flag after the pack: poll it
+          RegionHdr* h = n->core->region->hdr();
+          if (d.ipc.flag_node >= h->n_nodes || d.ipc.flag_index >= kFillFlags) {
+            ev->type = DORA_EVENT_ERROR;
+            ev->error = "fill flag out of range";
+            in->ptr = nullptr;
+          } else {
+            const std::atomic<uint64_t>& f = h->nodes[d.ipc.flag_node].fill[d.ipc.flag_index].epoch;
+            const uint64_t t0 = mono_ns();
+            unsigned spins = 0;
+            while (f.load(std::memory_order_acquire) < d.ipc.epoch) {
+              if (++spins < 4096) {
+                __builtin_ia32_pause();
+                continue;
+              }
+              spins = 0;
+              if (mono_ns() - t0 > 60000000000ull) {
+                ev->type = DORA_EVENT_ERROR;
+                ev->error = "the producer's fill did not complete within 60 s";
+                in->ptr = nullptr;
+                break;
+              }
+              if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
+            }
+          }
+        } else if (base && d.ipc.fill == FILL_EVENT) {
           // the producer's fill completes when its interprocess event fires
           hipEvent_t fill = nullptr;
           std::string key(reinterpret_cast<const char*>(d.ipc.event), 64);
@@ -374,6 +428,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           }
         }
       }
+      if (in->has_token) trace(TP_FILLED, in->token);
       ev->data = std::move(in);
       break;
     }
@@ -436,7 +491,8 @@ std::vector<uint8_t> encode_metadata(const std::vector<uint8_t>& ti, const uint8
 }
 
 int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
-                const uint8_t* params, size_t params_len, dora_sample* sample) {
+                const uint8_t* params, size_t params_len, dora_sample* sample,
+                DropToken* token_out = nullptr) {
   handle_finished_drop_tokens(n);
   if (!n->outputs.count(output_id)) {
     delete sample;  // the sample is consumed either way
@@ -459,8 +515,13 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.ipc.offset = 0;
       d.ipc.len = sample->len;
       d.ipc.token = generate_drop_token();
-      d.ipc.has_event = sample->event_fill ? 1 : 0;
-      if (sample->event_fill) std::memcpy(d.ipc.event, &slot->done_handle, 64);
+      d.ipc.fill = sample->fill;
+      if (sample->fill == FILL_FLAG) {
+        d.ipc.flag_node = static_cast<uint32_t>(n->core->idx);
+        d.ipc.flag_index = static_cast<uint32_t>(slot->flag);
+        d.ipc.epoch = sample->epoch;
+      }
+      if (sample->fill == FILL_EVENT) std::memcpy(d.ipc.event, &slot->done_handle, 64);
     } else {
       d.kind = DATA_VEC;
       d.vec = std::move(sample->vec);
@@ -476,7 +537,11 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     if (slot) add_to_cache(n, slot);
     return rc;
   }
-  if (slot) n->sent_out[d.ipc.token] = slot;
+  if (slot) {
+    n->sent_out[d.ipc.token] = slot;
+    if (token_out) *token_out = d.ipc.token;
+    trace(TP_SENT, d.ipc.token);
+  }
   return DORA_OK;
 }
 
@@ -562,8 +627,11 @@ TimingPair* next_timing_pair(dora_node* n, uint64_t bytes) {
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
                   size_t params_len) {
   dora_sample* s = nullptr;
+  const uint64_t t0 = mono_ns();
   int rc = alloc_sample(n, plan->size, &s);
   if (rc != DORA_OK) return rc;
+  const uint64_t t1 = mono_ns();
+  uint64_t t2 = t1, t3 = t1;
   if (plan->size && !s->slot) {
     // host-only node: small host payload copied into the inline Vec (arrow_utils.rs:48)
     if (plan->dev == ARROW_DEVICE_ROCM) {
@@ -584,11 +652,18 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       delete s;
       return rc;
     }
+    t2 = mono_ns();
     hipError_t e;
-    if (s->slot->done) {
-      // async: the receiver waits on the slot's interprocess event, the sender moves on
+    if (s->slot->flag >= 0) {
+      // async: the stream writes the send epoch into the slot's fill flag once the pack has
+      // completed; the receiver polls it, the sender moves on
+      s->epoch = ++n->core->epoch;
+      e = hipStreamWriteValue64(st, n->core->flag_dev(s->slot->flag), s->epoch, 0);
+      s->fill = FILL_FLAG;
+    } else if (s->slot->done) {
+      // async fallback: interprocess event
       e = hipEventRecord(s->slot->done, st);
-      s->event_fill = true;
+      s->fill = FILL_EVENT;
     } else {
       // sync: the sample must be complete before its descriptor leaves the process
       e = hipStreamSynchronize(st);
@@ -598,10 +673,27 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       delete s;
       return fail(DORA_ERR_HIP, "pack: %s", hipGetErrorString(e));
     }
+    t3 = mono_ns();
   }
   std::vector<uint8_t> ti;
   serialize_type_info(plan->root, ti);
-  return send_sample(n, output_id, ti, params, params_len, s);
+  DropToken tok{};
+  const bool traced = trace_enabled() && s->slot;
+  rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
+  const uint64_t t4 = mono_ns();
+  if (traced && rc == DORA_OK) {
+    const uint64_t off = now_ns() - mono_ns();  // mono -> realtime for the trace
+    trace_at(TP_ALLOC_BEGIN, tok, t0 + off);
+    trace_at(TP_ALLOC_END, tok, t1 + off);
+    trace_at(TP_LAUNCHED, tok, t2 + off);
+    trace_at(TP_FILL_ORDERED, tok, t3 + off);
+  }
+  n->phase_ns[0] += t1 - t0;
+  n->phase_ns[1] += t2 - t1;
+  n->phase_ns[2] += t3 - t2;
+  n->phase_ns[3] += t4 - t3;
+  ++n->phase_count;
+  return rc;
 }
 
 }  // namespace
@@ -631,9 +723,22 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   core->ev = dora::RingReader(core->region.get(), &e.events);
   core->drops = dora::RingReader(core->region.get(), &e.drops);
   core->device = device;
+  dora::trace_set_name(node_id);
   if (device >= 0) {  // device < 0: host-only node (control plane + inline Vec samples only)
     DORA_HIP(hipSetDevice(device));
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
+    if (dora::async_sends()) {
+      // host-register the control region so this node's stream can write fill epochs into it
+      void* dev = nullptr;
+      if (hipHostRegister(core->region->base(), core->region->size(), hipHostRegisterMapped) ==
+              hipSuccess &&
+          hipHostGetDevicePointer(&dev, core->region->base(), 0) == hipSuccess) {
+        core->region_dev = static_cast<uint8_t*>(dev);
+        for (uint32_t k = dora::kFillFlags; k-- > 0;) core->free_flags.push_back(k);
+      } else {
+        (void)hipGetLastError();  // fall back to interprocess events
+      }
+    }
   }
 
   auto* n = new dora_node();
@@ -686,6 +791,9 @@ int dora_node_init_from_env(dora_node** out) {
 
 void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   if (!n) return;
+  struct Flush {
+    ~Flush() { dora::trace_flush(); }
+  } flush_trace_at_end;
   std::vector<std::string> outs(n->outputs.begin(), n->outputs.end());
   dora::WBuf w;
   w.u32(static_cast<uint32_t>(outs.size()));
@@ -701,8 +809,8 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
   }
   (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
-  for (auto& kv : n->sent_out) dora::free_slot(kv.second);
-  for (auto* s : n->cache) dora::free_slot(s);
+  for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
+  for (auto* s : n->cache) dora::free_slot(n, s);
   dora::harvest_all(n);
   for (auto& p : n->timing) {
     (void)hipEventDestroy(p.start);
@@ -884,6 +992,14 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
   return DORA_OK;
 }
 
+int dora_node_send_profile(dora_node* n, double* out_us, size_t n_out, uint64_t* count) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  const double c = n->phase_count ? double(n->phase_count) : 1.0;
+  for (size_t i = 0; i < n_out && i < 4; ++i) out_us[i] = double(n->phase_ns[i]) / c / 1000.0;
+  if (count) *count = n->phase_count;
+  return DORA_OK;
+}
+
 int dora_node_set_profiling(dora_node* n, int enable) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (enable) {
@@ -893,6 +1009,8 @@ int dora_node_set_profiling(dora_node* n, int enable) {
   }
   dora::harvest_all(n);
   n->profile = enable != 0;
+  for (auto& x : n->phase_ns) x = 0;
+  n->phase_count = 0;
   n->pack_count = 0;
   n->pack_ms = 0;
   n->pack_bytes = 0;

@@ -34,8 +34,17 @@ struct RingHdr {
 };
 
 constexpr size_t kListLen = 2048;
+constexpr uint32_t kFillFlags = 64;  // per node: one per live device slot
+
+// A fill-completion word: the owner's stream writes the send epoch here (hipStreamWriteValue64
+// into the host-registered region) once the pack that filled the slot has completed; receivers
+// poll it with plain loads.  One cache line each.
+struct FillFlag {
+  alignas(64) std::atomic<uint64_t> epoch;
+};
 
 struct NodeEntry {
+  FillFlag fill[kFillFlags];
   char id[kIdLen];
   char outputs[kListLen];  // "out1,out2"           (NodeRunConfig.outputs)
   char inputs[kListLen];   // "in1=10,in2=1"        (input id = queue_size)
@@ -70,6 +79,7 @@ class Region {
   uint8_t* base() const { return reinterpret_cast<uint8_t*>(hdr_); }
   int node_index(const std::string& id) const;
   void unlink();
+  size_t size() const { return size_; }
   const std::string& name() const { return name_; }
 
  private:

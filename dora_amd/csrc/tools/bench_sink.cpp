@@ -36,6 +36,12 @@ double mean(const std::vector<double>& v) {
   return v.empty() ? 0 : s / v.size();
 }
 
+uint64_t mono() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
 uint64_t now_ns() {
   timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
@@ -58,9 +64,12 @@ int main() {
   dora_gpu_malloc(reinterpret_cast<void**>(&csum_dev), 8);
   dora_stream_t st = dora_node_stream(node);
   int errors = 0;
+  uint64_t t_next = 0, t_free = 0, n_inputs = 0;
   for (;;) {
     dora_event* ev = nullptr;
+    const uint64_t tn0 = mono();
     int rc = dora_node_next_event(node, -1, &ev);
+    t_next += mono() - tn0;
     if (rc != 0) break;
     const int type = dora_event_type(ev);
     if (type == DORA_EVENT_INPUT) {
@@ -93,7 +102,10 @@ int main() {
       }
       const bool ack = params.count("ack") != 0;
       const int64_t seq = params.count("seq") ? params["seq"].i : -1;
+      const uint64_t tf0 = mono();
       dora_event_free(ev);  // zero-copy consumer done: token goes back to the sender
+      t_free += mono() - tf0;
+      ++n_inputs;
       if (ack) {
         std::map<std::string, Param> ap;
         ap["seq"].i = seq;
@@ -117,8 +129,12 @@ int main() {
   uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
   dora_node_stats(node, &slots, &hits, &inflight, &dropped);
   FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
-  std::fprintf(f, "{\"errors\": %d, \"dropped_inputs\": %llu, \"series\": [", errors,
-               (unsigned long long)dropped);
+  std::fprintf(f,
+               "{\"errors\": %d, \"dropped_inputs\": %llu, \"next_event_us\": %.3f, "
+               "\"free_us\": %.3f, \"series\": [",
+               errors, (unsigned long long)dropped,
+               n_inputs ? double(t_next) / n_inputs / 1000.0 : 0.0,
+               n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0);
   bool first = true;
   for (auto& kv : stats) {
     Series& s = kv.second;

@@ -1,0 +1,34 @@
+// Lightweight per-process message tracing (the data-plane part of the reference's tracing spans,
+// libraries/extensions/telemetry/tracing): when DORA_GPU_TRACE=<dir> is set, every send /
+// route / receive / release of a sample is stamped (CLOCK_REALTIME ns, keyed by drop token) into
+// a preallocated buffer and written to <dir>/<who>-<pid>.trace.csv at exit.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "wire.h"
+
+namespace dora {
+
+enum TracePoint : uint8_t {
+  TP_ALLOC_BEGIN = 1,  // sender: allocate_data_sample entered
+  TP_ALLOC_END,        // sender: slot in hand
+  TP_LAUNCHED,         // sender: pack kernel enqueued
+  TP_FILL_ORDERED,     // sender: fill flag / event / sync issued
+  TP_SENT,             // sender: descriptor pushed to the daemon
+  TP_TOKEN_BACK,       // sender: OutputDropped received
+  TP_ROUTED,           // daemon: Input pushed to a receiver
+  TP_TOKEN_DONE,       // daemon: token complete, OutputDropped pushed
+  TP_POPPED,           // receiver: event popped from the ring
+  TP_FILLED,           // receiver: fill observed complete
+  TP_RELEASED,         // receiver: drop token reported
+};
+
+bool trace_enabled();
+void trace(TracePoint p, const DropToken& t);
+void trace_at(TracePoint p, const DropToken& t, uint64_t t_ns);
+void trace_set_name(const std::string& who);
+void trace_flush();
+
+}  // namespace dora

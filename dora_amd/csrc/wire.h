@@ -53,9 +53,16 @@ struct DeviceIpc {
   uint64_t offset;     // sample offset inside the slot allocation
   uint64_t len;
   DropToken token;
-  uint8_t has_event;     // 1: the fill completes when `event` fires (hipEventInterprocess)
-  uint8_t event[64];     // hipIpcEventHandle_t of the slot's completion event
+  // How the receiver learns that the fill is complete:
+  //   FILL_DONE  the sender synchronised before sending;
+  //   FILL_FLAG  poll region node `flag_node`'s FillFlag[flag_index] until >= epoch;
+  //   FILL_EVENT wait on the interprocess event `event` (fallback when no flag is free).
+  uint8_t fill = 0;
+  uint32_t flag_node = 0, flag_index = 0;
+  uint64_t epoch = 0;
+  uint8_t event[64];  // hipIpcEventHandle_t
 };
+enum : uint8_t { FILL_DONE = 0, FILL_FLAG = 1, FILL_EVENT = 2 };
 
 struct DataMsg {
   uint8_t kind = DATA_NONE;
@@ -101,8 +108,13 @@ class WBuf {
       u64(d.ipc.offset);
       u64(d.ipc.len);
       token(d.ipc.token);
-      u8(d.ipc.has_event);
-      if (d.ipc.has_event) raw(d.ipc.event, 64);
+      u8(d.ipc.fill);
+      if (d.ipc.fill == FILL_FLAG) {
+        u32(d.ipc.flag_node);
+        u32(d.ipc.flag_index);
+        u64(d.ipc.epoch);
+      }
+      if (d.ipc.fill == FILL_EVENT) raw(d.ipc.event, 64);
     }
   }
   void metadata(const Metadata& m) {
@@ -181,8 +193,14 @@ class RBuf {
       d.ipc.offset = u64();
       d.ipc.len = u64();
       d.ipc.token = token();
-      d.ipc.has_event = u8();
-      if (d.ipc.has_event) raw(d.ipc.event, 64);
+      d.ipc.fill = u8();
+      if (d.ipc.fill == FILL_FLAG) {
+        d.ipc.flag_node = u32();
+        d.ipc.flag_index = u32();
+        d.ipc.epoch = u64();
+      }
+      if (d.ipc.fill == FILL_EVENT) raw(d.ipc.event, 64);
+      if (d.ipc.fill > FILL_EVENT) throw std::invalid_argument("unknown fill kind");
     }
     if (d.kind > DATA_DEVICE_IPC) throw std::invalid_argument("unknown DataMessage kind");
     return d;

@@ -215,6 +215,12 @@ class Node:
         call("dora_node_pack_stats", self.handle, byref(c), byref(ms), byref(b))
         return {"count": c.value, "total_ms": ms.value, "bytes": b.value}
 
+    def send_profile(self) -> dict:
+        out, cnt = (c_double * 4)(), c_uint64()
+        call("dora_node_send_profile", self.handle, out, 4, byref(cnt))
+        return {"alloc_us": out[0], "launch_us": out[1], "fill_us": out[2], "send_us": out[3],
+                "count": cnt.value}
+
     def close(self):
         if self.handle:
             self._lib.dora_node_free(self.handle)

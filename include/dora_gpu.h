@@ -270,6 +270,9 @@ int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hi
 /* Pack-kernel timing on the node stream (HIP events around every pack launch). */
 int dora_node_set_profiling(dora_node* node, int enable);
 int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);
+/* Mean host time (µs) per send phase since profiling was (re)enabled: [0] allocate incl.
+ * backpressure, [1] pack launch, [2] fill event record / stream sync, [3] descriptor send. */
+int dora_node_send_profile(dora_node* node, double* out_us, size_t n_out, uint64_t* count);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Daemon — the data-plane part of binaries/daemon (send_out, drop tokens, input closing)     */
