@@ -110,6 +110,7 @@ _SIGS = {
     "dora_node_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
                                 POINTER(c_uint64)]),
     "dora_node_set_profiling": (c_int, [c_void_p, c_int]),
+    "dora_node_peer_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_send_profile": (c_int, [c_void_p, POINTER(c_double), c_size_t, POINTER(c_uint64)]),
     "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),
                                      POINTER(c_uint64)]),

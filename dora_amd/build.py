@@ -79,6 +79,7 @@ def build(verbose: bool = False) -> str:
 TOOLS = {  # binary name -> sources (linked against libdora_gpu.so, rpath $ORIGIN)
     "dora-gpu-daemon": ["tools/daemon_main.cpp"],
     "dora-gpu-bench-sink": ["tools/bench_sink.cpp"],
+    "dora-gpu-relay": ["tools/relay.cpp"],
 }
 
 

@@ -78,6 +78,15 @@ size_t max_in_flight() {
   return v;
 }
 
+// Force the cross-GPU copy path on same-GPU edges (tests on a one-GPU box).
+bool edge_copy_forced() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_EDGE_COPY");
+    return e && *e && *e != '0';
+  }();
+  return v;
+}
+
 uint64_t slot_wait_ns() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_SLOT_WAIT_US");
@@ -123,6 +132,39 @@ struct NodeCore {
   std::vector<uint32_t> free_flags;
   uint64_t epoch = 0;
 
+  // Receive pool for cross-GPU edges: local HBM copies of remote samples, recycled by size.
+  std::mutex pool_mu;
+  std::multimap<uint64_t, void*> recv_pool;
+  static constexpr size_t kMaxPooled = 16;
+
+  void* recv_pool_get(uint64_t len, uint64_t* cap) {
+    {
+      std::lock_guard<std::mutex> g(pool_mu);
+      auto it = recv_pool.lower_bound(len);
+      if (it != recv_pool.end() && it->first <= 2 * len + 4096) {
+        void* p = it->second;
+        *cap = it->first;
+        recv_pool.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    const uint64_t c = (len + 4095) / 4096 * 4096;
+    if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+    *cap = c;
+    return p;
+  }
+
+  void recv_pool_put(void* p, uint64_t cap) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    if (recv_pool.size() >= kMaxPooled) {
+      auto it = recv_pool.begin();  // evict the smallest
+      (void)hipFree(it->second);
+      recv_pool.erase(it);
+    }
+    recv_pool.emplace(cap, p);
+  }
+
   uint64_t* flag_dev(int idx) const {
     const uint8_t* host = reinterpret_cast<const uint8_t*>(&region->hdr()->nodes[this->idx].fill[idx]);
     return reinterpret_cast<uint64_t*>(region_dev + (host - region->base()));
@@ -158,6 +200,7 @@ struct NodeCore {
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
     if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& kv : recv_pool) (void)hipFree(kv.second);
     if (region_dev) (void)hipHostUnregister(region->base());
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -170,15 +213,21 @@ struct InputData {
   uint64_t len = 0;
   bool has_token = false;
   DropToken token{};
-  std::vector<uint8_t> vec;  // inline (Vec) samples stay on the host
+  std::vector<uint8_t> vec;   // inline (Vec) samples stay on the host
+  void* local = nullptr;      // cross-GPU edge: local copy in this node's receive pool
+  uint64_t local_cap = 0;
   ~InputData() {
-    if (has_token && core) {
-      // consumer reads on the node stream must be complete before the owner may reuse the slot
+    if (!core) return;
+    if (has_token || local) {
+      // consumer reads on the node stream must be complete before the memory is reused
       if (core->stream && hipStreamQuery(core->stream) != hipSuccess)
         (void)hipStreamSynchronize(core->stream);
+    }
+    if (has_token) {
       core->report_drop_token(token);
       trace(TP_RELEASED, token);
     }
+    if (local) core->recv_pool_put(local, local_cap);
   }
 };
 
@@ -229,6 +278,7 @@ struct dora_node {
   // host time per send phase: allocate (incl. backpressure), launch, fill sync/record, send
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
+  uint64_t peer_copies = 0, peer_bytes = 0;  // cross-GPU edges pulled into local slots
 };
 
 namespace dora {
@@ -429,6 +479,32 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         }
       }
       if (in->has_token) trace(TP_FILLED, in->token);
+      if (in->has_token && in->ptr && in->len &&
+          (d.ipc.device != n->core->device || edge_copy_forced())) {
+        // Cross-GPU edge: pull the sample over xGMI into a local slot with one
+        // peer copy on the node stream, then hand the producer its slot back at once.
+        uint64_t cap = 0;
+        void* local = n->core->recv_pool_get(in->len, &cap);
+        hipError_t e = local ? hipMemcpyPeerAsync(local, n->core->device, in->ptr, d.ipc.device,
+                                                  in->len, n->core->stream)
+                             : hipErrorOutOfMemory;
+        if (e == hipSuccess) e = hipStreamSynchronize(n->core->stream);
+        if (e != hipSuccess) {
+          if (local) n->core->recv_pool_put(local, cap);
+          ev->type = DORA_EVENT_ERROR;
+          ev->error = std::string("cross-GPU peer copy: ") + hipGetErrorString(e);
+          in->ptr = nullptr;
+        } else {
+          in->local = local;
+          in->local_cap = cap;
+          in->ptr = local;
+          n->core->report_drop_token(in->token);
+          trace(TP_RELEASED, in->token);
+          in->has_token = false;
+          ++n->peer_copies;
+          n->peer_bytes += in->len;
+        }
+      }
       ev->data = std::move(in);
       break;
     }
@@ -989,6 +1065,13 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
   if (count) *count = n->pack_count;
   if (total_ms) *total_ms = n->pack_ms;
   if (bytes) *bytes = n->pack_bytes;
+  return DORA_OK;
+}
+
+int dora_node_peer_stats(dora_node* n, uint64_t* copies, uint64_t* bytes) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (copies) *copies = n->peer_copies;
+  if (bytes) *bytes = n->peer_bytes;
   return DORA_OK;
 }
 

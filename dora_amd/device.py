@@ -140,6 +140,20 @@ class DeviceArray:
     def length(self) -> int:
         return self.array.length
 
+    # DLPack (kDLROCM): zero-copy hand-off of fixed-width device samples to torch & co.
+    def __dlpack__(self, stream=None, **kwargs):
+        from .dlpack import to_dlpack_capsule, values_view
+        ptr, n, fmt = values_view(self)
+        return to_dlpack_capsule(ptr, n, fmt, self.device_id, self)
+
+    def __dlpack_device__(self):
+        from .dlpack import kDLROCM
+        return (kDLROCM, self.device_id)
+
+    @property
+    def device_id(self) -> int:
+        return getattr(self, "_device_id", 0)
+
     def close(self):
         release_array(self.array)
         self._keepalive = None

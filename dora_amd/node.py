@@ -184,6 +184,7 @@ class Node:
                 t = pa.DataType._import_from_c(ctypes.addressof(s))
                 # the array keeps the input alive; the event handle can go
                 out["value"] = DeviceArray(a, t)
+                out["value"]._device_id = self.device
             else:   # inline DataMessage::Vec sample of a host-only node
                 out["value"] = ctypes.string_at(dp.value, dn.value) if dn.value else b""
         out["_event"] = ev
@@ -204,8 +205,12 @@ class Node:
     def stats(self) -> dict:
         v = [c_uint64() for _ in range(4)]
         call("dora_node_stats", self.handle, *[byref(x) for x in v])
-        return dict(zip(["slots_created", "cache_hits", "in_flight", "dropped_inputs"],
-                        [x.value for x in v]))
+        out = dict(zip(["slots_created", "cache_hits", "in_flight", "dropped_inputs"],
+                       [x.value for x in v]))
+        c, b = c_uint64(), c_uint64()
+        call("dora_node_peer_stats", self.handle, byref(c), byref(b))
+        out["peer_copies"], out["peer_bytes"] = c.value, b.value
+        return out
 
     def set_profiling(self, enable: bool = True):
         call("dora_node_set_profiling", self.handle, int(enable))

@@ -267,6 +267,11 @@ void dora_event_free(dora_event* ev);
 
 int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs);
+/* Cross-GPU edges: inputs whose slot lives on another GPU are pulled into a local
+ * receive slot with one hipMemcpyPeerAsync over xGMI and the producer's token is returned at
+ * once.  Counts and bytes of such pulls.  DORA_GPU_EDGE_COPY=1 forces the path on same-GPU
+ * edges. */
+int dora_node_peer_stats(dora_node* node, uint64_t* copies, uint64_t* bytes);
 /* Pack-kernel timing on the node stream (HIP events around every pack launch). */
 int dora_node_set_profiling(dora_node* node, int enable);
 int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);

@@ -171,6 +171,50 @@ def test_host_pyarrow_send_to_device_receiver(launcher):
         assert results[seq]["arrow_equal_len"] == len(arr)
 
 
+def test_pipeline_with_peer_copy_edges(launcher, tmp_path):
+    """C5 shape on one GPU: node -> relay -> sink with the cross-GPU pull path forced
+    (DORA_GPU_EDGE_COPY=1: hipMemcpyPeerAsync into a local slot, token returned at once); every
+    payload arrives bit-exact after two hops."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    from dora_amd.workloads import payload_seed
+    res = str(tmp_path / "sink.json")
+    env = {"DORA_GPU_EDGE_COPY": "1"}
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["data"], "inputs": {"ack": "sink/ack"}},
+        {"id": "relay", "path": "dora-gpu-relay", "outputs": ["out"], "env": env,
+         "inputs": {"in": {"source": "node/data", "queue_size": 100}}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"data": {"source": "relay/out", "queue_size": 100}},
+         "env": dict(env, DORA_BENCH_RESULT=res)},
+    ]}
+    sizes = [4096, 409600, 40960000]
+    with Dataflow(desc, launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        s = device.Stream()
+        for size in sizes:
+            buf = device.DeviceBuffer(size)
+            device.fill_splitmix(buf.ptr, size, payload_seed(size), s)
+            s.sync()
+            c = device.csum64(buf.ptr, size, s)
+            for k in range(4):
+                node.send_output_device_bytes("data", buf.ptr, size,
+                                              {"csum": to_i64(c), "verify": True, "seq": k})
+            buf.free()
+        node.close()
+        codes = df.wait(120)
+        relay_log = df.log("relay")
+    assert codes["relay"] == 0 and codes["sink"] == 0, relay_log
+    out = json.load(open(res))
+    got = {x["size"]: x for x in out["series"]}
+    for size in sizes:
+        assert got[size]["verified"] == 4 and got[size]["mismatches"] == 0
+    relay = json.loads(relay_log.strip().splitlines()[-1])
+    assert relay["relay_peer_copies"] == 12 and relay["errors"] == 0
+
+
 def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
     """queue_size 2 and a burst: dropped inputs still return their drop tokens."""
     from dora_amd import device

@@ -202,3 +202,18 @@ def test_golden_cases_checksums(dev):
             assert device.csum64(buf.ptr, n, dev) == c["sample_csum64"], c["name"]
         finally:
             plan.close(); buf.free(); da.close()
+
+
+@pytest.mark.parametrize("dtype", ["uint8", "int32", "float32", "float64"])
+def test_dlpack_export_to_torch(dev, dtype):
+    """§8f-1: a device sample reaches torch zero-copy through DLPack (kDLROCM)."""
+    import pyarrow as pa
+    import torch
+    from dora_amd.device import DeviceArray
+    vals = np.arange(1000, dtype=dtype) * 3
+    arr = pa.array(vals).slice(10, 900)
+    with DeviceArray.from_pyarrow(arr) as da:
+        t = torch.from_dlpack(da)
+        assert t.device.type == "cuda" and t.shape == (900,)
+        assert np.array_equal(t.cpu().numpy(), vals[10:910])
+        del t
