@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the per-launch kernel stamps (roofline then unmeasured)")
     return ap.parse_args()
 
 
@@ -194,7 +196,7 @@ def main():
             b.free()
 
     # ---- timed region: K back-to-back steps, closed by the sink's ack ----
-    node.set_profiling(True)
+    node.set_profiling(not args.no_kernel_timing)
     barrier()
     device.set_device(local_rank)
     from dora_amd._lib import call

@@ -256,6 +256,8 @@ struct dora_event {
   dora::Metadata meta;
   std::shared_ptr<dora::InputData> data;
   std::string error;
+  bool pending = false;  // device input not yet completed (fill wait / cross-GPU pull)
+  dora::DeviceIpc ipc{};
 };
 
 struct dora_node {
@@ -419,91 +421,10 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           }
         }
         if (base) in->ptr = static_cast<uint8_t*>(base) + d.ipc.offset;
-        if (base && d.ipc.fill == FILL_FLAG) {
-          // the producer's stream writes the epoch into its fill flag after the pack: poll it
-          RegionHdr* h = n->core->region->hdr();
-          if (d.ipc.flag_node >= h->n_nodes || d.ipc.flag_index >= kFillFlags) {
-            ev->type = DORA_EVENT_ERROR;
-            ev->error = "fill flag out of range";
-            in->ptr = nullptr;
-          } else {
-            const std::atomic<uint64_t>& f = h->nodes[d.ipc.flag_node].fill[d.ipc.flag_index].epoch;
-            const uint64_t t0 = mono_ns();
-            unsigned spins = 0;
-            while (f.load(std::memory_order_acquire) < d.ipc.epoch) {
-              if (++spins < 4096) {
-                __builtin_ia32_pause();
-                continue;
-              }
-              spins = 0;
-              if (mono_ns() - t0 > 60000000000ull) {
-                ev->type = DORA_EVENT_ERROR;
-                ev->error = "the producer's fill did not complete within 60 s";
-                in->ptr = nullptr;
-                break;
-              }
-              if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
-            }
-          }
-        } else if (base && d.ipc.fill == FILL_EVENT) {
-          // the producer's fill completes when its interprocess event fires
-          hipEvent_t fill = nullptr;
-          std::string key(reinterpret_cast<const char*>(d.ipc.event), 64);
-          {
-            std::lock_guard<std::mutex> g(n->core->ipc_mu);
-            auto it = n->core->ipc_events.find(key);
-            if (it != n->core->ipc_events.end()) {
-              fill = it->second;
-            } else {
-              hipIpcEventHandle_t h;
-              std::memcpy(&h, d.ipc.event, sizeof(h));
-              if (hipIpcOpenEventHandle(&fill, h) == hipSuccess) n->core->ipc_events[key] = fill;
-              else fill = nullptr;
-            }
-          }
-          // spin on the event (hipEventSynchronize sleeps in ~1 ms quanta on interprocess
-          // events that are not yet complete), then fall back to the blocking wait
-          hipError_t e = fill ? hipEventQuery(fill) : hipErrorInvalidHandle;
-          const uint64_t t0 = mono_ns();
-          while (e == hipErrorNotReady && mono_ns() - t0 < 20000000ull) {
-            __builtin_ia32_pause();
-            e = hipEventQuery(fill);
-          }
-          if (e == hipErrorNotReady) e = hipEventSynchronize(fill);
-          if (e != hipSuccess) {
-            ev->type = DORA_EVENT_ERROR;
-            ev->error = std::string("waiting for the producer's fill event: ") +
-                        hipGetErrorString(e);
-            in->ptr = nullptr;
-          }
-        }
-      }
-      if (in->has_token) trace(TP_FILLED, in->token);
-      if (in->has_token && in->ptr && in->len &&
-          (d.ipc.device != n->core->device || edge_copy_forced())) {
-        // Cross-GPU edge: pull the sample over xGMI into a local slot with one
-        // peer copy on the node stream, then hand the producer its slot back at once.
-        uint64_t cap = 0;
-        void* local = n->core->recv_pool_get(in->len, &cap);
-        hipError_t e = local ? hipMemcpyPeerAsync(local, n->core->device, in->ptr, d.ipc.device,
-                                                  in->len, n->core->stream)
-                             : hipErrorOutOfMemory;
-        if (e == hipSuccess) e = hipStreamSynchronize(n->core->stream);
-        if (e != hipSuccess) {
-          if (local) n->core->recv_pool_put(local, cap);
-          ev->type = DORA_EVENT_ERROR;
-          ev->error = std::string("cross-GPU peer copy: ") + hipGetErrorString(e);
-          in->ptr = nullptr;
-        } else {
-          in->local = local;
-          in->local_cap = cap;
-          in->ptr = local;
-          n->core->report_drop_token(in->token);
-          trace(TP_RELEASED, in->token);
-          in->has_token = false;
-          ++n->peer_copies;
-          n->peer_bytes += in->len;
-        }
+        // the fill wait and a cross-GPU pull happen when the event is handed out
+        // (finish_input), so draining a burst never serialises on later fills
+        ev->pending = true;
+        ev->ipc = d.ipc;
       }
       ev->data = std::move(in);
       break;
@@ -522,6 +443,101 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
       return;  // EV_READY after init is ignored
   }
   n->queue.push_back(std::move(ev));
+}
+
+// Complete a queued device input right before it is handed to the user: wait for the
+// producer's fill (flag or interprocess event) and, for a slot on another GPU, pull it into a
+// local receive slot with one peer copy and return the producer's token at once.
+void finish_input(dora_node* n, dora_event* ev) {
+  if (!ev->pending) return;
+  ev->pending = false;
+  InputData* in = ev->data.get();
+  const DeviceIpc& d = ev->ipc;
+  if (!in || !in->ptr) return;
+  if (d.fill == FILL_FLAG) {
+    // the producer's stream writes the epoch into its fill flag after the pack: poll it
+    RegionHdr* h = n->core->region->hdr();
+    if (d.flag_node >= h->n_nodes || d.flag_index >= kFillFlags) {
+      ev->type = DORA_EVENT_ERROR;
+      ev->error = "fill flag out of range";
+      in->ptr = nullptr;
+      return;
+    }
+    const std::atomic<uint64_t>& f = h->nodes[d.flag_node].fill[d.flag_index].epoch;
+    const uint64_t t0 = mono_ns();
+    unsigned spins = 0;
+    while (f.load(std::memory_order_acquire) < d.epoch) {
+      if (++spins < 4096) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      spins = 0;
+      if (mono_ns() - t0 > 60000000000ull) {
+        ev->type = DORA_EVENT_ERROR;
+        ev->error = "the producer's fill did not complete within 60 s";
+        in->ptr = nullptr;
+        return;
+      }
+      if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
+    }
+  } else if (d.fill == FILL_EVENT) {
+    // the producer's fill completes when its interprocess event fires
+    hipEvent_t fill = nullptr;
+    std::string key(reinterpret_cast<const char*>(d.event), 64);
+    {
+      std::lock_guard<std::mutex> g(n->core->ipc_mu);
+      auto it = n->core->ipc_events.find(key);
+      if (it != n->core->ipc_events.end()) {
+        fill = it->second;
+      } else {
+        hipIpcEventHandle_t h;
+        std::memcpy(&h, d.event, sizeof(h));
+        if (hipIpcOpenEventHandle(&fill, h) == hipSuccess) n->core->ipc_events[key] = fill;
+        else fill = nullptr;
+      }
+    }
+    // spin on the event (hipEventSynchronize sleeps in ~1 ms quanta on interprocess events
+    // that are not yet complete), then fall back to the blocking wait
+    hipError_t e = fill ? hipEventQuery(fill) : hipErrorInvalidHandle;
+    const uint64_t t0 = mono_ns();
+    while (e == hipErrorNotReady && mono_ns() - t0 < 20000000ull) {
+      __builtin_ia32_pause();
+      e = hipEventQuery(fill);
+    }
+    if (e == hipErrorNotReady) e = hipEventSynchronize(fill);
+    if (e != hipSuccess) {
+      ev->type = DORA_EVENT_ERROR;
+      ev->error = std::string("waiting for the producer's fill event: ") + hipGetErrorString(e);
+      in->ptr = nullptr;
+      return;
+    }
+  }
+  trace(TP_FILLED, in->token);
+  if (in->len && (d.device != n->core->device || edge_copy_forced())) {
+    // Cross-GPU edge: pull the sample over xGMI into a local slot with one peer
+    // copy on the node stream, then hand the producer its slot back at once.
+    uint64_t cap = 0;
+    void* local = n->core->recv_pool_get(in->len, &cap);
+    hipError_t e = local ? hipMemcpyPeerAsync(local, n->core->device, in->ptr, d.device, in->len,
+                                              n->core->stream)
+                         : hipErrorOutOfMemory;
+    if (e == hipSuccess) e = hipStreamSynchronize(n->core->stream);
+    if (e != hipSuccess) {
+      if (local) n->core->recv_pool_put(local, cap);
+      ev->type = DORA_EVENT_ERROR;
+      ev->error = std::string("cross-GPU peer copy: ") + hipGetErrorString(e);
+      in->ptr = nullptr;
+      return;
+    }
+    in->local = local;
+    in->local_cap = cap;
+    in->ptr = local;
+    n->core->report_drop_token(in->token);
+    trace(TP_RELEASED, in->token);
+    in->has_token = false;
+    ++n->peer_copies;
+    n->peer_bytes += in->len;
+  }
 }
 
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
@@ -988,6 +1004,7 @@ int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
     if (!n->queue.empty()) {
       *out = n->queue.front().release();
       n->queue.pop_front();
+      dora::finish_input(n, *out);
       return DORA_OK;
     }
     if (n->ended) return dora::fail(DORA_ERR_CLOSED, "event stream closed");
@@ -1015,7 +1032,9 @@ int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
   return DORA_OK;
 }
 
-int dora_event_is_device(const dora_event* e) { return e && e->data && e->data->has_token; }
+int dora_event_is_device(const dora_event* e) {
+  return e && e->data && (e->data->has_token || e->data->local);
+}
 
 int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
   if (!e || !ti || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
@@ -1040,7 +1059,7 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
     return dora::fail(DORA_ERR_INVALID, "not an input event");
   if (!e->data->ptr && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", e->error.c_str());
-  if (!e->data->has_token && e->data->len)
+  if (!e->data->has_token && !e->data->local && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "inline (host Vec) sample: read it with dora_event_data");
   std::shared_ptr<void> keep = e->data;
   return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
