@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=40960000)
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+                    help="c2: UInt8 payloads (BASELINE configs[1], default); c3: nested "
+                         "List<Struct<x,y,z,intensity>> 1M-point clouds (configs[2])")
     ap.add_argument("--lat-n", type=int, default=50, help="latency-mode messages per size")
     ap.add_argument("--lat-gap-us", type=int, default=1000)
     ap.add_argument("--no-ladder", action="store_true")
@@ -144,15 +147,38 @@ def main():
 
     node = Node("node", dataflow=df.shm, device=local_rank)
     stream = device.Stream()
-    S = args.size
-    nsrc = args.sources or max(2, min(16, (640 << 20) // max(S, 1)))
-    srcs = []
-    for _ in range(nsrc):   # rotate > 512 MiB of sources so the Infinity Cache cannot hold them
-        b = device.DeviceBuffer(S)
-        device.fill_splitmix(b.ptr, S, payload_seed(S), stream)
-        srcs.append(b)
-    stream.sync()
-    csum = device.csum64(srcs[0].ptr, S, stream)
+    if args.workload == "c2":
+        S = args.size
+        nsrc = args.sources or max(2, min(16, (640 << 20) // max(S, 1)))
+        srcs = []
+        for _ in range(nsrc):  # rotate > 512 MiB of sources so the Infinity Cache cannot hold them
+            b = device.DeviceBuffer(S)
+            device.fill_splitmix(b.ptr, S, payload_seed(S), stream)
+            srcs.append(b)
+        stream.sync()
+        csum = device.csum64(srcs[0].ptr, S, stream)
+
+        def send(k, meta):
+            node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S, meta)
+    else:
+        # C3: List<Struct<x,y,z:f32,intensity:u8>> 1M-point clouds resident in HBM; each send is
+        # plan (host DFS + validity read-back for the type info) + nested pack kernel
+        from dora_amd.arrow_utils import Plan
+        from dora_amd.device import DeviceArray
+        from dora_amd.workloads import point_cloud
+        cloud = point_cloud()
+        nsrc = args.sources or 24
+        srcs = [DeviceArray.from_pyarrow(cloud) for _ in range(nsrc)]
+        with Plan.of(srcs[0]) as p:
+            S = p.size
+            ref = device.DeviceBuffer(S)
+            p.pack(ref.ptr, S, stream)
+            stream.sync()
+        csum = device.csum64(ref.ptr, S, stream)
+        ref.free()
+
+        def send(k, meta):
+            node.send_output("throughput", srcs[k % nsrc], meta)
 
     def wait_ack(seq, timeout=60.0):
         deadline = time.time() + timeout
@@ -169,7 +195,7 @@ def main():
         meta = {"seq": seq, "t_start": time.time_ns()}
         if k < 3:
             meta.update({"csum": to_i64(csum), "verify": True})
-        node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S, meta)
+        send(k, meta)
         seq += 1
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     wait_ack(seq)
@@ -203,8 +229,7 @@ def main():
     call("dora_gpu_device_sync")
     t0 = time.perf_counter()
     for k in range(args.steps):
-        node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S,
-                                      {"seq": seq, "t_start": time.time_ns()})
+        send(k, {"seq": seq, "t_start": time.time_ns()})
         seq += 1
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     wait_ack(seq)
@@ -236,14 +261,23 @@ def main():
                                    "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
     verified = sum(s["verified"] for s in sink.get("series", []))
     mismatches = sum(s["mismatches"] for s in sink.get("series", []))
+    if args.workload == "c2":
+        metric = f"node->node GB/s ({S:,} B UInt8 samples) + p50/p99 latency per msg size"
+        workload = ("C2: examples/benchmark node->sink edge, device-resident UInt8 samples, "
+                    "1 node + 1 sink per GPU")
+        data = "synthetic (splitmix64 payloads, seed 0xD05A + size)"
+    else:
+        metric = "node->node GB/s (List<Struct<x,y,z:f32,intensity:u8>> 1M points) + latency"
+        workload = ("C3: nested Arrow packing, 1M-point clouds in 16 lists with validity "
+                    "bitmaps, node->sink edge per GPU")
+        data = "synthetic (seeded point clouds, dora_amd.workloads.point_cloud)"
     line = {
-        "metric": "node->node GB/s (40,960,000 B UInt8 samples) + p50/p99 latency per msg size",
+        "metric": metric,
         "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (splitmix64 payloads, seed 0xD05A + size)",
-        "config": {"workload": "C2: examples/benchmark node->sink edge, device-resident UInt8 "
-                               "samples, 1 node + 1 sink per GPU",
+        "data": data,
+        "config": {"workload": workload,
                    "msg_bytes": S, "parallelism": f"dp{world} (one dataflow per GPU)",
                    "sources_rotated": nsrc},
         "latency_us": lat,
@@ -252,6 +286,9 @@ def main():
                      "traffic": traffic[1] if traffic else None,
                      "traffic_source": traffic[0] if traffic else None, "kernel": "pack_kernel",
                      "avg_kernel_us": round(avg_pack_ms * 1e3, 3),
+                     "kernel_stamps": pack["count"],
+                     "timing": "hipExtLaunchKernel start/stop stamps on the node stream, every "
+                               "8th pack of the timed region (DORA_GPU_TIMING_SAMPLE)",
                      "algorithmic_bytes_per_launch": 2 * S},
         "parity": {"verified_msgs": verified, "mismatches": mismatches},
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},

@@ -78,6 +78,15 @@ size_t max_in_flight() {
   return v;
 }
 
+uint64_t timing_sample() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_TIMING_SAMPLE");
+    long x = e ? std::atol(e) : 8;
+    return static_cast<uint64_t>(x > 0 ? x : 8);
+  }();
+  return v;
+}
+
 // Force the cross-GPU copy path on same-GPU edges (tests on a one-GPU box).
 bool edge_copy_forced() {
   static const bool v = [] {
@@ -274,6 +283,7 @@ struct dora_node {
   bool profile = false;
   std::vector<dora::TimingPair> timing;  // ring of kTimingPairs
   size_t timing_next = 0;
+  uint64_t timing_seq = 0;
   uint64_t pack_count = 0, pack_bytes = 0;
   double pack_ms = 0;
   uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
@@ -733,7 +743,10 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     for (const Segment& g : plan->segs) std::memcpy(s->vec.data() + g.dst_off, g.src, g.len);
   } else if (plan->size) {
     hipStream_t st = n->core->stream;
-    const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU;
+    // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
+    // every `timing_sample()`-th pack is stamped (DORA_GPU_TIMING_SAMPLE, default 8).
+    const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU &&
+                       (n->timing_seq++ % timing_sample()) == 0;
     TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
     rc = launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                      static_cast<uint8_t*>(s->slot->ptr), st, tp ? tp->start : nullptr,
@@ -1114,6 +1127,7 @@ int dora_node_set_profiling(dora_node* n, int enable) {
   for (auto& x : n->phase_ns) x = 0;
   n->phase_count = 0;
   n->pack_count = 0;
+  n->timing_seq = 0;
   n->pack_ms = 0;
   n->pack_bytes = 0;
   return DORA_OK;
