@@ -59,6 +59,9 @@ _SIGS = {
     "dora_gpu_plan": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema), c_int32,
                               POINTER(c_void_p)]),
     "dora_gpu_plan_bytes": (c_int, [c_void_p, c_size_t, c_int32, POINTER(c_void_p)]),
+    "dora_gpu_plan_compact": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema), c_int32,
+                                      POINTER(c_void_p)]),
+    "dora_node_set_compact": (c_int, [c_void_p, c_int]),
     "dora_gpu_plan_free": (None, [c_void_p]),
     "dora_gpu_plan_size": (c_size_t, [c_void_p]),
     "dora_gpu_plan_num_segments": (c_size_t, [c_void_p]),

@@ -27,18 +27,21 @@ class Plan:
         self._lib = load()
 
     @classmethod
-    def of(cls, array) -> "Plan":
+    def of(cls, array, compact: bool = False) -> "Plan":
+        """Reference layout (`copy_array_into_sample`), or with `compact=True` the compacting
+        plan (slices reduced to their own bytes, offset 0 everywhere)."""
         h = c_void_p()
+        fn = "dora_gpu_plan_compact" if compact else "dora_gpu_plan"
         if isinstance(array, DeviceArray):
             s = array.export_schema()
             try:
-                call("dora_gpu_plan", byref(array.array), byref(s), ARROW_DEVICE_ROCM, byref(h))
+                call(fn, byref(array.array), byref(s), ARROW_DEVICE_ROCM, byref(h))
             finally:
                 release_schema(s)
             return cls(h.value, array)
         c = CArray.from_pyarrow(array)
         try:
-            call("dora_gpu_plan", byref(c.array), byref(c.schema), ARROW_DEVICE_CPU, byref(h))
+            call(fn, byref(c.array), byref(c.schema), ARROW_DEVICE_CPU, byref(h))
         except Exception:
             c.close()
             raise

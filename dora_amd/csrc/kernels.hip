@@ -196,6 +196,73 @@ Variant pack_variant() {
   return v;
 }
 
+// ------------------------------------------------------------------------------------------
+// Transform segments of compacting plans: bitmap slices shifted to bit 0 and offsets rebased to
+// 0.  Elementwise and tiny next to the value buffers (a bitmap is len/8 bytes, offsets
+// 4-8 B per list), so one simple grid over all transform segments.
+// ------------------------------------------------------------------------------------------
+struct XSeg {
+  const uint8_t* src;
+  uint64_t dst_off;
+  uint64_t len;      // output bytes
+  uint64_t src_len;  // readable source bytes (bitshift)
+  uint32_t op;
+  uint32_t aux;      // bit offset (bitshift)
+};
+
+struct XArgs {
+  uint8_t* dst;
+  uint32_t nseg;
+  uint32_t block_end[kMaxSegs];
+  XSeg seg[kMaxSegs];
+};
+
+constexpr uint64_t kXElems = 4096;  // output elements per workgroup
+
+template <typename T>
+__device__ __forceinline__ void rebase(const uint8_t* src, uint8_t* dst, uint64_t count,
+                                       uint64_t e0, uint64_t e1) {
+  T base;
+  __builtin_memcpy(&base, src, sizeof(T));
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) &
+                        (sizeof(T) - 1)) == 0;
+  for (uint64_t i = e0 + threadIdx.x; i < e1 && i < count; i += kThreads) {
+    if (aligned) {
+      reinterpret_cast<T*>(dst)[i] = reinterpret_cast<const T*>(src)[i] - base;
+    } else {
+      T v;
+      __builtin_memcpy(&v, src + i * sizeof(T), sizeof(T));
+      v -= base;
+      __builtin_memcpy(dst + i * sizeof(T), &v, sizeof(T));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void transform_kernel(XArgs a) {
+  const uint32_t blk = blockIdx.x;
+  uint32_t s = 0;
+  while (s + 1 < a.nseg && blk >= a.block_end[s]) ++s;
+  const XSeg g = a.seg[s];
+  const uint64_t c = blk - (s ? a.block_end[s - 1] : 0u);
+  const uint64_t e0 = c * kXElems, e1 = e0 + kXElems;
+  uint8_t* dst = a.dst + g.dst_off;
+  if (g.op == SEG_BITSHIFT) {
+    for (uint64_t j = e0 + threadIdx.x; j < e1 && j < g.len; j += kThreads) {
+      const uint32_t lo = g.src[j];
+      const uint32_t hi = j + 1 < g.src_len ? g.src[j + 1] : 0u;
+      dst[j] = static_cast<uint8_t>(g.aux ? ((lo >> g.aux) | (hi << (8 - g.aux))) : lo);
+    }
+  } else if (g.op == SEG_REBASE32) {
+    rebase<int32_t>(g.src, dst, g.len / 4, e0, e1);
+  } else if (g.op == SEG_REBASE64) {
+    rebase<int64_t>(g.src, dst, g.len / 8, e0, e1);
+  }
+}
+
+uint64_t xseg_elems(const Segment& s) {
+  return s.op == SEG_REBASE32 ? s.len / 4 : s.op == SEG_REBASE64 ? s.len / 8 : s.len;
+}
+
 uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
   if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
@@ -272,18 +339,33 @@ unsigned grid_for(uint64_t items) {
 
 }  // namespace
 
-// Launch the pack of `n` segments into `dst` (device).  Segments with device sources go to
-// pack_kernel in batches of kMaxSegs; host sources are DMA'd with hipMemcpyAsync.  With timing
-// events the launches go through hipExtLaunchKernelGGL, whose dispatch packet stamps the first
-// kernel's begin into `ev_start` and the last kernel's end into `ev_stop`.
-int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
+// Launch the pack of `n` segments into `dst` (device).  Copy segments with device sources go
+// to pack_kernel in batches of kMaxSegs, transform segments (compacting plans) to
+// transform_kernel; host sources are DMA'd with hipMemcpyAsync.  With timing events the
+// launches go through hipExtLaunchKernelGGL, whose dispatch packet stamps the first kernel's
+// begin into `ev_start` and the last kernel's end into `ev_stop`.
+int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_t* dst,
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
+  bool any_x = false;
+  for (size_t i = 0; i < n_in; ++i) any_x |= segs_in[i].op != SEG_COPY;
   if (dev == ARROW_DEVICE_CPU) {
-    for (size_t i = 0; i < n; ++i)
-      DORA_HIP(hipMemcpyAsync(dst + segs[i].dst_off, segs[i].src, segs[i].len,
+    if (any_x) return fail(DORA_ERR_UNSUPPORTED, "compacting plans need device-resident arrays");
+    for (size_t i = 0; i < n_in; ++i)
+      DORA_HIP(hipMemcpyAsync(dst + segs_in[i].dst_off, segs_in[i].src, segs_in[i].len,
                               hipMemcpyHostToDevice, stream));
     return DORA_OK;
   }
+  std::vector<Segment> copies, xforms;
+  const Segment* segs = segs_in;
+  size_t n = n_in;
+  if (any_x) {
+    for (size_t i = 0; i < n_in; ++i) (segs_in[i].op == SEG_COPY ? copies : xforms).push_back(segs_in[i]);
+    segs = copies.data();
+    n = copies.size();
+  }
+  const size_t n_launch_x = (xforms.size() + kMaxSegs - 1) / kMaxSegs;
+  size_t launch = 0;
+  const size_t n_launch = (n + kMaxSegs - 1) / kMaxSegs + n_launch_x;
   size_t i = 0;
   while (i < n) {
     PackArgs a;
@@ -309,7 +391,7 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
       a.chunk_end[k] = static_cast<uint32_t>(chunks);
     }
     a.nseg = static_cast<uint32_t>(m);
-    const bool first = i == 0, last = i + m == n;
+    const bool first = launch == 0, last = launch + 1 == n_launch;
     void (*kern)(PackArgs) = pack_kernel<4, false>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, true> : pack_kernel<2, false>;
@@ -322,6 +404,32 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
     }
     DORA_HIP(hipGetLastError());
     i += m;
+    ++launch;
+  }
+  for (size_t j = 0; j < xforms.size(); j += kMaxSegs) {
+    XArgs x;
+    std::memset(&x, 0, sizeof(x));
+    x.dst = dst;
+    const size_t m = std::min<size_t>(kMaxSegs, xforms.size() - j);
+    uint64_t blocks = 0;
+    for (size_t k = 0; k < m; ++k) {
+      const Segment& s = xforms[j + k];
+      x.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len, s.src_len, s.op, s.aux};
+      blocks += std::max<uint64_t>(1, (xseg_elems(s) + kXElems - 1) / kXElems);
+      if (blocks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many blocks");
+      x.block_end[k] = static_cast<uint32_t>(blocks);
+    }
+    x.nseg = static_cast<uint32_t>(m);
+    const bool first = launch == 0, last = launch + 1 == n_launch;
+    if (ev_start || ev_stop) {
+      hipExtLaunchKernelGGL(transform_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kThreads),
+                            0, stream, first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, x);
+    } else {
+      hipLaunchKernelGGL(transform_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
+                         stream, x);
+    }
+    DORA_HIP(hipGetLastError());
+    ++launch;
   }
   return DORA_OK;
 }

@@ -291,6 +291,7 @@ struct dora_node {
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
   uint64_t peer_copies = 0, peer_bytes = 0;  // cross-GPU edges pulled into local slots
+  bool compact = false;                      // send_output uses compacting plans
 };
 
 namespace dora {
@@ -963,7 +964,9 @@ int dora_node_send_output(dora_node* n, const char* output_id, const struct Arro
   if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
   dora_plan* plan = nullptr;
-  int rc = dora::build_plan(array, schema, device_type, &plan);
+  int rc = (n->compact && device_type == ARROW_DEVICE_ROCM)
+               ? dora::build_plan_compact(array, schema, device_type, &plan)
+               : dora::build_plan(array, schema, device_type, &plan);
   if (rc != DORA_OK) return rc;
   rc = dora::pack_and_send(n, output_id, plan, params, params_len);
   delete plan;
@@ -990,6 +993,12 @@ int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void*
   if (len) plan.segs.push_back({data, 0, len});
   return dora::pack_and_send(n, output_id, &plan, params, params_len);
   DORA_GUARD_END
+}
+
+int dora_node_set_compact(dora_node* n, int enable) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  n->compact = enable != 0;
+  return DORA_OK;
 }
 
 int dora_node_close_outputs(dora_node* n, const char* const* ids, size_t count) {

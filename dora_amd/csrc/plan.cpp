@@ -266,6 +266,127 @@ void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t&
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Compacting walk (new capability; the reference copies sliced buffers whole and passes the
+// offset through, F3): every node is reduced to exactly its logical range [phys, phys + len) of
+// its buffers — fixed-width values sliced, Boolean bitmaps bit-shifted to bit 0, offsets rebased
+// to start at 0 with the child / value ranges they address sliced recursively, validity
+// bit-shifted on the host for the type info — so a slice moves only its own bytes and the
+// receiver gets offset 0 everywhere.  `phys` is the element index into this node's buffers.
+// ---------------------------------------------------------------------------------------------
+std::vector<uint8_t> shift_bits_host(const std::vector<uint8_t>& src, uint64_t bit0,
+                                     uint64_t nbits) {
+  std::vector<uint8_t> out((nbits + 7) / 8, 0);
+  for (uint64_t i = 0; i < nbits; ++i)
+    if ((src[(bit0 + i) >> 3] >> ((bit0 + i) & 7)) & 1) out[i >> 3] |= uint8_t(1u << (i & 7));
+  return out;
+}
+
+void walk_compact(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t phys,
+                  uint64_t len, uint64_t& next, std::vector<Segment>& segs, TypeInfoNode& ti) {
+  if (!a || !s || !s->format) throw std::invalid_argument("null ArrowArray/ArrowSchema node");
+  const std::string fmt = s->format;
+  const bool is_dict = s->dictionary != nullptr;
+  if (fmt == "+r") throw std::domain_error("run-end encoded arrays cannot be compacted");
+  Layout l = layout_of(fmt);
+  if (is_dict) l.offsets_first = false;
+  const int64_t begin = l.can_null ? 1 : 0;
+  if (a->n_buffers < begin + static_cast<int64_t>(l.specs.size()))
+    throw std::invalid_argument("ArrowArray for '" + fmt + "' has too few buffers");
+  ti.sig = schema_sig(s);
+  serialize_schema(s, true, ti.schema);
+  ti.len = len;
+  ti.offset = 0;
+  ti.null_count = 0;
+  ti.has_validity = false;
+
+  uint64_t o_start = 0, o_end = 0;  // child / value range addressed by an offsets buffer
+  for (size_t k = 0; k < l.specs.size(); ++k) {
+    const BufSpec& sp = l.specs[k];
+    const uint8_t* p = static_cast<const uint8_t*>(a->buffers[begin + static_cast<int64_t>(k)]);
+    Segment seg{nullptr, 0, 0};
+    if (sp.kind == BufSpec::Bitmap) {
+      seg.len = (len + 7) / 8;
+      seg.src = p + phys / 8;
+      seg.op = SEG_BITSHIFT;
+      seg.aux = static_cast<uint32_t>(phys % 8);
+      seg.src_len = (phys + len + 7) / 8 - phys / 8;
+    } else if (k == 0 && l.offsets_first) {
+      const uint32_t w = sp.width;
+      seg.len = (len + 1) * w;
+      seg.src = p + phys * w;
+      seg.op = w == 4 ? SEG_REBASE32 : SEG_REBASE64;
+      if (w == 4) {
+        int32_t v[2];
+        rd.read(&v[0], p + phys * 4, 4);
+        rd.read(&v[1], p + (phys + len) * 4, 4);
+        if (v[0] < 0 || v[1] < v[0]) throw std::invalid_argument("bad offsets");
+        o_start = uint64_t(v[0]);
+        o_end = uint64_t(v[1]);
+      } else {
+        int64_t v[2];
+        rd.read(&v[0], p + phys * 8, 8);
+        rd.read(&v[1], p + (phys + len) * 8, 8);
+        if (v[0] < 0 || v[1] < v[0]) throw std::invalid_argument("bad offsets");
+        o_start = uint64_t(v[0]);
+        o_end = uint64_t(v[1]);
+      }
+    } else if (sp.kind == BufSpec::Var) {
+      seg.len = o_end - o_start;
+      seg.src = p + o_start;
+    } else {
+      seg.len = len * sp.width;
+      seg.src = p + phys * sp.width;
+    }
+    if (!p && seg.len) throw std::invalid_argument("null buffer with data in '" + fmt + "'");
+    next = pad_to(next, sp);
+    seg.dst_off = next;
+    ti.bufs.push_back({next, seg.len});
+    if (seg.len) segs.push_back(seg);
+    next += seg.len;
+  }
+
+  if (l.can_null && a->n_buffers > 0 && a->buffers[0] && len) {
+    std::vector<uint8_t> v((phys + len + 7) / 8);
+    rd.read(v.data(), a->buffers[0], v.size());
+    std::vector<uint8_t> sv = shift_bits_host(v, phys, len);
+    const uint64_t nc = count_nulls(sv, 0, len);
+    if (nc != 0) {
+      ti.has_validity = true;
+      ti.validity = std::move(sv);
+      ti.null_count = nc;
+    }
+  }
+
+  if (is_dict) {
+    if (!a->dictionary) throw std::invalid_argument("dictionary schema without dictionary data");
+    ti.children.emplace_back();
+    const ArrowArray* d = a->dictionary;
+    walk_compact(d, s->dictionary, rd, uint64_t(d->offset), uint64_t(d->length), next, segs,
+                 ti.children.back());
+    return;
+  }
+  if (a->n_children != s->n_children)
+    throw std::invalid_argument("array/schema child count mismatch for '" + fmt + "'");
+  for (int64_t i = 0; i < a->n_children; ++i) {
+    const ArrowArray* c = a->children[i];
+    uint64_t cphys, clen;
+    if (l.offsets_first) {  // list / large list / map: the offsets address the child range
+      cphys = uint64_t(c->offset) + o_start;
+      clen = o_end - o_start;
+    } else if (fmt.rfind("+w:", 0) == 0) {  // fixed-size list of k
+      const uint64_t kk = std::stoull(fmt.substr(3));
+      cphys = uint64_t(c->offset) + phys * kk;
+      clen = len * kk;
+    } else {  // struct: children are indexed by the parent's physical index
+      cphys = uint64_t(c->offset) + phys;
+      clen = len;
+    }
+    ti.children.emplace_back();
+    walk_compact(c, s->children[i], rd, cphys, clen, next, segs, ti.children.back());
+  }
+}
+
 void put_u8(std::vector<uint8_t>& o, uint8_t v) { o.push_back(v); }
 void put_u32(std::vector<uint8_t>& o, uint32_t v) {
   for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(v >> (8 * i)));
@@ -294,6 +415,34 @@ void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& o) {
   }
   put_u32(o, static_cast<uint32_t>(t.children.size()));
   for (auto& c : t.children) serialize_type_info(c, o);
+}
+
+int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
+                       dora_plan** out) {
+  if (!out) return fail(DORA_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  // host arrays can be planned (sizes, type info) but only device arrays packed
+  if (dev != ARROW_DEVICE_CPU && dev != ARROW_DEVICE_ROCM && dev != ARROW_DEVICE_ROCM_HOST)
+    return fail(DORA_ERR_INVALID, "unsupported device_type %d", dev);
+  if (!array || !schema) return fail(DORA_ERR_INVALID, "null ArrowArray/ArrowSchema");
+  auto* p = new dora_plan();
+  p->dev = dev;
+  p->compact = true;
+  try {
+    Reader rd{dev};
+    uint64_t next = 0;
+    walk_compact(array, schema, rd, uint64_t(array->offset), uint64_t(array->length), next,
+                 p->segs, p->root);
+    p->size = next;
+  } catch (const std::domain_error& e) {
+    delete p;
+    return fail(DORA_ERR_UNSUPPORTED, "%s", e.what());
+  } catch (const std::exception& e) {
+    delete p;
+    return fail(DORA_ERR_INVALID, "plan: %s", e.what());
+  }
+  *out = p;
+  return DORA_OK;
 }
 
 int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
@@ -327,6 +476,11 @@ extern "C" {
 int dora_gpu_plan(const struct ArrowArray* array, const struct ArrowSchema* schema,
                   ArrowDeviceType device_type, dora_plan** out) {
   return dora::build_plan(array, schema, device_type, out);
+}
+
+int dora_gpu_plan_compact(const struct ArrowArray* array, const struct ArrowSchema* schema,
+                          ArrowDeviceType device_type, dora_plan** out) {
+  return dora::build_plan_compact(array, schema, device_type, out);
 }
 
 int dora_gpu_plan_bytes(const void* src, size_t len, ArrowDeviceType device_type,

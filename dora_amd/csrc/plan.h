@@ -36,10 +36,22 @@ struct TypeInfoNode {
 };
 
 // One copy of `copy_array_into_sample_inner` (arrow_utils.rs:48): src -> sample[dst_off..+len].
+// Compacting plans (dora_gpu_plan_compact) also carry transforms: a bit-shifted bitmap slice
+// and rebased offsets.
+enum SegOp : uint32_t {
+  SEG_COPY = 0,      // len bytes verbatim
+  SEG_BITSHIFT = 1,  // len bytes of bitmap starting `aux` bits into src (src_len readable bytes)
+  SEG_REBASE32 = 2,  // len/4 int32 offsets minus src[0]
+  SEG_REBASE64 = 3,  // len/8 int64 offsets minus src[0]
+};
+
 struct Segment {
   const void* src;
   uint64_t dst_off;
   uint64_t len;
+  uint32_t op = SEG_COPY;
+  uint32_t aux = 0;
+  uint64_t src_len = 0;
 };
 
 void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& out);
@@ -52,11 +64,14 @@ uint64_t metadata_len(const char* meta);
 Layout layout_of(const std::string& format);
 int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
                dora_plan** out);
+int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
+                       dora_plan** out);
 
 }  // namespace dora
 
 struct dora_plan {
   ArrowDeviceType dev = ARROW_DEVICE_ROCM;
+  bool compact = false;  // built by dora_gpu_plan_compact (carries transform segments)
   uint64_t size = 0;
   std::vector<dora::Segment> segs;
   dora::TypeInfoNode root;

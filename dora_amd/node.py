@@ -141,6 +141,10 @@ class Node:
         call("dora_node_send_output_bytes", self.handle, output_id.encode(), ptr, n,
              ARROW_DEVICE_ROCM, _u8(params), len(params))
 
+    def set_compact(self, enable: bool = True):
+        """Send device arrays with compacting plans (slices move only their own bytes)."""
+        call("dora_node_set_compact", self.handle, int(enable))
+
     def close_outputs(self, outputs):
         arr = (ctypes.c_char_p * len(outputs))(*[o.encode() for o in outputs])
         call("dora_node_close_outputs", self.handle, arr, len(outputs))

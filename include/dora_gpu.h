@@ -125,6 +125,17 @@ typedef struct dora_plan dora_plan;
  */
 int dora_gpu_plan(const struct ArrowArray* array, const struct ArrowSchema* schema,
                   ArrowDeviceType device_type, dora_plan** out);
+/*
+ * Compacting plan (new capability; the reference copies sliced buffers whole and passes the
+ * offset through): every node is reduced to its logical range — fixed-width values
+ * sliced, Boolean bitmaps bit-shifted to bit 0, offsets rebased to 0 with the child / value
+ * ranges they address sliced recursively, validity shifted for the type info — so the type info
+ * has offset 0 everywhere and a slice moves only its own bytes.  Receivers are unchanged
+ * (`into_arrow_array` yields a logically equal array).  Device-resident arrays only; run-end
+ * encoded arrays are rejected.
+ */
+int dora_gpu_plan_compact(const struct ArrowArray* array, const struct ArrowSchema* schema,
+                          ArrowDeviceType device_type, dora_plan** out);
 /* Plan for `ArrowTypeInfo::byte_array(len)` over one contiguous buffer (metadata.rs:74-87):
  * what `send_output_raw`'s copy closure writes (node/mod.rs:180-196). */
 int dora_gpu_plan_bytes(const void* src, size_t len, ArrowDeviceType device_type,
@@ -242,6 +253,8 @@ int dora_node_send_output(dora_node* node, const char* output_id, const struct A
 int dora_node_send_output_bytes(dora_node* node, const char* output_id, const void* data,
                                 size_t len, ArrowDeviceType device_type, const uint8_t* params,
                                 size_t params_len);
+/* Use compacting plans (dora_gpu_plan_compact) in dora_node_send_output for device arrays. */
+int dora_node_set_compact(dora_node* node, int enable);
 /* close_outputs (mod.rs:277-289). */
 int dora_node_close_outputs(dora_node* node, const char* const* output_ids, size_t count);
 
