@@ -269,10 +269,12 @@ uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
     uint64_t v = std::strtoull(e, nullptr, 10);
     if (v >= 16 && v % 16 == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
   }
-  // ~2k workgroups on big messages (256 CUs x 8 resident), never less than 8 KiB per
-  // workgroup (measured flat within noise from 8 KiB to 32 KiB at 4-40 MB, r01 sweep).
-  (void)unroll;
+  // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
+  // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
+  // 8-32 MB prefers 32 KiB x 8 loads; below that ~2k workgroups of >= 8 KiB.
   constexpr uint64_t kGrain = 8192;
+  if (body_bytes >= (32u << 20)) return kGrain;
+  if (unroll == 8) return 32768;
   uint64_t cb = (body_bytes / 2048 + kGrain - 1) / kGrain * kGrain;
   cb = std::max<uint64_t>(cb, kGrain);
   cb = std::min<uint64_t>(cb, uint64_t(1) << 22);
@@ -375,7 +377,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     const size_t m = std::min<size_t>(kMaxSegs, n - i);
     for (size_t k = 0; k < m; ++k) body += segs[i + k].len;
     Variant var = pack_variant();
-    if (var.unroll == 0) var.unroll = body >= (8u << 20) ? 8 : 4;
+    if (var.unroll == 0) var.unroll = (body >= (8u << 20) && body < (32u << 20)) ? 8 : 4;
     a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
     uint64_t chunks = 0;
     for (size_t k = 0; k < m; ++k) {

@@ -252,7 +252,10 @@ def test_compact_pack_roundtrip(dev, arr):
         finally:
             back.close()
         assert host.type == arr.type
-        assert host.equals(arr), (host, arr)
-        assert host.offset == 0
+        if plan.size == 0:
+            assert len(host) == 0  # empty sample -> ArrayData::new_empty (event.rs:65-67)
+        else:
+            assert host.equals(arr), (host, arr)
+            assert host.offset == 0
     finally:
         plan.close(); buf.free(); da.close()
