@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
+    ap.add_argument("--no-cross-gpu", action="store_true",
+                    help="N>1: skip the C4 fan-out / C5 chain runs after the timed region")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch kernel stamps (roofline then unmeasured)")
     return ap.parse_args()
@@ -113,6 +115,128 @@ def cpu_baseline(rank_cores):
     return json.loads(out)
 
 
+XGMI_LINK_GBPS = 153.0  # MI355X: 7 xGMI links x ~153 GB/s per GPU (one link per peer)
+C4_FRAME = 1920 * 1080 * 3      # BASELINE configs C4: 6,220,800 B frames
+C5_SIZES = [4096, 40960000]      # BASELINE configs C5: control message + tensor per stage
+
+
+def _source_env(result, lat_sizes, tp_size, tp_n, acks, lat_n=30, gap_us=33333):
+    return {"DORA_BENCH_RESULT": result, "DORA_BENCH_LAT_SIZES": ",".join(map(str, lat_sizes)),
+            "DORA_BENCH_LAT_N": str(lat_n), "DORA_BENCH_LAT_GAP_US": str(gap_us),
+            "DORA_BENCH_TP_SIZE": str(tp_size), "DORA_BENCH_TP_N": str(tp_n),
+            "DORA_BENCH_ACKS": str(acks)}
+
+
+def c4_descriptor(n_gpus, tmp, peer_copy="kernel", tp_n=200, gpu=lambda g: g, env=None):
+    """C4: one producer on GPU 0, a consumer on every other GPU (1 -> n_gpus-1 fan-out).  Each
+    consumer pulls the frame from the producer's slot over its own xGMI link (no collective:
+    every receiver keeps its own queue and drop-oldest policy)."""
+    sinks = [f"sink{g}" for g in range(1, n_gpus)]
+    env = dict(env or {}, DORA_GPU_PEER_COPY=peer_copy)
+    nodes = [{"id": "source", "path": "dora-gpu-bench-source",
+              "outputs": ["latency", "throughput"],
+              "inputs": {f"ack{k}": f"{s}/ack" for k, s in enumerate(sinks)},
+              "env": _source_env(os.path.join(tmp, "source.json"), [C4_FRAME], C4_FRAME, tp_n,
+                                 len(sinks)),
+              "_unstable_deploy": {"gpu": gpu(0)}}]
+    for g, s in zip(range(1, n_gpus), sinks):
+        nodes.append({"id": s, "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+                      "inputs": {o: {"source": f"source/{o}", "queue_size": 1000}
+                                 for o in ("latency", "throughput")},
+                      "env": dict(env, DORA_BENCH_RESULT=os.path.join(tmp, f"{s}.json")),
+                      "_unstable_deploy": {"gpu": gpu(g)}})
+    return {"nodes": nodes}
+
+
+def c5_descriptor(n_gpus, tmp, peer_copy="kernel", tp_n=100, gpu=lambda g: g, env=None):
+    """C5: an n_gpus-stage chain, one node per GPU: source (GPU 0) -> relays -> sink (last GPU);
+    each hop is one xGMI pull straight into the next stage's slot (dora_node_forward)."""
+    env = dict(env or {}, DORA_GPU_PEER_COPY=peer_copy)
+    stages = ["source"] + [f"relay{g}" for g in range(1, n_gpus - 1)] + ["sink"]
+    outs = ("latency", "throughput")
+    nodes = [{"id": "source", "path": "dora-gpu-bench-source", "outputs": list(outs),
+              "inputs": {"ack0": "sink/ack"},
+              "env": _source_env(os.path.join(tmp, "source.json"), C5_SIZES, C5_SIZES[1], tp_n,
+                                 1),
+              "_unstable_deploy": {"gpu": gpu(0)}}]
+    for g in range(1, n_gpus):
+        prev, me = stages[g - 1], stages[g]
+        inputs = {o: {"source": f"{prev}/{o}", "queue_size": 1000} for o in outs}
+        if me == "sink":
+            nodes.append({"id": me, "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+                          "inputs": inputs,
+                          "env": dict(env, DORA_BENCH_RESULT=os.path.join(tmp, "sink.json")),
+                          "_unstable_deploy": {"gpu": gpu(g)}})
+        else:
+            nodes.append({"id": me, "path": "dora-gpu-relay", "outputs": list(outs),
+                          "inputs": inputs, "env": env, "_unstable_deploy": {"gpu": gpu(g)}})
+    return {"nodes": nodes}
+
+
+def _load(path):
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
+def run_cross_gpu(n_gpus, launcher, timeout=240.0, runs=None, **desc_kw):
+    """Cross-GPU configurations C4 and C5 on this node's GPUs (rank 0, after the timed region;
+    each stage is its own process).  Failures are reported, never raised: the headline line
+    must not depend on them."""
+    from dora_amd.dataflow import Dataflow
+    out = {}
+    runs = runs or [("c4_fanout_kernel", c4_descriptor, "kernel"),
+                    ("c4_fanout_sdma", c4_descriptor, "sdma"),
+                    ("c5_chain_kernel", c5_descriptor, "kernel")]
+    for name, fn, mode in runs:
+        tmp = tempfile.mkdtemp(prefix=f"dora-{name}-")
+        try:
+            df = Dataflow(fn(n_gpus, tmp, mode, **desc_kw), launcher=launcher).start()
+            try:
+                codes = df.wait(timeout)
+                logs = {k: df.log(k)[-400:] for k, c in codes.items() if c not in (0, None)}
+            finally:
+                df.stop()
+            src = _load(os.path.join(tmp, "source.json")) or {}
+            sinks = {f[:-5]: _load(os.path.join(tmp, f)) for f in sorted(os.listdir(tmp))
+                     if f.endswith(".json") and f != "source.json"}
+            out[name] = summarize_cross(name, src, sinks, codes, logs)
+        except Exception as e:  # noqa: BLE001 — reported in the JSON line
+            out[name] = {"error": repr(e)}
+    return out
+
+
+def summarize_cross(name, src, sinks, codes, logs):
+    lat, verified, mismatches, dropped, errors = {}, 0, 0, 0, 0
+    for sname, r in sinks.items():
+        if not r:
+            errors += 1
+            continue
+        dropped += r.get("dropped_inputs", 0)
+        errors += r.get("errors", 0)
+        for s in r.get("series", []):
+            verified += s["verified"]
+            mismatches += s["mismatches"]
+            if s["input"] == "latency" and s["size"]:
+                lat.setdefault(str(s["size"]), []).append(
+                    {"sink": sname, "p50_us": s["p50_us"], "p99_us": s["p99_us"],
+                     "e2e_p50_us": s["full_p50_us"], "e2e_p99_us": s["full_p99_us"], "n": s["n"]})
+    per_rx = src.get("tp_per_receiver_GBps", 0.0)
+    res = {"ok": bool(src.get("ok")) and errors == 0 and mismatches == 0,
+           "receivers": src.get("receivers"), "msg_bytes": src.get("tp_size"),
+           "tp_msgs": src.get("tp_n"), "delivered_GBps": src.get("tp_delivered_GBps"),
+           "per_link_GBps": per_rx,
+           "roofline": {"bound": "xgmi", "achieved": per_rx, "peak": XGMI_LINK_GBPS,
+                        "unit": "GB/s", "frac": round(per_rx / XGMI_LINK_GBPS, 4)},
+           "latency_us": lat, "parity": {"verified_msgs": verified, "mismatches": mismatches},
+           "dropped_inputs": dropped, "errors": errors, "exit_codes": codes,
+           "source_send_phase_us": src.get("send_phase_us")}
+    if logs:
+        res["logs"] = logs
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -124,6 +248,11 @@ def main():
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline(affinity)
+
+    launcher = None
+    if world > 1 and rank == 0 and not args.no_cross_gpu:
+        from dora_amd.launcher import Launcher
+        launcher = Launcher()  # spawns the cross-GPU stages after this process touched HIP
 
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
@@ -246,6 +375,11 @@ def main():
 
     t_max = max_over_ranks(elapsed)
     total_bytes = sum_over_ranks(float(args.steps * S))
+    cross = None
+    if launcher is not None:
+        cross = run_cross_gpu(world, launcher)
+        launcher.close()
+    barrier()
     value = total_bytes / t_max / 1e9
     avg_pack_ms = pack["total_ms"] / max(pack["count"], 1)
     achieved = 2.0 * S / (avg_pack_ms * 1e-3) / 1e9 if pack["count"] else 0.0
@@ -294,6 +428,8 @@ def main():
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
         "node_stats": stats, "exit_codes": codes,
     }
+    if cross is not None:
+        line["cross_gpu"] = cross
     if base is not None:
         tp = [s for s in base["series"] if s["mode"] == "throughput" and s["size"] == 40960000]
         line["cpu_baseline"] = {

@@ -80,6 +80,7 @@ TOOLS = {  # binary name -> sources (linked against libdora_gpu.so, rpath $ORIGI
     "dora-gpu-daemon": ["tools/daemon_main.cpp"],
     "dora-gpu-bench-sink": ["tools/bench_sink.cpp"],
     "dora-gpu-relay": ["tools/relay.cpp"],
+    "dora-gpu-bench-source": ["tools/bench_source.cpp"],
 }
 
 

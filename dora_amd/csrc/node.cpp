@@ -17,6 +17,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -87,6 +88,18 @@ uint64_t timing_sample() {
   return v;
 }
 
+enum PeerCopyMode { PEER_KERNEL, PEER_SDMA };
+
+// How cross-GPU samples are pulled: the pack kernel on the receiving GPU reading the peer's HBM
+// (default) or the copy engines via hipMemcpyPeerAsync (DORA_GPU_PEER_COPY=sdma).
+PeerCopyMode peer_copy_mode() {
+  static const PeerCopyMode v = [] {
+    const char* e = std::getenv("DORA_GPU_PEER_COPY");
+    return (e && std::string(e) == "sdma") ? PEER_SDMA : PEER_KERNEL;
+  }();
+  return v;
+}
+
 // Force the cross-GPU copy path on same-GPU edges (tests on a one-GPU box).
 bool edge_copy_forced() {
   static const bool v = [] {
@@ -102,6 +115,20 @@ uint64_t slot_wait_ns() {
     return uint64_t(e ? std::atoll(e) : 5000) * 1000;
   }();
   return v;
+}
+
+// Slots of every node in this process by process-wide id: a sample whose owner is this process
+// (another node here, or the node itself) is read in place — IPC handles cannot be opened in
+// the process that exported them.
+struct OwnSlots {
+  std::mutex mu;
+  std::unordered_map<uint64_t, void*> ptrs;
+  std::atomic<uint64_t> next_id{1};
+};
+
+OwnSlots& own_slots() {
+  static OwnSlots* o = new OwnSlots();  // never destroyed: nodes may outlive static teardown
+  return *o;
 }
 
 std::vector<std::string> split(const char* s, char sep) {
@@ -134,8 +161,6 @@ struct NodeCore {
   std::mutex ipc_mu;
   std::unordered_map<std::string, void*> ipc_cache;  // handle bytes -> mapped base
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
-  std::unordered_map<uint64_t, Slot*> own_slots;       // for self-delivery
-  std::mutex own_mu;
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
   std::vector<uint32_t> free_flags;
@@ -145,6 +170,8 @@ struct NodeCore {
   std::mutex pool_mu;
   std::multimap<uint64_t, void*> recv_pool;
   static constexpr size_t kMaxPooled = 16;
+  std::set<int> peer_enabled;  // peer devices this node's device may access (under ipc_mu)
+  std::atomic<uint64_t> peer_copies{0}, peer_bytes{0};  // cross-GPU samples pulled
 
   void* recv_pool_get(uint64_t len, uint64_t* cap) {
     {
@@ -225,6 +252,7 @@ struct InputData {
   std::vector<uint8_t> vec;   // inline (Vec) samples stay on the host
   void* local = nullptr;      // cross-GPU edge: local copy in this node's receive pool
   uint64_t local_cap = 0;
+  int remote_device = -1;     // >= 0: `ptr` is a peer GPU's slot not yet pulled (ensure_local)
   ~InputData() {
     if (!core) return;
     if (has_token || local) {
@@ -276,7 +304,6 @@ struct dora_node {
   std::map<std::string, uint32_t> queue_size;
   std::deque<dora::Slot*> cache;
   std::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out;
-  uint64_t next_slot_id = 1;
   std::deque<std::unique_ptr<dora_event>> queue;
   bool ended = false;
   // profiling of the pack kernel on the node stream
@@ -290,8 +317,7 @@ struct dora_node {
   // host time per send phase: allocate (incl. backpressure), launch, fill sync/record, send
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
-  uint64_t peer_copies = 0, peer_bytes = 0;  // cross-GPU edges pulled into local slots
-  bool compact = false;                      // send_output uses compacting plans
+  bool compact = false;                     // send_output uses compacting plans
 };
 
 namespace dora {
@@ -299,6 +325,10 @@ namespace {
 
 void free_slot(dora_node* n, Slot* s) {
   if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(own_slots().mu);
+    own_slots().ptrs.erase(s->id);
+  }
   if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
   if (s->done) {
     (void)hipEventSynchronize(s->done);
@@ -313,10 +343,6 @@ void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
   while (n->cache.size() > kMaxCacheSize) {
     Slot* old = n->cache.front();
     n->cache.pop_front();
-    {
-      std::lock_guard<std::mutex> g(n->core->own_mu);
-      n->core->own_slots.erase(old->id);
-    }
     free_slot(n, old);
   }
 }
@@ -356,7 +382,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   }
   auto* s = new Slot();
   s->cap = len;
-  s->id = n->next_slot_id++;
+  s->id = own_slots().next_id.fetch_add(1);
   hipError_t e = hipMalloc(&s->ptr, (len + 4095) / 4096 * 4096);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
   if (e == hipSuccess && async_sends()) {
@@ -377,8 +403,8 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
                 hipGetErrorString(e));
   }
   {
-    std::lock_guard<std::mutex> g(n->core->own_mu);
-    n->core->own_slots[s->id] = s;
+    std::lock_guard<std::mutex> g(own_slots().mu);
+    own_slots().ptrs[s->id] = s->ptr;
   }
   ++n->slots_created;
   *out = s;
@@ -409,9 +435,9 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         in->len = d.ipc.len;
         void* base = nullptr;
         if (d.ipc.owner_pid == getpid()) {
-          std::lock_guard<std::mutex> g(n->core->own_mu);
-          auto it = n->core->own_slots.find(d.ipc.slot_id);
-          if (it != n->core->own_slots.end()) base = it->second->ptr;
+          std::lock_guard<std::mutex> g(own_slots().mu);
+          auto it = own_slots().ptrs.find(d.ipc.slot_id);
+          if (it != own_slots().ptrs.end()) base = it->second;
         } else {
           std::string key(reinterpret_cast<const char*>(d.ipc.handle), 64);
           std::lock_guard<std::mutex> g(n->core->ipc_mu);
@@ -525,30 +551,64 @@ void finish_input(dora_node* n, dora_event* ev) {
   }
   trace(TP_FILLED, in->token);
   if (in->len && (d.device != n->core->device || edge_copy_forced())) {
-    // Cross-GPU edge: pull the sample over xGMI into a local slot with one peer
-    // copy on the node stream, then hand the producer its slot back at once.
-    uint64_t cap = 0;
-    void* local = n->core->recv_pool_get(in->len, &cap);
-    hipError_t e = local ? hipMemcpyPeerAsync(local, n->core->device, in->ptr, d.device, in->len,
-                                              n->core->stream)
-                         : hipErrorOutOfMemory;
-    if (e == hipSuccess) e = hipStreamSynchronize(n->core->stream);
-    if (e != hipSuccess) {
-      if (local) n->core->recv_pool_put(local, cap);
-      ev->type = DORA_EVENT_ERROR;
-      ev->error = std::string("cross-GPU peer copy: ") + hipGetErrorString(e);
-      in->ptr = nullptr;
-      return;
-    }
-    in->local = local;
-    in->local_cap = cap;
-    in->ptr = local;
-    n->core->report_drop_token(in->token);
-    trace(TP_RELEASED, in->token);
-    in->has_token = false;
-    ++n->peer_copies;
-    n->peer_bytes += in->len;
+    // Cross-GPU edge: the sample is pulled over xGMI on first access to its data
+    // (ensure_local), or straight into an outgoing slot by dora_node_forward.
+    in->remote_device = d.device;
   }
+}
+
+// Enqueue one copy of `len` bytes from a slot on `src_device` (IPC-mapped) into local HBM on
+// the node stream: the pack kernel reading the peer's HBM over xGMI (default), or the copy
+// engines (DORA_GPU_PEER_COPY=sdma).
+int enqueue_peer_copy(NodeCore* c, void* dst, const void* src, int src_device, uint64_t len) {
+  if (src_device != c->device) {
+    std::lock_guard<std::mutex> g(c->ipc_mu);
+    if (!c->peer_enabled.count(src_device)) {
+      hipError_t e = hipDeviceEnablePeerAccess(src_device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(DORA_ERR_HIP, "enable peer access %d -> %d: %s", c->device, src_device,
+                    hipGetErrorString(e));
+      (void)hipGetLastError();
+      c->peer_enabled.insert(src_device);
+    }
+  }
+  if (peer_copy_mode() == PEER_SDMA) {
+    hipError_t e = hipMemcpyPeerAsync(dst, c->device, src, src_device, len, c->stream);
+    if (e != hipSuccess) return fail(DORA_ERR_HIP, "hipMemcpyPeerAsync: %s", hipGetErrorString(e));
+    return DORA_OK;
+  }
+  Segment seg{src, 0, len};
+  return launch_pack(&seg, 1, ARROW_DEVICE_ROCM, static_cast<uint8_t*>(dst), c->stream, nullptr,
+                     nullptr);
+}
+
+// Pull a cross-GPU input into this node's receive pool (complete on return) and hand the
+// producer its slot back at once.
+int ensure_local(InputData* in) {
+  if (!in || in->remote_device < 0) return DORA_OK;
+  NodeCore* c = in->core.get();
+  uint64_t cap = 0;
+  void* local = c->recv_pool_get(in->len, &cap);
+  if (!local) return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->len);
+  int rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->len);
+  if (rc == DORA_OK) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "cross-GPU pull: %s", hipGetErrorString(e));
+  }
+  if (rc != DORA_OK) {
+    c->recv_pool_put(local, cap);
+    return rc;
+  }
+  in->local = local;
+  in->local_cap = cap;
+  in->ptr = local;
+  in->remote_device = -1;
+  c->report_drop_token(in->token);
+  trace(TP_RELEASED, in->token);
+  in->has_token = false;
+  c->peer_copies.fetch_add(1, std::memory_order_relaxed);
+  c->peer_bytes.fetch_add(in->len, std::memory_order_relaxed);
+  return DORA_OK;
 }
 
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
@@ -727,6 +787,68 @@ TimingPair* next_timing_pair(dora_node* n, uint64_t bytes) {
   return &p;
 }
 
+// Tell receivers when the fill enqueued on the node stream is complete.
+hipError_t order_fill(dora_node* n, dora_sample* s) {
+  hipStream_t st = n->core->stream;
+  if (s->slot->flag >= 0) {
+    // async: the stream writes the send epoch into the slot's fill flag once the fill has
+    // completed; the receiver polls it, the sender moves on
+    s->epoch = ++n->core->epoch;
+    s->fill = FILL_FLAG;
+    return hipStreamWriteValue64(st, n->core->flag_dev(s->slot->flag), s->epoch, 0);
+  }
+  if (s->slot->done) {
+    // async fallback: interprocess event
+    s->fill = FILL_EVENT;
+    return hipEventRecord(s->slot->done, st);
+  }
+  // sync: the sample must be complete before its descriptor leaves the process
+  return hipStreamSynchronize(st);
+}
+
+// Re-send a received input on an output with its type info (a relay stage): one copy into a
+// fresh slot of this node — for a cross-GPU input straight from the peer's slot over xGMI, so
+// a pipeline hop moves the payload once.
+int forward_input(dora_node* n, const char* output_id, const dora_event* ev, const uint8_t* params,
+                  size_t params_len) {
+  InputData* in = ev->data.get();
+  const uint64_t len = in->len;
+  dora_sample* s = nullptr;
+  int rc = alloc_sample(n, len, &s);
+  if (rc != DORA_OK) return rc;
+  const bool device_src = in->has_token || in->local;
+  if (len && !s->slot) {
+    if (device_src) {
+      delete s;
+      return fail(DORA_ERR_INVALID, "host-only node cannot forward device-resident data");
+    }
+    std::memcpy(s->vec.data(), in->ptr, len);
+  } else if (len) {
+    Segment seg{in->ptr, 0, len};
+    if (in->remote_device >= 0) {
+      rc = enqueue_peer_copy(n->core.get(), s->slot->ptr, in->ptr, in->remote_device, len);
+      if (rc == DORA_OK) {
+        n->core->peer_copies.fetch_add(1, std::memory_order_relaxed);
+        n->core->peer_bytes.fetch_add(len, std::memory_order_relaxed);
+      }
+    } else {
+      rc = launch_pack(&seg, 1, device_src ? ARROW_DEVICE_ROCM : ARROW_DEVICE_CPU,
+                       static_cast<uint8_t*>(s->slot->ptr), n->core->stream, nullptr, nullptr);
+    }
+    hipError_t e = rc == DORA_OK ? order_fill(n, s) : hipSuccess;
+    if (rc == DORA_OK && e != hipSuccess)
+      rc = fail(DORA_ERR_HIP, "forward: %s", hipGetErrorString(e));
+    if (rc != DORA_OK) {
+      add_to_cache(n, s->slot);
+      delete s;
+      return rc;
+    }
+  }
+  // the input keeps the producer's token until this node's stream has passed the copy
+  // (InputData's destructor), so the producer cannot refill the slot under it
+  return send_sample(n, output_id, ev->meta.type_info, params, params_len, s);
+}
+
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
                   size_t params_len) {
   dora_sample* s = nullptr;
@@ -759,21 +881,7 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       return rc;
     }
     t2 = mono_ns();
-    hipError_t e;
-    if (s->slot->flag >= 0) {
-      // async: the stream writes the send epoch into the slot's fill flag once the pack has
-      // completed; the receiver polls it, the sender moves on
-      s->epoch = ++n->core->epoch;
-      e = hipStreamWriteValue64(st, n->core->flag_dev(s->slot->flag), s->epoch, 0);
-      s->fill = FILL_FLAG;
-    } else if (s->slot->done) {
-      // async fallback: interprocess event
-      e = hipEventRecord(s->slot->done, st);
-      s->fill = FILL_EVENT;
-    } else {
-      // sync: the sample must be complete before its descriptor leaves the process
-      e = hipStreamSynchronize(st);
-    }
+    hipError_t e = order_fill(n, s);
     if (e != hipSuccess) {
       add_to_cache(n, s->slot);
       delete s;
@@ -1049,6 +1157,10 @@ const char* dora_event_error(const dora_event* e) { return e ? e->error.c_str() 
 int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
   if (!e || !ptr || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!e->data) return dora::fail(DORA_ERR_INVALID, "event has no data");
+  DORA_GUARD_BEGIN
+  int rc = dora::ensure_local(e->data.get());
+  if (rc != DORA_OK) return rc;
+  DORA_GUARD_END
   *ptr = e->data->ptr;
   *len = e->data->len;
   return DORA_OK;
@@ -1081,6 +1193,10 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
     return dora::fail(DORA_ERR_INVALID, "not an input event");
   if (!e->data->ptr && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", e->error.c_str());
+  DORA_GUARD_BEGIN
+  int rc = dora::ensure_local(e->data.get());
+  if (rc != DORA_OK) return rc;
+  DORA_GUARD_END
   if (!e->data->has_token && !e->data->local && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "inline (host Vec) sample: read it with dora_event_data");
   std::shared_ptr<void> keep = e->data;
@@ -1089,6 +1205,18 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
 }
 
 void dora_event_free(dora_event* e) { delete e; }
+
+int dora_node_forward(dora_node* n, const char* output_id, const dora_event* ev,
+                      const uint8_t* params, size_t params_len) {
+  if (!n || !output_id || !ev) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (ev->type != DORA_EVENT_INPUT || !ev->data)
+    return dora::fail(DORA_ERR_INVALID, "only input events can be forwarded");
+  if (!ev->data->ptr && ev->data->len)
+    return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", ev->error.c_str());
+  DORA_GUARD_BEGIN
+  return dora::forward_input(n, output_id, ev, params, params_len);
+  DORA_GUARD_END
+}
 
 int dora_node_stats(dora_node* n, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs) {
@@ -1111,8 +1239,8 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
 
 int dora_node_peer_stats(dora_node* n, uint64_t* copies, uint64_t* bytes) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
-  if (copies) *copies = n->peer_copies;
-  if (bytes) *bytes = n->peer_bytes;
+  if (copies) *copies = n->core->peer_copies.load();
+  if (bytes) *bytes = n->core->peer_bytes.load();
   return DORA_OK;
 }
 

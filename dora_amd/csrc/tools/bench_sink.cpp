@@ -73,10 +73,15 @@ int main() {
     if (rc != 0) break;
     const int type = dora_event_type(ev);
     if (type == DORA_EVENT_INPUT) {
-      const uint64_t t = now_ns();
+      // data access first: a cross-GPU input is pulled into local HBM there, and the latency
+      // counts until the sample is readable on this GPU
       const void* p = nullptr;
       size_t len = 0;
-      dora_event_data(ev, &p, &len);
+      if (dora_event_data(ev, &p, &len) != 0) {
+        std::fprintf(stderr, "sink: input data: %s\n", dora_gpu_last_error());
+        ++errors;
+      }
+      const uint64_t t = now_ns();
       const uint8_t* pp = nullptr;
       size_t pl = 0;
       dora_event_parameters(ev, &pp, &pl);

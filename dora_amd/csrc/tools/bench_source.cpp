@@ -1,0 +1,200 @@
+// dora-gpu-bench-source: the benchmark node (examples/benchmark/node/src/main.rs:1-73) as a
+// native process for the multi-GPU configurations (BASELINE.json configs C4 fan-out and C5
+// chain), where the producer sits on one GPU and its receivers on others.  Payloads are
+// device-resident splitmix64 bytes (seed 0xD05A + size, like bench.py); the first messages of
+// every size carry their csum64 so receivers verify them bit-exact after the xGMI pulls.
+//
+// Modes (reference: latency mode = spaced messages, throughput mode = back-to-back):
+//   latency:    DORA_BENCH_LAT_SIZES (comma list) x DORA_BENCH_LAT_N messages,
+//               DORA_BENCH_LAT_GAP_US apart (33333 = 30 Hz, C5);
+//   throughput: DORA_BENCH_TP_N messages of DORA_BENCH_TP_SIZE bytes back-to-back, closed by an
+//               ack request that every one of the DORA_BENCH_ACKS receivers acknowledges.
+// Outputs `latency` and `throughput` (warmup and ack requests go on `throughput`, like the
+// reference node's two outputs); every input is an ack channel from a receiver.
+//   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE, DORA_BENCH_RESULT (path)
+#include <time.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "dora_gpu.h"
+#include "params.h"
+
+namespace {
+
+uint64_t mono() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+uint64_t realtime() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+long env_long(const char* k, long d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atol(v) : d;
+}
+
+std::vector<uint64_t> env_sizes(const char* k) {
+  std::vector<uint64_t> out;
+  const char* v = std::getenv(k);
+  if (!v) return out;
+  std::string cur;
+  for (const char* p = v;; ++p) {
+    if (*p == ',' || !*p) {
+      if (!cur.empty()) out.push_back(std::strtoull(cur.c_str(), nullptr, 10));
+      cur.clear();
+      if (!*p) break;
+    } else {
+      cur += *p;
+    }
+  }
+  return out;
+}
+
+struct Source {
+  void* ptr = nullptr;
+  uint64_t csum = 0;
+};
+
+}  // namespace
+
+int main() {
+  dora_node* node = nullptr;
+  if (dora_node_init_from_env(&node) != 0) {
+    std::fprintf(stderr, "source: init failed: %s\n", dora_gpu_last_error());
+    return 1;
+  }
+  const char* out_path = std::getenv("DORA_BENCH_RESULT");
+  const auto lat_sizes = env_sizes("DORA_BENCH_LAT_SIZES");
+  const long lat_n = env_long("DORA_BENCH_LAT_N", 30);
+  const long gap_us = env_long("DORA_BENCH_LAT_GAP_US", 33333);
+  const uint64_t tp_size = static_cast<uint64_t>(env_long("DORA_BENCH_TP_SIZE", 0));
+  const long tp_n = env_long("DORA_BENCH_TP_N", 100);
+  const long acks = env_long("DORA_BENCH_ACKS", 1);
+  const long verify_n = env_long("DORA_BENCH_VERIFY", 2);
+  dora_stream_t st = dora_node_stream(node);
+  int errors = 0;
+
+  std::map<uint64_t, Source> src;
+  std::vector<uint64_t> all = lat_sizes;
+  if (tp_size) all.push_back(tp_size);
+  for (uint64_t s : all) {
+    if (src.count(s) || s == 0) continue;
+    Source& x = src[s];
+    if (dora_gpu_malloc(&x.ptr, s) != 0 || dora_gpu_fill_splitmix(x.ptr, s, 0xD05A + s, st) != 0 ||
+        dora_gpu_csum64_sync(x.ptr, s, st, &x.csum) != 0) {
+      std::fprintf(stderr, "source: payload of %llu B: %s\n", (unsigned long long)s,
+                   dora_gpu_last_error());
+      return 1;
+    }
+  }
+
+  int64_t seq = 0;
+  auto send = [&](const char* output, uint64_t size, bool verify) {
+    std::map<std::string, Param> p;
+    p["seq"].i = seq++;
+    p["t_start"].i = static_cast<int64_t>(realtime());
+    if (verify) {
+      p["csum"].i = static_cast<int64_t>(src[size].csum);
+      p["verify"].tag = 0;
+      p["verify"].i = 1;
+    }
+    auto enc = encode_params(p);
+    if (dora_node_send_output_bytes(node, output, src[size].ptr, size, ARROW_DEVICE_ROCM,
+                                    enc.data(), enc.size()) != 0) {
+      std::fprintf(stderr, "source: send failed: %s\n", dora_gpu_last_error());
+      ++errors;
+    }
+  };
+  // ack barrier: every receiver acknowledges `seq` (sink `ack` output, any input of ours)
+  auto barrier = [&]() -> bool {
+    std::map<std::string, Param> p;
+    const int64_t want = seq++;
+    p["seq"].i = want;
+    p["ack"].tag = 0;
+    p["ack"].i = 1;
+    auto enc = encode_params(p);
+    if (dora_node_send_output_bytes(node, "throughput", nullptr, 0, ARROW_DEVICE_ROCM, enc.data(),
+                                    enc.size()) != 0) {
+      ++errors;
+      return false;
+    }
+    std::set<std::string> got;
+    const uint64_t t0 = mono();
+    while (static_cast<long>(got.size()) < acks) {
+      if (mono() - t0 > 120000000000ull) {
+        std::fprintf(stderr, "source: %zu/%ld acks for seq %lld\n", got.size(), acks,
+                     (long long)want);
+        ++errors;
+        return false;
+      }
+      dora_event* ev = nullptr;
+      if (dora_node_next_event(node, 1000000, &ev) != 0) continue;
+      if (dora_event_type(ev) == DORA_EVENT_INPUT) {
+        const uint8_t* pp = nullptr;
+        size_t pl = 0;
+        dora_event_parameters(ev, &pp, &pl);
+        auto ap = decode_params(pp, pl);
+        if (ap.count("seq") && ap["seq"].i == want) got.insert(dora_event_id(ev));
+      }
+      dora_event_free(ev);
+    }
+    return true;
+  };
+
+  // warmup: every size once per receiver path, first ones verified
+  for (auto& kv : src)
+    for (long k = 0; k < 3; ++k) send("throughput", kv.first, k < verify_n);
+  bool ok = barrier();
+
+  // latency mode
+  for (uint64_t s : lat_sizes) {
+    if (!ok) break;
+    for (long k = 0; k < lat_n; ++k) {
+      if (s) send("latency", s, k < verify_n);
+      usleep(static_cast<useconds_t>(gap_us));
+    }
+  }
+  if (ok && !lat_sizes.empty()) ok = barrier();
+
+  // throughput mode
+  double tp_s = 0;
+  if (ok && tp_size) {
+    dora_node_set_profiling(node, 0);  // resets the send-phase counters, no kernel stamps
+    const uint64_t t0 = mono();
+    for (long k = 0; k < tp_n; ++k) send("throughput", tp_size, false);
+    ok = barrier();
+    tp_s = double(mono() - t0) / 1e9;
+  }
+  double phase[4] = {0, 0, 0, 0};
+  uint64_t cnt = 0;
+  dora_node_send_profile(node, phase, 4, &cnt);
+  uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
+  dora_node_stats(node, &slots, &hits, &inflight, &dropped);
+
+  FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
+  const double delivered = double(tp_size) * double(tp_n) * double(acks);
+  std::fprintf(f,
+               "{\"errors\": %d, \"ok\": %s, \"receivers\": %ld, \"tp_size\": %llu, \"tp_n\": %ld, "
+               "\"tp_seconds\": %.6f, \"tp_delivered_GBps\": %.3f, \"tp_per_receiver_GBps\": %.3f, "
+               "\"send_phase_us\": {\"alloc_us\": %.2f, \"launch_us\": %.2f, \"fill_us\": %.2f, "
+               "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu}\n",
+               errors, ok ? "true" : "false", acks, (unsigned long long)tp_size, tp_n, tp_s,
+               tp_s > 0 ? delivered / tp_s / 1e9 : 0.0,
+               tp_s > 0 ? double(tp_size) * double(tp_n) / tp_s / 1e9 : 0.0, phase[0], phase[1],
+               phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits);
+  if (f != stdout) std::fclose(f);
+  for (auto& kv : src) dora_gpu_free(kv.second.ptr);
+  dora_node_free(node);
+  return errors || !ok ? 1 : 0;
+}

@@ -1,7 +1,8 @@
-// dora-gpu-relay: forwards every input `in` to output `out` with the same parameters — one stage
+// dora-gpu-relay: forwards every input to the output of the same name with the same parameters
+// (inputs `latency`, `throughput` -> outputs `latency`, `throughput`) — one stage
 // of the C5 pipeline (BASELINE.json configs[4]: one node per GPU, peer copies over xGMI).  An
-// input whose slot lives on another GPU arrives already pulled into a local slot (node.cpp); the
-// relay then packs it into its own output slot, which the next stage pulls in turn.
+// input whose slot lives on another GPU is copied over xGMI straight into the relay's own output
+// slot (dora_node_forward), which the next stage pulls in turn.
 //   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE
 #include <cstdio>
 
@@ -19,26 +20,11 @@ int main() {
     if (dora_node_next_event(node, -1, &ev) != 0) break;
     const int type = dora_event_type(ev);
     if (type == DORA_EVENT_INPUT) {
-      const void* p = nullptr;
-      size_t len = 0;
       const uint8_t* params = nullptr;
       size_t plen = 0;
-      const uint8_t* ti = nullptr;
-      size_t tilen = 0;
-      dora_event_data(ev, &p, &len);
       dora_event_parameters(ev, &params, &plen);
-      dora_event_type_info(ev, &ti, &tilen);
-      int rc;
-      if (len == 0) {
-        rc = dora_node_send_output_bytes(node, "out", nullptr, 0, ARROW_DEVICE_ROCM, params, plen);
-      } else {
-        // same type info, fresh sample: allocate, copy on the node stream, send
-        dora_sample* s = nullptr;
-        rc = dora_node_allocate_data_sample(node, len, &s);
-        if (rc == 0) rc = dora_gpu_memcpy_async(dora_sample_data(s), p, len, dora_node_stream(node));
-        if (rc == 0) rc = dora_gpu_stream_sync(dora_node_stream(node));
-        if (rc == 0) rc = dora_node_send_output_sample(node, "out", ti, tilen, params, plen, s);
-      }
+      // one copy per hop: a cross-GPU input goes from the peer's slot straight into ours
+      int rc = dora_node_forward(node, dora_event_id(ev), ev, params, plen);
       if (rc != 0) {
         std::fprintf(stderr, "relay: forward failed: %s\n", dora_gpu_last_error());
         ++errors;

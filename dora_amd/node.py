@@ -145,6 +145,14 @@ class Node:
         """Send device arrays with compacting plans (slices move only their own bytes)."""
         call("dora_node_set_compact", self.handle, int(enable))
 
+    def forward(self, output_id: str, event: dict, metadata: Optional[dict] = None):
+        """Re-send a received input on `output_id` with its type info (dora_node_forward): one
+        copy, a cross-GPU input straight from the peer's slot.  Parameters default to the
+        input's own."""
+        params = encode_parameters(event.get("metadata") if metadata is None else metadata)
+        call("dora_node_forward", self.handle, output_id.encode(), event["_event"].ptr,
+             _u8(params), len(params))
+
     def close_outputs(self, outputs):
         arr = (ctypes.c_char_p * len(outputs))(*[o.encode() for o in outputs])
         call("dora_node_close_outputs", self.handle, arr, len(outputs))

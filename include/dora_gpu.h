@@ -264,7 +264,9 @@ int dora_node_next_event(dora_node* node, int64_t timeout_us, dora_event** out);
 int dora_event_type(const dora_event* ev);
 const char* dora_event_id(const dora_event* ev);
 const char* dora_event_error(const dora_event* ev);
-/* Raw sample of an input: device pointer (mapped IPC slot) or host pointer for Vec data. */
+/* Raw sample of an input: device pointer (mapped IPC slot) or host pointer for Vec data.  An
+ * input whose slot lives on another GPU is pulled into local HBM on the first call (complete on
+ * return; see dora_node_peer_stats). */
 int dora_event_data(const dora_event* ev, const void** ptr, size_t* len);
 int dora_event_is_device(const dora_event* ev);
 /* Serialized ArrowTypeInfo / MetadataParameters / timestamp of the input's Metadata. */
@@ -277,13 +279,21 @@ int dora_event_array(const dora_event* ev, struct ArrowArray* out_array,
                      struct ArrowSchema* out_schema);
 /* Drop the event; the drop token is reported once no array references the data any more. */
 void dora_event_free(dora_event* ev);
+/* Relay stage (new; a reference relay node does recv -> send_output_sample with a copy of the
+ * data, apis/rust/node/src/node/mod.rs:180-275): send the input `ev` on `output_id` with its
+ * ArrowTypeInfo and the given parameters.  The payload moves once: a cross-GPU input is copied
+ * from the peer's slot straight into this node's new slot.  `ev` stays valid (free it after). */
+int dora_node_forward(dora_node* node, const char* output_id, const dora_event* ev,
+                      const uint8_t* params, size_t params_len);
 
 int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs);
-/* Cross-GPU edges: inputs whose slot lives on another GPU are pulled into a local
- * receive slot with one hipMemcpyPeerAsync over xGMI and the producer's token is returned at
- * once.  Counts and bytes of such pulls.  DORA_GPU_EDGE_COPY=1 forces the path on same-GPU
- * edges. */
+/* Cross-GPU edges: an input whose slot lives on another GPU is pulled over xGMI
+ * into a local receive slot on first access (dora_event_data / dora_event_array) and the
+ * producer's token is returned at once; dora_node_forward pulls it straight into an outgoing
+ * slot instead.  The pull is the pack kernel reading the peer's HBM (default) or the copy
+ * engines (DORA_GPU_PEER_COPY=sdma).  Counts and bytes of such pulls.  DORA_GPU_EDGE_COPY=1
+ * forces the path on same-GPU edges. */
 int dora_node_peer_stats(dora_node* node, uint64_t* copies, uint64_t* bytes);
 /* Pack-kernel timing on the node stream (HIP events around every pack launch). */
 int dora_node_set_profiling(dora_node* node, int enable);

@@ -48,3 +48,39 @@ def test_pmc_traffic_lookup():
     t = bench.pmc_traffic(40960000)
     assert t is not None and abs(t[1] / 81920000 - 1) < 0.05
     assert bench.pmc_traffic(123) is None
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_cross_gpu_descriptors(n, tmp_path):
+    """C4 fan-out / C5 chain dataflows of bench.py (N>1): valid descriptors, one stage per GPU."""
+    import bench
+    from dora_amd.dataflow import daemon_spec, parse_descriptor
+    c4 = parse_descriptor(bench.c4_descriptor(n, str(tmp_path)))
+    assert [x.gpu for x in c4] == list(range(n))
+    assert len([x for x in c4 if x.id.startswith("sink")]) == n - 1
+    assert c4[0].env["DORA_BENCH_ACKS"] == str(n - 1)
+    assert c4[0].env["DORA_BENCH_TP_SIZE"] == str(1920 * 1080 * 3)
+    c5 = parse_descriptor(bench.c5_descriptor(n, str(tmp_path), "sdma"))
+    assert [x.gpu for x in c5] == list(range(n))
+    assert [x.path for x in c5] == (["dora-gpu-bench-source"] + ["dora-gpu-relay"] * (n - 2)
+                                    + ["dora-gpu-bench-sink"])
+    for prev, cur in zip(c5, c5[1:]):
+        assert cur.inputs["throughput"][0] == prev.id and cur.env["DORA_GPU_PEER_COPY"] == "sdma"
+    assert "input source ack0 sink ack" in daemon_spec(c5)
+
+
+def test_summarize_cross():
+    import bench
+    src = {"ok": True, "receivers": 2, "tp_size": 100, "tp_n": 10, "tp_delivered_GBps": 200.0,
+           "tp_per_receiver_GBps": 100.0, "send_phase_us": {}}
+    sink = {"errors": 0, "dropped_inputs": 0, "series": [
+        {"input": "latency", "size": 100, "n": 5, "p50_us": 10.0, "p99_us": 20.0,
+         "full_p50_us": 12.0, "full_p99_us": 22.0, "verified": 2, "mismatches": 0},
+        {"input": "throughput", "size": 0, "n": 3, "p50_us": 1.0, "p99_us": 1.0,
+         "full_p50_us": 0, "full_p99_us": 0, "verified": 0, "mismatches": 0}]}
+    r = bench.summarize_cross("c4", src, {"sink1": sink, "sink2": sink}, {"source": 0}, {})
+    assert r["ok"] and r["parity"]["verified_msgs"] == 4
+    assert r["roofline"]["frac"] == round(100.0 / bench.XGMI_LINK_GBPS, 4)
+    assert len(r["latency_us"]["100"]) == 2
+    bad = dict(sink, series=[dict(sink["series"][0], mismatches=1)])
+    assert not bench.summarize_cross("c4", src, {"s": bad}, {}, {})["ok"]

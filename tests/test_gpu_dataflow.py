@@ -171,23 +171,25 @@ def test_host_pyarrow_send_to_device_receiver(launcher):
         assert results[seq]["arrow_equal_len"] == len(arr)
 
 
-def test_pipeline_with_peer_copy_edges(launcher, tmp_path):
+@pytest.mark.parametrize("peer_copy", ["kernel", "sdma"])
+def test_pipeline_with_peer_copy_edges(launcher, tmp_path, peer_copy):
     """C5 shape on one GPU: node -> relay -> sink with the cross-GPU pull path forced
-    (DORA_GPU_EDGE_COPY=1: hipMemcpyPeerAsync into a local slot, token returned at once); every
-    payload arrives bit-exact after two hops."""
+    (DORA_GPU_EDGE_COPY=1): the relay forwards each input straight from the producer's slot into
+    its own (dora_node_forward, one copy per hop), the sink pulls it into a receive slot; every
+    payload arrives bit-exact after two hops, with both pull engines."""
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.node import Node
     from dora_amd.verify import to_i64
     from dora_amd.workloads import payload_seed
     res = str(tmp_path / "sink.json")
-    env = {"DORA_GPU_EDGE_COPY": "1"}
+    env = {"DORA_GPU_EDGE_COPY": "1", "DORA_GPU_PEER_COPY": peer_copy}
     desc = {"nodes": [
         {"id": "node", "path": "dynamic", "outputs": ["data"], "inputs": {"ack": "sink/ack"}},
-        {"id": "relay", "path": "dora-gpu-relay", "outputs": ["out"], "env": env,
-         "inputs": {"in": {"source": "node/data", "queue_size": 100}}},
+        {"id": "relay", "path": "dora-gpu-relay", "outputs": ["data"], "env": env,
+         "inputs": {"data": {"source": "node/data", "queue_size": 100}}},
         {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
-         "inputs": {"data": {"source": "relay/out", "queue_size": 100}},
+         "inputs": {"data": {"source": "relay/data", "queue_size": 100}},
          "env": dict(env, DORA_BENCH_RESULT=res)},
     ]}
     sizes = [4096, 409600, 40960000]
@@ -202,6 +204,7 @@ def test_pipeline_with_peer_copy_edges(launcher, tmp_path):
             for k in range(4):
                 node.send_output_device_bytes("data", buf.ptr, size,
                                               {"csum": to_i64(c), "verify": True, "seq": k})
+            s.sync()
             buf.free()
         node.close()
         codes = df.wait(120)
@@ -213,6 +216,79 @@ def test_pipeline_with_peer_copy_edges(launcher, tmp_path):
         assert got[size]["verified"] == 4 and got[size]["mismatches"] == 0
     relay = json.loads(relay_log.strip().splitlines()[-1])
     assert relay["relay_peer_copies"] == 12 and relay["errors"] == 0
+
+
+def test_python_forward(launcher, tmp_path):
+    """Node.forward from Python: a relay written against the Python API keeps type info and
+    parameters (C3 point cloud through two hops, checked by the sink's checksum)."""
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    from dora_amd.device import DeviceArray
+    from dora_amd.arrow_utils import Plan
+    from dora_amd import device
+    res = str(tmp_path / "sink.json")
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["data"]},
+        {"id": "relay", "path": "dynamic", "outputs": ["data"], "inputs": {"data": "node/data"}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"data": {"source": "relay/data", "queue_size": 100}},
+         "env": {"DORA_BENCH_RESULT": res}},
+    ]}
+    import threading
+    from dora_amd.workloads import point_cloud
+    cloud = point_cloud(n_points=20000)
+    with Dataflow(desc, launcher=launcher) as df:
+        relay_err = []
+
+        def relay():
+            try:
+                r = Node("relay", dataflow=df.shm, device=0)
+                for ev in r:
+                    if ev["type"] == "INPUT":
+                        r.forward("data", ev)
+                        assert ev["type_info"].to_json()["len"] == len(cloud)
+                r.close()
+            except Exception as e:  # noqa: BLE001
+                relay_err.append(e)
+        t = threading.Thread(target=relay)
+        t.start()
+        node = Node("node", dataflow=df.shm, device=0)
+        s = device.Stream()
+        with DeviceArray.from_pyarrow(cloud) as da, Plan.of(da) as p:
+            ref = device.DeviceBuffer(p.size)
+            p.pack(ref.ptr, p.size, s)
+            s.sync()
+            c = device.csum64(ref.ptr, p.size, s)
+            ref.free()
+            for k in range(3):
+                node.send_output("data", da, {"csum": to_i64(c), "verify": True, "seq": k})
+        node.close()
+        t.join(60)
+        codes = df.wait(60)
+    assert not relay_err, relay_err
+    assert codes["sink"] == 0
+    out = json.load(open(res))
+    assert sum(x["verified"] for x in out["series"]) == 3
+    assert sum(x["mismatches"] for x in out["series"]) == 0
+
+
+def test_cross_gpu_bench_runs_on_one_gpu(launcher):
+    """bench.py's C4 fan-out and C5 chain machinery with every stage on GPU 0 and the pull path
+    forced: sources, relays and sinks finish, every verified payload is bit-exact."""
+    sys.path.insert(0, ROOT)
+    import bench
+    out = bench.run_cross_gpu(
+        3, launcher, timeout=180,
+        runs=[("c4", bench.c4_descriptor, "kernel"), ("c5", bench.c5_descriptor, "kernel"),
+              ("c5_sdma", bench.c5_descriptor, "sdma")],
+        gpu=lambda g: 0, env={"DORA_GPU_EDGE_COPY": "1"}, tp_n=20)
+    for name, r in out.items():
+        assert r.get("ok"), (name, r)
+        assert r["parity"]["mismatches"] == 0 and r["parity"]["verified_msgs"] > 0, r
+        assert r["dropped_inputs"] == 0
+    assert out["c4"]["receivers"] == 2
+    assert set(out["c5"]["latency_us"]) == {"4096", "40960000"}
 
 
 def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
