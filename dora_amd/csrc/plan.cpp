@@ -9,6 +9,7 @@
 //   * nulls: kept only when the null count is non-zero (ArrayDataBuilder::build filter).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -18,6 +19,10 @@
 #include "plan.h"
 
 namespace dora {
+
+int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
+                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
+
 namespace {
 
 bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
@@ -150,20 +155,87 @@ void serialize_schema(const ArrowSchema* s, bool top, std::vector<uint8_t>& o) {
 
 namespace {
 
+// Host reads a plan needs from the array (last offsets of Utf8/Binary data, validity bitmaps).
+// Device arrays: DIRECT does one blocking hipMemcpy per read; the reference walk (build_plan)
+// instead runs twice — COLLECT records every read (no address depends on a value read, so the
+// second walk asks for the same ranges in the same order), one gather launch of the pack kernel
+// copies them all into pinned host memory, REPLAY serves them from there.  One launch + one
+// sync per plan instead of one blocking copy per buffer.
 struct Reader {
-  ArrowDeviceType dev;
+  ArrowDeviceType dev = ARROW_DEVICE_CPU;
+  enum Mode { DIRECT, COLLECT, REPLAY } mode = DIRECT;
+  mutable std::vector<Segment> reqs;  // src, offset in the staging buffer, len
+  mutable uint64_t total = 0;
+  mutable size_t cursor = 0;
+  const uint8_t* staged = nullptr;
+
   void read(void* dst, const void* src, size_t n) const {
     if (n == 0) return;
-    if (dev == ARROW_DEVICE_ROCM) {
+    if (dev != ARROW_DEVICE_ROCM) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    if (mode == COLLECT) {
+      reqs.push_back({src, total, n});
+      total += (n + 15) / 16 * 16;
+      std::memset(dst, 0, n);
+    } else if (mode == REPLAY) {
+      if (cursor >= reqs.size() || reqs[cursor].src != src || reqs[cursor].len != n)
+        throw std::logic_error("plan: replayed read differs from the collected one");
+      std::memcpy(dst, staged + reqs[cursor++].dst_off, n);
+    } else {
       hipError_t e = hipMemcpy(dst, src, n, hipMemcpyDeviceToHost);
       if (e != hipSuccess)
         throw std::runtime_error(std::string("hipMemcpy D2H during plan: ") +
                                  hipGetErrorString(e));
-    } else {
-      std::memcpy(dst, src, n);
     }
   }
 };
+
+// Pinned staging buffer + stream of this thread for the current device (plans are built on the
+// caller's thread; the stream is a blocking one, ordered after legacy-stream work like the
+// hipMemcpy it replaces).
+struct GatherCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* host = nullptr;
+  void* host_dev = nullptr;
+  uint64_t cap = 0;
+};
+
+const uint8_t* gather_to_host(const std::vector<Segment>& reqs, uint64_t total) {
+  thread_local std::vector<GatherCtx> ctxs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw std::runtime_error("plan: no current device");
+  GatherCtx* c = nullptr;
+  for (auto& x : ctxs)
+    if (x.device == dev) c = &x;
+  if (!c) {
+    ctxs.push_back(GatherCtx{});
+    c = &ctxs.back();
+    c->device = dev;
+    if (hipStreamCreate(&c->stream) != hipSuccess)
+      throw std::runtime_error("plan: gather stream");
+  }
+  if (c->cap < total) {
+    if (c->host) (void)hipHostFree(c->host);
+    c->host = nullptr;
+    c->cap = 0;
+    const uint64_t cap = std::max<uint64_t>(total, 1 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->host), cap, hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&c->host_dev, c->host, 0) != hipSuccess)
+      throw std::runtime_error("plan: pinned staging buffer");
+    c->cap = cap;
+  }
+  int rc = launch_pack(reqs.data(), reqs.size(), ARROW_DEVICE_ROCM,
+                       static_cast<uint8_t*>(c->host_dev), c->stream, nullptr, nullptr);
+  if (rc != DORA_OK) throw std::runtime_error(std::string("plan: gather: ") + dora_gpu_last_error());
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("plan: gather: ") + hipGetErrorString(e));
+  return c->host;
+}
 
 uint64_t count_nulls(const std::vector<uint8_t>& v, uint64_t off, uint64_t len) {
   uint64_t n = 0;
@@ -429,7 +501,8 @@ int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, Arrow
   p->dev = dev;
   p->compact = true;
   try {
-    Reader rd{dev};
+    Reader rd;
+    rd.dev = dev;
     uint64_t next = 0;
     walk_compact(array, schema, rd, uint64_t(array->offset), uint64_t(array->length), next,
                  p->segs, p->root);
@@ -454,8 +527,21 @@ int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceTy
   auto* p = new dora_plan();
   p->dev = dev;
   try {
-    Reader rd{dev};
+    Reader rd;
+    rd.dev = dev;
     uint64_t next = 0;
+    if (dev == ARROW_DEVICE_ROCM) {
+      rd.mode = Reader::COLLECT;
+      dora_plan scratch;
+      walk(array, schema, rd, next, scratch.segs, scratch.root);
+      if (!rd.reqs.empty()) {
+        rd.staged = gather_to_host(rd.reqs, rd.total);
+        rd.mode = Reader::REPLAY;
+      } else {
+        rd.mode = Reader::DIRECT;
+      }
+      next = 0;
+    }
     walk(array, schema, rd, next, p->segs, p->root);
     p->size = next;
   } catch (const std::domain_error& e) {
