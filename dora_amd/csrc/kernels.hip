@@ -35,6 +35,9 @@ struct PackSeg {
 
 struct PackArgs {
   uint8_t* dst;
+  uint64_t* flag;        // fill flag to signal at the end (null: none)
+  uint32_t* counter;     // workgroups done (reset by the last one)
+  uint64_t epoch;
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
   uint32_t chunk_end[kMaxSegs];
@@ -111,7 +114,7 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
 }
 
 template <int U, bool NT>
-__global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
+__device__ __forceinline__ void pack_chunk(const PackArgs& args) {
   const uint32_t chunk = blockIdx.x;
   uint32_t s = 0;
   while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
@@ -162,6 +165,30 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
     case 2: copy_shifted<U, NT, 2>(dp, sbase, b, nunits); break;
     default: copy_shifted<U, NT, 3>(dp, sbase, b, nunits); break;
   }
+}
+
+// The sample is complete when every workgroup's stores are visible at the device coherence
+// point: each wave releases at agent scope (its stores done, its XCD's L2 written back), the
+// workgroup counts itself in, and the last one stores the send epoch into the host fill flag
+// with a system-scope release.  This replaces a separate stream write-value packet (a ~4 us
+// blit kernel plus a kernel boundary per message on ROCm 7).
+__device__ __forceinline__ void signal_fill(const PackArgs& a) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t done =
+        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
+  pack_chunk<U, NT>(args);
+  if (args.flag) signal_fill(args);
 }
 
 // Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
@@ -347,7 +374,9 @@ unsigned grid_for(uint64_t items) {
 // launches go through hipExtLaunchKernelGGL, whose dispatch packet stamps the first kernel's
 // begin into `ev_start` and the last kernel's end into `ev_stop`.
 int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_t* dst,
-                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
+                const FillSignal* signal, bool* signalled) {
+  if (signalled) *signalled = false;
   bool any_x = false;
   for (size_t i = 0; i < n_in; ++i) any_x |= segs_in[i].op != SEG_COPY;
   if (dev == ARROW_DEVICE_CPU) {
@@ -394,6 +423,11 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     }
     a.nseg = static_cast<uint32_t>(m);
     const bool first = launch == 0, last = launch + 1 == n_launch;
+    if (last && signal) {
+      a.flag = signal->flag;
+      a.counter = signal->counter;
+      a.epoch = signal->epoch;
+    }
     void (*kern)(PackArgs) = pack_kernel<4, false>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, true> : pack_kernel<2, false>;
@@ -405,6 +439,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0, stream, a);
     }
     DORA_HIP(hipGetLastError());
+    if (a.flag && signalled) *signalled = true;
     i += m;
     ++launch;
   }

@@ -40,9 +40,6 @@
 
 namespace dora {
 
-int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
-                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
-
 namespace {
 
 constexpr size_t kMaxCacheSize = 20;          // mod.rs:365
@@ -163,6 +160,7 @@ struct NodeCore {
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
+  uint32_t* fill_counters = nullptr;  // device: workgroups done per fill flag (kernel signal)
   std::vector<uint32_t> free_flags;
   uint64_t epoch = 0;
 
@@ -237,6 +235,7 @@ struct NodeCore {
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& kv : recv_pool) (void)hipFree(kv.second);
+    if (fill_counters) (void)hipFree(fill_counters);
     if (region_dev) (void)hipHostUnregister(region->base());
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -560,18 +559,22 @@ void finish_input(dora_node* n, dora_event* ev) {
 // Enqueue one copy of `len` bytes from a slot on `src_device` (IPC-mapped) into local HBM on
 // the node stream: the pack kernel reading the peer's HBM over xGMI (default), or the copy
 // engines (DORA_GPU_PEER_COPY=sdma).
+int ensure_peer_access(NodeCore* c, int src_device) {
+  if (src_device == c->device) return DORA_OK;
+  std::lock_guard<std::mutex> g(c->ipc_mu);
+  if (c->peer_enabled.count(src_device)) return DORA_OK;
+  hipError_t e = hipDeviceEnablePeerAccess(src_device, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+    return fail(DORA_ERR_HIP, "enable peer access %d -> %d: %s", c->device, src_device,
+                hipGetErrorString(e));
+  (void)hipGetLastError();
+  c->peer_enabled.insert(src_device);
+  return DORA_OK;
+}
+
 int enqueue_peer_copy(NodeCore* c, void* dst, const void* src, int src_device, uint64_t len) {
-  if (src_device != c->device) {
-    std::lock_guard<std::mutex> g(c->ipc_mu);
-    if (!c->peer_enabled.count(src_device)) {
-      hipError_t e = hipDeviceEnablePeerAccess(src_device, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-        return fail(DORA_ERR_HIP, "enable peer access %d -> %d: %s", c->device, src_device,
-                    hipGetErrorString(e));
-      (void)hipGetLastError();
-      c->peer_enabled.insert(src_device);
-    }
-  }
+  int rc = ensure_peer_access(c, src_device);
+  if (rc != DORA_OK) return rc;
   if (peer_copy_mode() == PEER_SDMA) {
     hipError_t e = hipMemcpyPeerAsync(dst, c->device, src, src_device, len, c->stream);
     if (e != hipSuccess) return fail(DORA_ERR_HIP, "hipMemcpyPeerAsync: %s", hipGetErrorString(e));
@@ -806,6 +809,41 @@ hipError_t order_fill(dora_node* n, dora_sample* s) {
   return hipStreamSynchronize(st);
 }
 
+// The pack kernel signals the fill flag itself (DORA_GPU_KERNEL_SIGNAL=0: a separate stream
+// write-value packet after the kernel, which ROCm runs as a ~4 us blit kernel).
+bool kernel_signal() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_KERNEL_SIGNAL");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// Launch the fill of sample `s` (segments into its slot) and order its completion signal.
+int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
+                ArrowDeviceType dev, hipEvent_t t_start, hipEvent_t t_stop) {
+  FillSignal sig{};
+  const FillSignal* sp = nullptr;
+  if (s->slot->flag >= 0 && n->core->fill_counters && kernel_signal()) {
+    sig.flag = n->core->flag_dev(s->slot->flag);
+    sig.epoch = ++n->core->epoch;
+    sig.counter = n->core->fill_counters + s->slot->flag;
+    sp = &sig;
+  }
+  bool signalled = false;
+  int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), n->core->stream,
+                       t_start, t_stop, sp, &signalled);
+  if (rc != DORA_OK) return rc;
+  if (signalled) {
+    s->epoch = sig.epoch;
+    s->fill = FILL_FLAG;
+    return DORA_OK;
+  }
+  hipError_t e = order_fill(n, s);
+  if (e != hipSuccess) return fail(DORA_ERR_HIP, "fill signal: %s", hipGetErrorString(e));
+  return DORA_OK;
+}
+
 // Re-send a received input on an output with its type info (a relay stage): one copy into a
 // fresh slot of this node — for a cross-GPU input straight from the peer's slot over xGMI, so
 // a pipeline hop moves the payload once.
@@ -825,19 +863,23 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
     std::memcpy(s->vec.data(), in->ptr, len);
   } else if (len) {
     Segment seg{in->ptr, 0, len};
-    if (in->remote_device >= 0) {
+    if (in->remote_device >= 0 && peer_copy_mode() == PEER_SDMA) {
       rc = enqueue_peer_copy(n->core.get(), s->slot->ptr, in->ptr, in->remote_device, len);
-      if (rc == DORA_OK) {
-        n->core->peer_copies.fetch_add(1, std::memory_order_relaxed);
-        n->core->peer_bytes.fetch_add(len, std::memory_order_relaxed);
-      }
+      hipError_t e = rc == DORA_OK ? order_fill(n, s) : hipSuccess;
+      if (rc == DORA_OK && e != hipSuccess)
+        rc = fail(DORA_ERR_HIP, "forward: %s", hipGetErrorString(e));
     } else {
-      rc = launch_pack(&seg, 1, device_src ? ARROW_DEVICE_ROCM : ARROW_DEVICE_CPU,
-                       static_cast<uint8_t*>(s->slot->ptr), n->core->stream, nullptr, nullptr);
+      // the pack kernel, reading the peer's HBM over xGMI for a cross-GPU input
+      rc = in->remote_device >= 0 ? ensure_peer_access(n->core.get(), in->remote_device)
+                                  : DORA_OK;
+      if (rc == DORA_OK)
+        rc = fill_sample(n, s, &seg, 1, device_src ? ARROW_DEVICE_ROCM : ARROW_DEVICE_CPU,
+                         nullptr, nullptr);
     }
-    hipError_t e = rc == DORA_OK ? order_fill(n, s) : hipSuccess;
-    if (rc == DORA_OK && e != hipSuccess)
-      rc = fail(DORA_ERR_HIP, "forward: %s", hipGetErrorString(e));
+    if (rc == DORA_OK && in->remote_device >= 0) {
+      n->core->peer_copies.fetch_add(1, std::memory_order_relaxed);
+      n->core->peer_bytes.fetch_add(len, std::memory_order_relaxed);
+    }
     if (rc != DORA_OK) {
       add_to_cache(n, s->slot);
       delete s;
@@ -865,29 +907,20 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     }
     for (const Segment& g : plan->segs) std::memcpy(s->vec.data() + g.dst_off, g.src, g.len);
   } else if (plan->size) {
-    hipStream_t st = n->core->stream;
     // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
     // every `timing_sample()`-th pack is stamped (DORA_GPU_TIMING_SAMPLE, default 8).
     const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU &&
                        (n->timing_seq++ % timing_sample()) == 0;
     TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
-    rc = launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
-                     static_cast<uint8_t*>(s->slot->ptr), st, tp ? tp->start : nullptr,
-                     tp ? tp->stop : nullptr);
+    rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
+                     tp ? tp->start : nullptr, tp ? tp->stop : nullptr);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
       delete s;
       return rc;
     }
-    t2 = mono_ns();
-    hipError_t e = order_fill(n, s);
-    if (e != hipSuccess) {
-      add_to_cache(n, s->slot);
-      delete s;
-      return fail(DORA_ERR_HIP, "pack: %s", hipGetErrorString(e));
-    }
-    t3 = mono_ns();
+    t2 = t3 = mono_ns();
   }
   std::vector<uint8_t> ti;
   serialize_type_info(plan->root, ti);
@@ -949,6 +982,13 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
           hipHostGetDevicePointer(&dev, core->region->base(), 0) == hipSuccess) {
         core->region_dev = static_cast<uint8_t*>(dev);
         for (uint32_t k = dora::kFillFlags; k-- > 0;) core->free_flags.push_back(k);
+        if (hipMalloc(&core->fill_counters, dora::kFillFlags * sizeof(uint32_t)) != hipSuccess ||
+            hipMemset(core->fill_counters, 0, dora::kFillFlags * sizeof(uint32_t)) !=
+                hipSuccess) {
+          (void)hipGetLastError();  // the stream write-value packet signals instead
+          if (core->fill_counters) (void)hipFree(core->fill_counters);
+          core->fill_counters = nullptr;
+        }
       } else {
         (void)hipGetLastError();  // fall back to interprocess events
       }

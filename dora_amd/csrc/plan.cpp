@@ -20,9 +20,6 @@
 
 namespace dora {
 
-int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
-                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
-
 namespace {
 
 bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }

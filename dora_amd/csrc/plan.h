@@ -6,6 +6,8 @@
 #include <utility>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "dora_gpu.h"
 
 namespace dora {
@@ -53,6 +55,22 @@ struct Segment {
   uint32_t aux = 0;
   uint64_t src_len = 0;
 };
+
+// Fill signal written by the last workgroup of a pack launch (kernels.hip): a system-scope
+// store of `epoch` into `flag` (device view of a host-registered fill flag) once every
+// workgroup's stores have been released; `counter` is a zeroed device word per flag.
+struct FillSignal {
+  uint64_t* flag;
+  uint64_t epoch;
+  uint32_t* counter;
+};
+
+// Launch the pack of `segs` into `dst` on `stream` (kernels.hip).  With `signal`, the last
+// launch writes the fill flag itself when it can (`*signalled` says whether it did; compacting
+// transforms and host sources leave it to the caller).
+int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
+                hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
+                const FillSignal* signal = nullptr, bool* signalled = nullptr);
 
 void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& out);
 // DataType as a schema tree: str format, str name, i64 flags, u8 has_meta [str meta],
