@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -38,6 +39,7 @@ struct PackArgs {
   uint64_t* flag;        // fill flag to signal at the end (null: none)
   uint32_t* counter;     // workgroups done (reset by the last one)
   uint64_t epoch;
+  uint32_t n_xcd;        // XCDs the grid is dealt over round-robin (kernel signal)
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
   uint32_t chunk_end[kMaxSegs];
@@ -168,21 +170,38 @@ __device__ __forceinline__ void pack_chunk(const PackArgs& args) {
 }
 
 // The sample is complete when every workgroup's stores are visible at the device coherence
-// point: each wave releases at agent scope (its stores done, its XCD's L2 written back), the
-// workgroup counts itself in, and the last one stores the send epoch into the host fill flag
-// with a system-scope release.  This replaces a separate stream write-value packet (a ~4 us
-// blit kernel plus a kernel boundary per message on ROCm 7).
+// point.  MI355X has one L2 per XCD, written back at kernel end; an L2 write-back per workgroup
+// costs ~0.1 us per XCD serially (tried: 560 us per 40 MB pack), so the release is per XCD:
+// workgroups are dispatched round-robin over the XCDs (checked once per device by
+// `xcd_round_robin`), each counts itself in on its XCD after its stores reached that L2, the
+// last one there writes the L2 back (agent-scope release), and the last XCD stores the send
+// epoch into the host fill flag with a system-scope release.  Replaces a separate stream
+// write-value packet (a ~4 us blit kernel plus a kernel boundary per message on ROCm 7).
+// counter[0]: XCDs done; counter[1 + x]: workgroups done on XCD x.
 __device__ __forceinline__ void signal_fill(const PackArgs& a) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are in the L2
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t done =
-        __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == gridDim.x - 1) {
-      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (threadIdx.x != 0) return;
+  const uint32_t nx = a.n_xcd;
+  const uint32_t x = blockIdx.x % nx;
+  const uint32_t on_x = (gridDim.x - x + nx - 1) / nx;
+  uint32_t* cx = a.counter + 1 + x;
+  if (__hip_atomic_fetch_add(cx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != on_x - 1)
+    return;
+  __hip_atomic_store(cx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t parts = gridDim.x < nx ? gridDim.x : nx;
+  // acq_rel at agent scope: this XCD's L2 is written back before the count is visible
+  if (__hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) !=
+      parts - 1)
+    return;
+  __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void xcc_probe_kernel(uint32_t* out) {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  if (threadIdx.x == 0) out[blockIdx.x] = x & 0xF;
 }
 
 template <int U, bool NT>
@@ -368,6 +387,37 @@ unsigned grid_for(uint64_t items) {
 
 }  // namespace
 
+// Number of XCDs the current device deals workgroups over round-robin (workgroup i on XCD
+// i mod n), checked once per device with a probe grid reading the XCC_ID register; 0 when the
+// dispatch does not follow that rule (then fills are signalled by a stream packet instead).
+int xcd_round_robin() {
+  static std::mutex mu;
+  static std::vector<int> known;  // per device: -1 unknown
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (known.size() <= static_cast<size_t>(dev)) known.resize(dev + 1, -1);
+  if (known[dev] >= 0) return known[dev];
+  known[dev] = 0;
+  constexpr uint32_t kProbe = 4096;
+  uint32_t* d = nullptr;
+  std::vector<uint32_t> h(kProbe);
+  if (hipMalloc(&d, kProbe * sizeof(uint32_t)) != hipSuccess) return 0;
+  hipLaunchKernelGGL(xcc_probe_kernel, dim3(kProbe), dim3(64), 0, nullptr, d);
+  const bool ok = hipGetLastError() == hipSuccess &&
+                  hipMemcpy(h.data(), d, kProbe * sizeof(uint32_t), hipMemcpyDeviceToHost) ==
+                      hipSuccess;
+  (void)hipFree(d);
+  if (!ok) return 0;
+  uint32_t nx = 0;
+  for (uint32_t v : h) nx = std::max(nx, v + 1);
+  if (nx == 0 || nx > kMaxXcd) return 0;
+  for (uint32_t i = 0; i < kProbe; ++i)
+    if (h[i] != i % nx) return 0;
+  known[dev] = static_cast<int>(nx);
+  return known[dev];
+}
+
 // Launch the pack of `n` segments into `dst` (device).  Copy segments with device sources go
 // to pack_kernel in batches of kMaxSegs, transform segments (compacting plans) to
 // transform_kernel; host sources are DMA'd with hipMemcpyAsync.  With timing events the
@@ -377,6 +427,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
                 const FillSignal* signal, bool* signalled) {
   if (signalled) *signalled = false;
+  const int n_xcd = signal ? xcd_round_robin() : 0;
   bool any_x = false;
   for (size_t i = 0; i < n_in; ++i) any_x |= segs_in[i].op != SEG_COPY;
   if (dev == ARROW_DEVICE_CPU) {
@@ -423,10 +474,11 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     }
     a.nseg = static_cast<uint32_t>(m);
     const bool first = launch == 0, last = launch + 1 == n_launch;
-    if (last && signal) {
+    if (last && signal && n_xcd > 0) {
       a.flag = signal->flag;
       a.counter = signal->counter;
       a.epoch = signal->epoch;
+      a.n_xcd = static_cast<uint32_t>(n_xcd);
     }
     void (*kern)(PackArgs) = pack_kernel<4, false>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;

@@ -827,7 +827,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   if (s->slot->flag >= 0 && n->core->fill_counters && kernel_signal()) {
     sig.flag = n->core->flag_dev(s->slot->flag);
     sig.epoch = ++n->core->epoch;
-    sig.counter = n->core->fill_counters + s->slot->flag;
+    sig.counter = n->core->fill_counters + size_t(s->slot->flag) * kFillCounterWords;
     sp = &sig;
   }
   bool signalled = false;
@@ -982,9 +982,10 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
           hipHostGetDevicePointer(&dev, core->region->base(), 0) == hipSuccess) {
         core->region_dev = static_cast<uint8_t*>(dev);
         for (uint32_t k = dora::kFillFlags; k-- > 0;) core->free_flags.push_back(k);
-        if (hipMalloc(&core->fill_counters, dora::kFillFlags * sizeof(uint32_t)) != hipSuccess ||
-            hipMemset(core->fill_counters, 0, dora::kFillFlags * sizeof(uint32_t)) !=
-                hipSuccess) {
+        const size_t cb = size_t(dora::kFillFlags) * dora::kFillCounterWords * sizeof(uint32_t);
+        if (dora::xcd_round_robin() == 0 || hipMalloc(&core->fill_counters, cb) != hipSuccess ||
+            hipMemset(core->fill_counters, 0, cb) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
           (void)hipGetLastError();  // the stream write-value packet signals instead
           if (core->fill_counters) (void)hipFree(core->fill_counters);
           core->fill_counters = nullptr;

@@ -62,8 +62,11 @@ struct Segment {
 struct FillSignal {
   uint64_t* flag;
   uint64_t epoch;
-  uint32_t* counter;
+  uint32_t* counter;  // kFillCounterWords zeroed device words
 };
+constexpr uint32_t kMaxXcd = 15;
+constexpr uint32_t kFillCounterWords = 1 + kMaxXcd;
+int xcd_round_robin();
 
 // Launch the pack of `segs` into `dst` on `stream` (kernels.hip).  With `signal`, the last
 // launch writes the fill flag itself when it can (`*signalled` says whether it did; compacting
