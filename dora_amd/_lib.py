@@ -70,6 +70,7 @@ _SIGS = {
     "dora_gpu_plan_type_info": (c_int, [c_void_p, POINTER(c_uint8), c_size_t,
                                         POINTER(c_size_t)]),
     "dora_gpu_pack": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dora_gpu_pack_signal_tune": (c_int, [ctypes.c_uint32, c_int]),
     "dora_gpu_pack_tune": (c_int, [c_int, c_int, ctypes.c_uint32]),
     "dora_gpu_array_upload": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema),
                                       POINTER(ArrowArray)]),

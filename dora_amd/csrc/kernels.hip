@@ -40,6 +40,7 @@ struct PackArgs {
   uint32_t* counter;     // workgroups done (reset by the last one)
   uint64_t epoch;
   uint32_t n_xcd;        // XCDs the grid is dealt over round-robin (kernel signal)
+  uint32_t n_chunks;     // chunks of this launch (>= grid size)
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
   uint32_t chunk_end[kMaxSegs];
@@ -116,8 +117,7 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
 }
 
 template <int U, bool NT>
-__device__ __forceinline__ void pack_chunk(const PackArgs& args) {
-  const uint32_t chunk = blockIdx.x;
+__device__ __forceinline__ void pack_chunk(const PackArgs& args, uint32_t chunk) {
   uint32_t s = 0;
   while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
   const PackSeg sg = args.seg[s];
@@ -206,7 +206,9 @@ __global__ void xcc_probe_kernel(uint32_t* out) {
 
 template <int U, bool NT>
 __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
-  pack_chunk<U, NT>(args);
+  // grid = chunks (one chunk per workgroup), or fewer workgroups striding over the chunks when
+  // the launch signals its fill (fewer workgroups to count in)
+  for (uint32_t c = blockIdx.x; c < args.n_chunks; c += gridDim.x) pack_chunk<U, NT>(args, c);
   if (args.flag) signal_fill(args);
 }
 
@@ -220,6 +222,8 @@ struct Variant {
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
+std::atomic<uint32_t> g_signal_wgs{128};  // workgroups per XCD of a signalling launch (0: all)
+std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
 // 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
@@ -474,21 +478,25 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     }
     a.nseg = static_cast<uint32_t>(m);
     const bool first = launch == 0, last = launch + 1 == n_launch;
+    a.n_chunks = static_cast<uint32_t>(chunks);
+    uint64_t grid = chunks;
     if (last && signal && n_xcd > 0) {
       a.flag = signal->flag;
       a.counter = signal->counter;
       a.epoch = signal->epoch;
       a.n_xcd = static_cast<uint32_t>(n_xcd);
+      const uint64_t cap = uint64_t(n_xcd) * g_signal_wgs.load(std::memory_order_relaxed);
+      if (cap && grid > cap) grid = cap;
     }
     void (*kern)(PackArgs) = pack_kernel<4, false>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, true> : pack_kernel<2, false>;
     else if (var.nt) kern = pack_kernel<4, true>;
     if (ev_start || ev_stop) {
-      hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0, stream,
+      hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream,
                             first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
     } else {
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(chunks)), dim3(kThreads), 0, stream, a);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, a);
     }
     DORA_HIP(hipGetLastError());
     if (a.flag && signalled) *signalled = true;
@@ -558,9 +566,30 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                       static_cast<unsigned long long>(plan->size));
   if (plan->segs.empty()) return DORA_OK;
   if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
+  if (dora::g_bench_signal.load()) {
+    // microbenchmark of signalling launches: a scratch flag + counters in device memory
+    static uint8_t* scratch = nullptr;
+    static uint64_t epoch = 0;
+    if (!scratch) {
+      DORA_HIP(hipMalloc(&scratch, 8 + dora::kFillCounterWords * 4));
+      DORA_HIP(hipMemset(scratch, 0, 8 + dora::kFillCounterWords * 4));
+      DORA_HIP(hipDeviceSynchronize());
+    }
+    dora::FillSignal sig{reinterpret_cast<uint64_t*>(scratch), ++epoch,
+                         reinterpret_cast<uint32_t*>(scratch + 8)};
+    return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
+                             static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream),
+                             nullptr, nullptr, &sig, nullptr);
+  }
   return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                            static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream), nullptr,
                            nullptr);
+}
+
+int dora_gpu_pack_signal_tune(uint32_t wgs_per_xcd, int bench_signal) {
+  dora::g_signal_wgs.store(wgs_per_xcd);
+  dora::g_bench_signal.store(bench_signal != 0);
+  return DORA_OK;
 }
 
 int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--sizes", default="4096000,16777216,40960000")
     ap.add_argument("--misalign", type=int, default=0)
     ap.add_argument("--sweep", action="store_true", help="sweep unroll x nt x chunk")
+    ap.add_argument("--signal-sweep", action="store_true",
+                    help="packs that signal their fill from the kernel, by workgroups per XCD")
     ap.add_argument("--c3", action="store_true",
                     help="C3 shape: 1M-point List<Struct<x,y,z,intensity>> clouds (f32 buffers "
                          "at 4 mod 16) instead of byte buffers; memcpy = one D2D of the sample")
@@ -39,6 +41,9 @@ def main():
     if args.sweep:
         variants = [("memcpy", 0, 0, 0)] + [("pack", u, nt, ch) for u, nt, ch in itertools.product(
             [2, 4, 8], [1], [0, 4096, 8192, 16384, 20480, 32768])]
+    elif args.signal_sweep:
+        variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)] + [
+            ("sig", w, -1, 0) for w in [0, 32, 64, 128, 192, 256, 512]]
     else:
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -65,9 +70,10 @@ def main():
                 kind, u, nt, ch = v
                 if kind == "pack":
                     call("dora_gpu_pack_tune", u, nt, ch)
+                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 128, int(kind == "sig"))
 
                 def launch(k):
-                    if kind == "pack":
+                    if kind in ("pack", "sig"):
                         plans[k].pack(dsts[k].ptr, size, s)
                     else:
                         call("dora_gpu_memcpy_async", dsts[k].ptr, srcs[k].ptr + args.misalign,
@@ -81,6 +87,7 @@ def main():
                 e1.sync()
                 res[v].append(e0.elapsed_ms(e1) / args.iters)
         call("dora_gpu_pack_tune", 0, -1, 0)
+        call("dora_gpu_pack_signal_tune", 128, 0)
         for v in variants:
             ms = statistics.median(res[v])
             gbs = 2 * size / (ms * 1e-3) / 1e9
