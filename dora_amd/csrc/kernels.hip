@@ -28,6 +28,9 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxSegs = 32;
 
+constexpr uint32_t kSigBench = 1, kSigNoXcdRelease = 2, kSigNoSysRelease = 4, kSigWtDevice = 8,
+                   kSigWtSystem = 16;
+
 struct PackSeg {
   const uint8_t* src;
   uint64_t dst_off;
@@ -40,6 +43,7 @@ struct PackArgs {
   uint32_t* counter;     // workgroups done (reset by the last one)
   uint64_t epoch;
   uint32_t n_xcd;        // XCDs the grid is dealt over round-robin (kernel signal)
+  uint32_t sig_flags;    // kSig* (experiments)
   uint32_t n_chunks;     // chunks of this launch (>= grid size)
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
@@ -49,14 +53,21 @@ struct PackArgs {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool NT>
+// Memory policy NT: 0 plain, 1 non-temporal loads and stores, 2/3 non-temporal loads and stores
+// written through to device (sc1) / system (sc0 sc1) scope — no L2 write-back needed before a
+// fill signal.
+template <int NT>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
   return *reinterpret_cast<const u32x4*>(p);
 }
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT) {
+  if constexpr (NT == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (NT == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (NT == 1) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
   } else {
     *reinterpret_cast<u32x4*>(p) = v;
@@ -77,7 +88,7 @@ __device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
 
 // Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned.  U loads of
 // 16 B per lane in flight before the stores.
-template <int U, bool NT>
+template <int U, int NT>
 __device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 v[U];
@@ -94,7 +105,7 @@ __device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uin
   }
 }
 
-template <int U, bool NT, int Q>
+template <int U, int NT, int Q>
 __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
                                              uint64_t nunits) {
   // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
@@ -116,7 +127,7 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
   }
 }
 
-template <int U, bool NT>
+template <int U, int NT>
 __device__ __forceinline__ void pack_chunk(const PackArgs& args, uint32_t chunk) {
   uint32_t s = 0;
   while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
@@ -191,11 +202,17 @@ __device__ __forceinline__ void signal_fill(const PackArgs& a) {
   __hip_atomic_store(cx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t parts = gridDim.x < nx ? gridDim.x : nx;
   // acq_rel at agent scope: this XCD's L2 is written back before the count is visible
-  if (__hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) !=
-      parts - 1)
-    return;
+  uint32_t prev;
+  if (a.sig_flags & kSigNoXcdRelease)
+    prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != parts - 1) return;
   __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.sig_flags & kSigNoSysRelease)
+    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void xcc_probe_kernel(uint32_t* out) {
@@ -204,7 +221,7 @@ __global__ void xcc_probe_kernel(uint32_t* out) {
   if (threadIdx.x == 0) out[blockIdx.x] = x & 0xF;
 }
 
-template <int U, bool NT>
+template <int U, int NT>
 __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   // grid = chunks (one chunk per workgroup), or fewer workgroups striding over the chunks when
   // the launch signals its fill (fewer workgroups to count in)
@@ -223,7 +240,7 @@ std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
 std::atomic<uint32_t> g_signal_wgs{128};  // workgroups per XCD of a signalling launch (0: all)
-std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
+std::atomic<uint32_t> g_sig_flags{0};     // kSig*: bench scratch signal, release experiments
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
 // 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
@@ -485,13 +502,19 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
       a.counter = signal->counter;
       a.epoch = signal->epoch;
       a.n_xcd = static_cast<uint32_t>(n_xcd);
+      a.sig_flags = g_sig_flags.load(std::memory_order_relaxed);
       const uint64_t cap = uint64_t(n_xcd) * g_signal_wgs.load(std::memory_order_relaxed);
       if (cap && grid > cap) grid = cap;
     }
-    void (*kern)(PackArgs) = pack_kernel<4, false>;
-    if (var.unroll == 8) kern = var.nt ? pack_kernel<8, true> : pack_kernel<8, false>;
-    else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, true> : pack_kernel<2, false>;
-    else if (var.nt) kern = pack_kernel<4, true>;
+    void (*kern)(PackArgs) = pack_kernel<4, 0>;
+    if (var.unroll == 8) kern = var.nt ? pack_kernel<8, 1> : pack_kernel<8, 0>;
+    else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, 1> : pack_kernel<2, 0>;
+    else if (var.nt) kern = pack_kernel<4, 1>;
+    if (a.flag && (a.sig_flags & (kSigWtDevice | kSigWtSystem))) {
+      const bool sys = a.sig_flags & kSigWtSystem;
+      if (var.unroll == 8) kern = sys ? pack_kernel<8, 3> : pack_kernel<8, 2>;
+      else kern = sys ? pack_kernel<4, 3> : pack_kernel<4, 2>;
+    }
     if (ev_start || ev_stop) {
       hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream,
                             first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
@@ -566,7 +589,7 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                       static_cast<unsigned long long>(plan->size));
   if (plan->segs.empty()) return DORA_OK;
   if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
-  if (dora::g_bench_signal.load()) {
+  if (dora::g_sig_flags.load() & dora::kSigBench) {
     // microbenchmark of signalling launches: a scratch flag + counters in device memory
     static uint8_t* scratch = nullptr;
     static uint64_t epoch = 0;
@@ -586,9 +609,9 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                            nullptr);
 }
 
-int dora_gpu_pack_signal_tune(uint32_t wgs_per_xcd, int bench_signal) {
+int dora_gpu_pack_signal_tune(uint32_t wgs_per_xcd, int flags) {
   dora::g_signal_wgs.store(wgs_per_xcd);
-  dora::g_bench_signal.store(bench_signal != 0);
+  dora::g_sig_flags.store(static_cast<uint32_t>(flags));
   return DORA_OK;
 }
 

@@ -42,8 +42,10 @@ def main():
         variants = [("memcpy", 0, 0, 0)] + [("pack", u, nt, ch) for u, nt, ch in itertools.product(
             [2, 4, 8], [1], [0, 4096, 8192, 16384, 20480, 32768])]
     elif args.signal_sweep:
+        # (kind, workgroups per XCD, signal flags): 2/4 drop the per-XCD / final release
+        # (timing experiments only), 8/16 write the sample through to device / system scope
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)] + [
-            ("sig", w, -1, 0) for w in [0, 32, 64, 128, 192, 256, 512]]
+            ("sig", w, f, 0) for w in [32, 64, 128] for f in [0, 2, 4, 6, 8 | 2, 16 | 2]]
     else:
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -70,7 +72,8 @@ def main():
                 kind, u, nt, ch = v
                 if kind == "pack":
                     call("dora_gpu_pack_tune", u, nt, ch)
-                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 128, int(kind == "sig"))
+                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 128,
+                     (1 | nt) if kind == "sig" else 0)
 
                 def launch(k):
                     if kind in ("pack", "sig"):
