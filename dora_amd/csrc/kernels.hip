@@ -28,8 +28,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxSegs = 32;
 
-constexpr uint32_t kSigBench = 1, kSigNoXcdRelease = 2, kSigNoSysRelease = 4, kSigWtDevice = 8,
-                   kSigWtSystem = 16;
 
 struct PackSeg {
   const uint8_t* src;
@@ -40,10 +38,8 @@ struct PackSeg {
 struct PackArgs {
   uint8_t* dst;
   uint64_t* flag;        // fill flag to signal at the end (null: none)
-  uint32_t* counter;     // workgroups done (reset by the last one)
+  uint32_t* done;        // per workgroup: epoch (low 32 bits) once its stores are complete
   uint64_t epoch;
-  uint32_t n_xcd;        // XCDs the grid is dealt over round-robin (kernel signal)
-  uint32_t sig_flags;    // kSig* (experiments)
   uint32_t n_chunks;     // chunks of this launch (>= grid size)
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
@@ -71,6 +67,16 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
   } else {
     *reinterpret_cast<u32x4*>(p) = v;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
+  if constexpr (NT >= 2) {
+    const uint32_t w = v;
+    asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+  } else {
+    *p = v;
   }
 }
 
@@ -148,13 +154,13 @@ __device__ __forceinline__ void pack_chunk(const PackArgs& args, uint32_t chunk)
     // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1), byte by byte (< 16 each).
     const uint64_t hend = a0 < d1 ? a0 : d1;
     const uint64_t nhead = hend - d0;
-    if (threadIdx.x < nhead) dst[d0 + threadIdx.x] = src[threadIdx.x];
+    if (threadIdx.x < nhead) st1<NT>(dst + d0 + threadIdx.x, src[threadIdx.x]);
     if (a0 < d1) {
       const uint64_t t0 = a1 > a0 ? a1 : a0;
       const uint64_t ntail = d1 - t0;
       if (threadIdx.x >= 64 && threadIdx.x - 64 < ntail) {
         const uint64_t d = t0 + (threadIdx.x - 64);
-        dst[d] = src[d - d0];
+        st1<NT>(dst + d, src[d - d0]);
       }
     }
   }
@@ -180,45 +186,38 @@ __device__ __forceinline__ void pack_chunk(const PackArgs& args, uint32_t chunk)
   }
 }
 
-// The sample is complete when every workgroup's stores are visible at the device coherence
-// point.  MI355X has one L2 per XCD, written back at kernel end; an L2 write-back per workgroup
-// costs ~0.1 us per XCD serially (tried: 560 us per 40 MB pack), so the release is per XCD:
-// workgroups are dispatched round-robin over the XCDs (checked once per device by
-// `xcd_round_robin`), each counts itself in on its XCD after its stores reached that L2, the
-// last one there writes the L2 back (agent-scope release), and the last XCD stores the send
-// epoch into the host fill flag with a system-scope release.  Replaces a separate stream
-// write-value packet (a ~4 us blit kernel plus a kernel boundary per message on ROCm 7).
-// counter[0]: XCDs done; counter[1 + x]: workgroups done on XCD x.
+// In-kernel fill signal.  A signalling launch writes the sample through to device scope (sc1:
+// no dirty lines left in the per-XCD L2s, so no cache write-back is needed), every workgroup
+// waits for its stores to complete and publishes the epoch in its own done word, and
+// workgroup 0 — dispatched first — polls all done words and then stores the epoch into the
+// host fill flag with a system-scope release.  No same-address atomics (those serialise at
+// ~0.1 us each across XCDs) and no L2 write-back per workgroup (~0.1 us each, serial per
+// XCD): this replaces the stream write-value packet, a ~4 us blit kernel plus a kernel
+// boundary per message on ROCm 7.
+template <int U, int NT>
 __device__ __forceinline__ void signal_fill(const PackArgs& a) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are in the L2
+  const uint32_t e = static_cast<uint32_t>(a.epoch);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores are complete
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  const uint32_t nx = a.n_xcd;
-  const uint32_t x = blockIdx.x % nx;
-  const uint32_t on_x = (gridDim.x - x + nx - 1) / nx;
-  uint32_t* cx = a.counter + 1 + x;
-  if (__hip_atomic_fetch_add(cx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != on_x - 1)
-    return;
-  __hip_atomic_store(cx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t parts = gridDim.x < nx ? gridDim.x : nx;
-  // acq_rel at agent scope: this XCD's L2 is written back before the count is visible
-  uint32_t prev;
-  if (a.sig_flags & kSigNoXcdRelease)
-    prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    prev = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev != parts - 1) return;
-  __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (a.sig_flags & kSigNoSysRelease)
-    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else
+  if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, e, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x != 0) return;
+  // bounded wait (~seconds): a lost workgroup must not hang the device; the flag then stays
+  // unset and the receiver reports the fill as failed
+  bool ok = true;
+  for (uint32_t i = threadIdx.x; i < gridDim.x && ok; i += kThreads) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e) {
+      if (++spins > (1u << 22)) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  ok = __syncthreads_and(ok);
+  if (threadIdx.x == 0 && ok)
     __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ void xcc_probe_kernel(uint32_t* out) {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  if (threadIdx.x == 0) out[blockIdx.x] = x & 0xF;
 }
 
 template <int U, int NT>
@@ -226,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   // grid = chunks (one chunk per workgroup), or fewer workgroups striding over the chunks when
   // the launch signals its fill (fewer workgroups to count in)
   for (uint32_t c = blockIdx.x; c < args.n_chunks; c += gridDim.x) pack_chunk<U, NT>(args, c);
-  if (args.flag) signal_fill(args);
+  if constexpr (NT >= 2) signal_fill<U, NT>(args);
 }
 
 // Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
@@ -239,8 +238,8 @@ struct Variant {
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
-std::atomic<uint32_t> g_signal_wgs{128};  // workgroups per XCD of a signalling launch (0: all)
-std::atomic<uint32_t> g_sig_flags{0};     // kSig*: bench scratch signal, release experiments
+std::atomic<uint32_t> g_signal_grid{0};  // workgroups of a signalling launch (0: kMaxSignalWgs)
+std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
 // 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
@@ -408,37 +407,6 @@ unsigned grid_for(uint64_t items) {
 
 }  // namespace
 
-// Number of XCDs the current device deals workgroups over round-robin (workgroup i on XCD
-// i mod n), checked once per device with a probe grid reading the XCC_ID register; 0 when the
-// dispatch does not follow that rule (then fills are signalled by a stream packet instead).
-int xcd_round_robin() {
-  static std::mutex mu;
-  static std::vector<int> known;  // per device: -1 unknown
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  std::lock_guard<std::mutex> g(mu);
-  if (known.size() <= static_cast<size_t>(dev)) known.resize(dev + 1, -1);
-  if (known[dev] >= 0) return known[dev];
-  known[dev] = 0;
-  constexpr uint32_t kProbe = 4096;
-  uint32_t* d = nullptr;
-  std::vector<uint32_t> h(kProbe);
-  if (hipMalloc(&d, kProbe * sizeof(uint32_t)) != hipSuccess) return 0;
-  hipLaunchKernelGGL(xcc_probe_kernel, dim3(kProbe), dim3(64), 0, nullptr, d);
-  const bool ok = hipGetLastError() == hipSuccess &&
-                  hipMemcpy(h.data(), d, kProbe * sizeof(uint32_t), hipMemcpyDeviceToHost) ==
-                      hipSuccess;
-  (void)hipFree(d);
-  if (!ok) return 0;
-  uint32_t nx = 0;
-  for (uint32_t v : h) nx = std::max(nx, v + 1);
-  if (nx == 0 || nx > kMaxXcd) return 0;
-  for (uint32_t i = 0; i < kProbe; ++i)
-    if (h[i] != i % nx) return 0;
-  known[dev] = static_cast<int>(nx);
-  return known[dev];
-}
-
 // Launch the pack of `n` segments into `dst` (device).  Copy segments with device sources go
 // to pack_kernel in batches of kMaxSegs, transform segments (compacting plans) to
 // transform_kernel; host sources are DMA'd with hipMemcpyAsync.  With timing events the
@@ -448,7 +416,6 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
                 const FillSignal* signal, bool* signalled) {
   if (signalled) *signalled = false;
-  const int n_xcd = signal ? xcd_round_robin() : 0;
   bool any_x = false;
   for (size_t i = 0; i < n_in; ++i) any_x |= segs_in[i].op != SEG_COPY;
   if (dev == ARROW_DEVICE_CPU) {
@@ -497,23 +464,19 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     const bool first = launch == 0, last = launch + 1 == n_launch;
     a.n_chunks = static_cast<uint32_t>(chunks);
     uint64_t grid = chunks;
-    if (last && signal && n_xcd > 0) {
-      a.flag = signal->flag;
-      a.counter = signal->counter;
-      a.epoch = signal->epoch;
-      a.n_xcd = static_cast<uint32_t>(n_xcd);
-      a.sig_flags = g_sig_flags.load(std::memory_order_relaxed);
-      const uint64_t cap = uint64_t(n_xcd) * g_signal_wgs.load(std::memory_order_relaxed);
-      if (cap && grid > cap) grid = cap;
-    }
     void (*kern)(PackArgs) = pack_kernel<4, 0>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, 1> : pack_kernel<8, 0>;
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, 1> : pack_kernel<2, 0>;
     else if (var.nt) kern = pack_kernel<4, 1>;
-    if (a.flag && (a.sig_flags & (kSigWtDevice | kSigWtSystem))) {
-      const bool sys = a.sig_flags & kSigWtSystem;
-      if (var.unroll == 8) kern = sys ? pack_kernel<8, 3> : pack_kernel<8, 2>;
-      else kern = sys ? pack_kernel<4, 3> : pack_kernel<4, 2>;
+    if (last && signal) {
+      // signalling launch: write-through stores, at most kMaxSignalWgs workgroups
+      a.flag = signal->flag;
+      a.done = signal->done;
+      a.epoch = signal->epoch;
+      const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+      const uint64_t cap = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kMaxSignalWgs;
+      if (grid > cap) grid = cap;
+      kern = var.unroll == 8 ? pack_kernel<8, 2> : pack_kernel<4, 2>;
     }
     if (ev_start || ev_stop) {
       hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream,
@@ -589,13 +552,13 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                       static_cast<unsigned long long>(plan->size));
   if (plan->segs.empty()) return DORA_OK;
   if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
-  if (dora::g_sig_flags.load() & dora::kSigBench) {
+  if (dora::g_bench_signal.load()) {
     // microbenchmark of signalling launches: a scratch flag + counters in device memory
     static uint8_t* scratch = nullptr;
     static uint64_t epoch = 0;
     if (!scratch) {
-      DORA_HIP(hipMalloc(&scratch, 8 + dora::kFillCounterWords * 4));
-      DORA_HIP(hipMemset(scratch, 0, 8 + dora::kFillCounterWords * 4));
+      DORA_HIP(hipMalloc(&scratch, 8 + dora::kMaxSignalWgs * 4));
+      DORA_HIP(hipMemset(scratch, 0, 8 + dora::kMaxSignalWgs * 4));
       DORA_HIP(hipDeviceSynchronize());
     }
     dora::FillSignal sig{reinterpret_cast<uint64_t*>(scratch), ++epoch,
@@ -609,9 +572,9 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                            nullptr);
 }
 
-int dora_gpu_pack_signal_tune(uint32_t wgs_per_xcd, int flags) {
-  dora::g_signal_wgs.store(wgs_per_xcd);
-  dora::g_sig_flags.store(static_cast<uint32_t>(flags));
+int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal) {
+  dora::g_signal_grid.store(grid);
+  dora::g_bench_signal.store(bench_signal != 0);
   return DORA_OK;
 }
 

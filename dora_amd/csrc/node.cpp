@@ -160,7 +160,7 @@ struct NodeCore {
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
-  uint32_t* fill_counters = nullptr;  // device: workgroups done per fill flag (kernel signal)
+  uint32_t* fill_done = nullptr;  // device: per fill flag, kMaxSignalWgs workgroup done words
   std::vector<uint32_t> free_flags;
   uint64_t epoch = 0;
 
@@ -235,7 +235,7 @@ struct NodeCore {
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& kv : recv_pool) (void)hipFree(kv.second);
-    if (fill_counters) (void)hipFree(fill_counters);
+    if (fill_done) (void)hipFree(fill_done);
     if (region_dev) (void)hipHostUnregister(region->base());
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -824,10 +824,10 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
                 ArrowDeviceType dev, hipEvent_t t_start, hipEvent_t t_stop) {
   FillSignal sig{};
   const FillSignal* sp = nullptr;
-  if (s->slot->flag >= 0 && n->core->fill_counters && kernel_signal()) {
+  if (s->slot->flag >= 0 && n->core->fill_done && kernel_signal()) {
     sig.flag = n->core->flag_dev(s->slot->flag);
     sig.epoch = ++n->core->epoch;
-    sig.counter = n->core->fill_counters + size_t(s->slot->flag) * kFillCounterWords;
+    sig.done = n->core->fill_done + size_t(s->slot->flag) * kMaxSignalWgs;
     sp = &sig;
   }
   bool signalled = false;
@@ -982,13 +982,13 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
           hipHostGetDevicePointer(&dev, core->region->base(), 0) == hipSuccess) {
         core->region_dev = static_cast<uint8_t*>(dev);
         for (uint32_t k = dora::kFillFlags; k-- > 0;) core->free_flags.push_back(k);
-        const size_t cb = size_t(dora::kFillFlags) * dora::kFillCounterWords * sizeof(uint32_t);
-        if (dora::xcd_round_robin() == 0 || hipMalloc(&core->fill_counters, cb) != hipSuccess ||
-            hipMemset(core->fill_counters, 0, cb) != hipSuccess ||
+        const size_t cb = size_t(dora::kFillFlags) * dora::kMaxSignalWgs * sizeof(uint32_t);
+        if (hipMalloc(&core->fill_done, cb) != hipSuccess ||
+            hipMemset(core->fill_done, 0, cb) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) {
           (void)hipGetLastError();  // the stream write-value packet signals instead
-          if (core->fill_counters) (void)hipFree(core->fill_counters);
-          core->fill_counters = nullptr;
+          if (core->fill_done) (void)hipFree(core->fill_done);
+          core->fill_done = nullptr;
         }
       } else {
         (void)hipGetLastError();  // fall back to interprocess events

@@ -56,17 +56,15 @@ struct Segment {
   uint64_t src_len = 0;
 };
 
-// Fill signal written by the last workgroup of a pack launch (kernels.hip): a system-scope
-// store of `epoch` into `flag` (device view of a host-registered fill flag) once every
-// workgroup's stores have been released; `counter` is a zeroed device word per flag.
+// Fill signal written by a pack launch itself (kernels.hip): once every workgroup's stores are
+// complete, a system-scope store of `epoch` into `flag` (device view of a host-registered fill
+// flag).  `done` = kMaxSignalWgs device words owned by this flag (zeroed once).
 struct FillSignal {
   uint64_t* flag;
   uint64_t epoch;
-  uint32_t* counter;  // kFillCounterWords zeroed device words
+  uint32_t* done;
 };
-constexpr uint32_t kMaxXcd = 15;
-constexpr uint32_t kFillCounterWords = 1 + kMaxXcd;
-int xcd_round_robin();
+constexpr uint32_t kMaxSignalWgs = 4096;
 
 // Launch the pack of `segs` into `dst` on `stream` (kernels.hip).  With `signal`, the last
 // launch writes the fill flag itself when it can (`*signalled` says whether it did; compacting

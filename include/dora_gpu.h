@@ -165,12 +165,10 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
 /* Tuning knob of the pack kernel (process-wide): 16-B loads in flight per lane (0 = default,
  * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1), bytes per workgroup (0 = auto). */
 int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
-/* Tuning of packs that signal their fill from the kernel (node sends): workgroups per XCD of
- * such a launch, which then strides over the chunks (0: one workgroup per chunk), and flags:
- * 1 = dora_gpu_pack signals a scratch flag too (microbenchmarks); 2/4 = skip the per-XCD /
- * final release (experiments only: unsafe); 8/16 = write the sample through to device /
- * system scope. */
-int dora_gpu_pack_signal_tune(uint32_t wgs_per_xcd, int flags);
+/* Tuning of packs that signal their fill from the kernel (node sends): workgroups of such a
+ * launch, which then strides over the chunks (0: up to 4096).  With `bench_signal`,
+ * dora_gpu_pack signals a scratch flag too (microbenchmarks). */
+int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident Arrow arrays                                                               */

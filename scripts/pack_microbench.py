@@ -42,10 +42,9 @@ def main():
         variants = [("memcpy", 0, 0, 0)] + [("pack", u, nt, ch) for u, nt, ch in itertools.product(
             [2, 4, 8], [1], [0, 4096, 8192, 16384, 20480, 32768])]
     elif args.signal_sweep:
-        # (kind, workgroups per XCD, signal flags): 2/4 drop the per-XCD / final release
-        # (timing experiments only), 8/16 write the sample through to device / system scope
+        # (kind, signalling grid): the pack signals a scratch flag from its workgroup 0
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)] + [
-            ("sig", w, f, 0) for w in [32, 64, 128] for f in [0, 2, 4, 6, 8 | 2, 16 | 2]]
+            ("sig", w, 0, 0) for w in [256, 512, 1024, 2048, 4096]]
     else:
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -72,8 +71,7 @@ def main():
                 kind, u, nt, ch = v
                 if kind == "pack":
                     call("dora_gpu_pack_tune", u, nt, ch)
-                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 128,
-                     (1 | nt) if kind == "sig" else 0)
+                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 0, int(kind == "sig"))
 
                 def launch(k):
                     if kind in ("pack", "sig"):
@@ -90,7 +88,7 @@ def main():
                 e1.sync()
                 res[v].append(e0.elapsed_ms(e1) / args.iters)
         call("dora_gpu_pack_tune", 0, -1, 0)
-        call("dora_gpu_pack_signal_tune", 128, 0)
+        call("dora_gpu_pack_signal_tune", 0, 0)
         for v in variants:
             ms = statistics.median(res[v])
             gbs = 2 * size / (ms * 1e-3) / 1e9
