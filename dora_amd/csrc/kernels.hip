@@ -27,6 +27,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxSegs = 32;
+// Workgroups of a signalling pack (r01 sweep, profiles/r01_signal_sweep.jsonl: 1024 beats 512
+// and 2048-4096 at 16-40 MB, flat at 4 MB).
+constexpr uint32_t kSignalGrid = 1024;
 
 
 struct PackSeg {
@@ -216,8 +219,11 @@ __device__ __forceinline__ void signal_fill(const PackArgs& a) {
     }
   }
   ok = __syncthreads_and(ok);
+  // Relaxed: everything this store publishes is already written through (sample stores and done
+  // words are device-scope write-through and complete), and it issues only after every done
+  // word was observed; a release would write back this XCD's whole L2 for nothing.
   if (threadIdx.x == 0 && ok)
-    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int U, int NT>
@@ -238,7 +244,7 @@ struct Variant {
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
-std::atomic<uint32_t> g_signal_grid{0};  // workgroups of a signalling launch (0: kMaxSignalWgs)
+std::atomic<uint32_t> g_signal_grid{0};  // workgroups of a signalling launch (0: kSignalGrid)
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
@@ -474,7 +480,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
       a.done = signal->done;
       a.epoch = signal->epoch;
       const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-      const uint64_t cap = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kMaxSignalWgs;
+      const uint64_t cap = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
       if (grid > cap) grid = cap;
       kern = var.unroll == 8 ? pack_kernel<8, 2> : pack_kernel<4, 2>;
     }

@@ -44,7 +44,8 @@ def main():
     elif args.signal_sweep:
         # (kind, signalling grid): the pack signals a scratch flag from its workgroup 0
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)] + [
-            ("sig", w, 0, 0) for w in [256, 512, 1024, 2048, 4096]]
+            ("sig", w, u, ch) for w in [512, 1024] for u in [0, 4, 8]
+            for ch in [0, 8192, 16384, 32768]]
     else:
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -71,6 +72,8 @@ def main():
                 kind, u, nt, ch = v
                 if kind == "pack":
                     call("dora_gpu_pack_tune", u, nt, ch)
+                elif kind == "sig":  # (grid, unroll, chunk)
+                    call("dora_gpu_pack_tune", nt, -1, ch)
                 call("dora_gpu_pack_signal_tune", u if kind == "sig" else 0, int(kind == "sig"))
 
                 def launch(k):
@@ -89,6 +92,7 @@ def main():
                 res[v].append(e0.elapsed_ms(e1) / args.iters)
         call("dora_gpu_pack_tune", 0, -1, 0)
         call("dora_gpu_pack_signal_tune", 0, 0)
+        call("dora_gpu_pack_tune", 0, -1, 0)
         for v in variants:
             ms = statistics.median(res[v])
             gbs = 2 * size / (ms * 1e-3) / 1e9
