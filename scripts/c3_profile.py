@@ -30,6 +30,8 @@ def main():
 
     timeit("export_schema_us", lambda: release_schema(da.export_schema()))
     timeit("plan_us", lambda: Plan.of(da).close())
+    cloud = point_cloud()
+    timeit("plan_host_array_us", lambda: Plan.of(cloud).close())  # same walk, no device reads
     p = Plan.of(da)
     timeit("type_info_us", lambda: p.type_info())
     buf = device.DeviceBuffer(p.size)
