@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <mutex>
 #include <cstring>
@@ -202,6 +203,11 @@ __device__ __forceinline__ void signal_fill(const PackArgs& a) {
   const uint32_t e = static_cast<uint32_t>(a.epoch);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores are complete
   __syncthreads();
+  if (gridDim.x == 1) {  // nothing to wait for but this workgroup's own stores
+    if (threadIdx.x == 0)
+      __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, e, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x != 0) return;
@@ -520,6 +526,59 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     DORA_HIP(hipGetLastError());
     ++launch;
   }
+  return DORA_OK;
+}
+
+// Launch a pack and wait for it by spinning on a host flag the launch writes itself (a
+// blocking stream synchronise sleeps and wakes tens of microseconds late).  Per thread and
+// device: the pinned flag, its device view and the done words.  Falls back to a stream
+// synchronise when the launch cannot signal (transform segments) or the flag does not come.
+int launch_pack_wait(const Segment* segs, size_t n, uint8_t* dst, hipStream_t stream) {
+  struct WaitCtx {
+    int device = -1;
+    uint64_t* host = nullptr;
+    uint64_t* dev = nullptr;
+    uint32_t* done = nullptr;
+    uint64_t epoch = 0;
+  };
+  thread_local std::vector<WaitCtx> ctxs;
+  int device = 0;
+  DORA_HIP(hipGetDevice(&device));
+  WaitCtx* c = nullptr;
+  for (auto& x : ctxs)
+    if (x.device == device) c = &x;
+  if (!c) {
+    WaitCtx x;
+    x.device = device;
+    void* dv = nullptr;
+    DORA_HIP(hipHostMalloc(reinterpret_cast<void**>(&x.host), 64, hipHostMallocMapped));
+    DORA_HIP(hipHostGetDevicePointer(&dv, x.host, 0));
+    x.dev = static_cast<uint64_t*>(dv);
+    *reinterpret_cast<volatile uint64_t*>(x.host) = 0;
+    DORA_HIP(hipMalloc(&x.done, kMaxSignalWgs * sizeof(uint32_t)));
+    DORA_HIP(hipMemset(x.done, 0, kMaxSignalWgs * sizeof(uint32_t)));
+    DORA_HIP(hipDeviceSynchronize());
+    ctxs.push_back(x);
+    c = &ctxs.back();
+  }
+  FillSignal sig{c->dev, ++c->epoch, c->done};
+  bool signalled = false;
+  int rc = launch_pack(segs, n, ARROW_DEVICE_ROCM, dst, stream, nullptr, nullptr, &sig,
+                       &signalled);
+  if (rc != DORA_OK) return rc;
+  if (signalled) {
+    const volatile uint64_t* f = c->host;
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (*f < sig.epoch) {
+      __builtin_ia32_pause();
+      if (++spins % 4096 == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200))
+        break;  // slow or failed signal: the stream synchronise below decides
+    }
+    if (*f >= sig.epoch) return DORA_OK;
+  }
+  DORA_HIP(hipStreamSynchronize(stream));
   return DORA_OK;
 }
 

@@ -593,10 +593,18 @@ int ensure_local(InputData* in) {
   uint64_t cap = 0;
   void* local = c->recv_pool_get(in->len, &cap);
   if (!local) return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->len);
-  int rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->len);
-  if (rc == DORA_OK) {
-    hipError_t e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "cross-GPU pull: %s", hipGetErrorString(e));
+  int rc;
+  if (peer_copy_mode() == PEER_SDMA) {
+    rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->len);
+    if (rc == DORA_OK) {
+      hipError_t e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "cross-GPU pull: %s", hipGetErrorString(e));
+    }
+  } else {
+    // the pack kernel reads the peer's HBM over xGMI; wait on its own completion flag
+    rc = ensure_peer_access(c, in->remote_device);
+    Segment seg{in->ptr, 0, in->len};
+    if (rc == DORA_OK) rc = launch_pack_wait(&seg, 1, static_cast<uint8_t*>(local), c->stream);
   }
   if (rc != DORA_OK) {
     c->recv_pool_put(local, cap);

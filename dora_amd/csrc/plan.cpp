@@ -225,12 +225,9 @@ const uint8_t* gather_to_host(const std::vector<Segment>& reqs, uint64_t total) 
       throw std::runtime_error("plan: pinned staging buffer");
     c->cap = cap;
   }
-  int rc = launch_pack(reqs.data(), reqs.size(), ARROW_DEVICE_ROCM,
-                       static_cast<uint8_t*>(c->host_dev), c->stream, nullptr, nullptr);
+  int rc = launch_pack_wait(reqs.data(), reqs.size(), static_cast<uint8_t*>(c->host_dev),
+                            c->stream);
   if (rc != DORA_OK) throw std::runtime_error(std::string("plan: gather: ") + dora_gpu_last_error());
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e != hipSuccess)
-    throw std::runtime_error(std::string("plan: gather: ") + hipGetErrorString(e));
   return c->host;
 }
 

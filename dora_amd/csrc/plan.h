@@ -73,6 +73,10 @@ int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
                 const FillSignal* signal = nullptr, bool* signalled = nullptr);
 
+// Pack device segments into `dst` (device or mapped host memory) and return once complete,
+// waiting on the launch's own fill signal instead of a blocking stream synchronise.
+int launch_pack_wait(const Segment* segs, size_t n, uint8_t* dst, hipStream_t stream);
+
 void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& out);
 // DataType as a schema tree: str format, str name, i64 flags, u8 has_meta [str meta],
 // u32 n_children × Schema, u8 has_dict [Schema].  The top level carries no name and only the
