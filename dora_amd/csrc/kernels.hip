@@ -211,20 +211,30 @@ __device__ __forceinline__ void signal_fill(const PackArgs& a) {
   if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, e, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x != 0) return;
-  // bounded wait (~seconds): a lost workgroup must not hang the device; the flag then stays
-  // unset and the receiver reports the fill as failed
-  bool ok = true;
-  for (uint32_t i = threadIdx.x; i < gridDim.x && ok; i += kThreads) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e) {
-      if (++spins > (1u << 22)) {
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
+  // Poll every done word at once per round (up to kMaxSignalWgs / kThreads = 16 independent
+  // loads in flight per lane), so completion is seen one load round trip after the last
+  // workgroup.  Bounded (~seconds): a lost workgroup must not hang the device; the flag then
+  // stays unset and the receiver reports the fill as failed.
+  constexpr int kPer = kMaxSignalWgs / kThreads;
+  bool ok = false;
+  for (uint32_t round = 0; round < (1u << 22); ++round) {
+    uint32_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = threadIdx.x + k * kThreads;
+      v[k] = i < gridDim.x ? __hip_atomic_load(a.done + i, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : e;
     }
+    bool mine = true;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) mine &= v[k] == e;
+    if (__syncthreads_and(mine)) {
+      ok = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  ok = __syncthreads_and(ok);
   // Relaxed: everything this store publishes is already written through (sample stores and done
   // words are device-scope write-through and complete), and it issues only after every done
   // word was observed; a release would write back this XCD's whole L2 for nothing.
