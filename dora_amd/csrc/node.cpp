@@ -76,6 +76,20 @@ size_t max_in_flight() {
   return v;
 }
 
+// Streams the sends of a node spread their fills over (DORA_GPU_FILL_STREAMS, default 3).  A
+// pack ends in a drain tail (its last workgroups, the fill signal) and starts with a ramp; on
+// one stream consecutive fills serialise those, on three hardware queues the next fill streams
+// through them (r01 probe, profiles/r01_stream_probe.jsonl: 40.96 MB 17.1 -> 13.2 us per
+// message, 16 MB 9.8 -> 6.0).  1 = every fill on the node stream.
+size_t fill_stream_count() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DORA_GPU_FILL_STREAMS");
+    long x = e ? std::atol(e) : 3;
+    return static_cast<size_t>(x < 1 ? 1 : x > 8 ? 8 : x);
+  }();
+  return v;
+}
+
 uint64_t timing_sample() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_TIMING_SAMPLE");
@@ -151,6 +165,14 @@ struct NodeCore {
   int idx = -1;
   int device = 0;
   hipStream_t stream = nullptr;
+  // Fill streams (fill_stream_count() > 1): sends rotate over them.  Work already queued on the
+  // node stream is ordered before a fill (node_ev), and fills are ordered before node-stream
+  // work queued after dora_node_stream() hands the stream out (fence_fills).
+  std::vector<hipStream_t> fill_streams;
+  std::vector<hipEvent_t> fill_events;
+  std::vector<uint8_t> fill_dirty;
+  hipEvent_t node_ev = nullptr;
+  size_t fill_next = 0;
   RingWriter req;
   RingReader ev;
   RingReader drops;
@@ -230,9 +252,41 @@ struct NodeCore {
     (void)request(REQ_REPORT_DROP_TOKENS, w.b);
   }
 
+  // The stream the next fill runs on (round robin), ordered after the node stream's queued work.
+  hipStream_t next_fill_stream() {
+    if (fill_streams.empty()) return stream;
+    const size_t i = fill_next++ % fill_streams.size();
+    hipStream_t s = fill_streams[i];
+    if (hipStreamQuery(stream) == hipErrorNotReady) {
+      // producer kernels of the source may still run on the node stream
+      if (hipEventRecord(node_ev, stream) == hipSuccess) (void)hipStreamWaitEvent(s, node_ev, 0);
+    }
+    (void)hipGetLastError();
+    fill_dirty[i] = 1;
+    return s;
+  }
+
+  // Order every fill launched so far before work queued on the node stream from now on.
+  void fence_fills() {
+    for (size_t i = 0; i < fill_streams.size(); ++i) {
+      if (!fill_dirty[i]) continue;
+      fill_dirty[i] = 0;
+      if (hipStreamQuery(fill_streams[i]) == hipSuccess) continue;  // already drained
+      if (hipEventRecord(fill_events[i], fill_streams[i]) == hipSuccess)
+        (void)hipStreamWaitEvent(stream, fill_events[i], 0);
+    }
+    (void)hipGetLastError();
+  }
+
   ~NodeCore() {
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
+    for (hipStream_t s : fill_streams) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+    for (hipEvent_t e : fill_events) (void)hipEventDestroy(e);
+    if (node_ev) (void)hipEventDestroy(node_ev);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& kv : recv_pool) (void)hipFree(kv.second);
     if (fill_done) (void)hipFree(fill_done);
@@ -310,6 +364,15 @@ struct dora_node {
   std::vector<dora::TimingPair> timing;  // ring of kTimingPairs
   size_t timing_next = 0;
   uint64_t timing_seq = 0;
+  uint64_t timing_period = 0;            // stamp every n-th pack (0: DORA_GPU_TIMING_SAMPLE)
+  hipEvent_t timing_ref = nullptr;       // recorded when profiling is (re)enabled
+  std::vector<double> intervals;         // (start, stop) ms after timing_ref per stamped pack
+  // Timed region (dora_node_region_begin/end): the first pack after begin stamps its start;
+  // end records a stop event on every fill stream once the packs queued there have finished.
+  bool region_armed = false, region_started = false;
+  hipEvent_t region_start = nullptr;
+  std::vector<hipEvent_t> region_stop;
+  uint64_t region_packs = 0, region_bytes = 0;
   uint64_t pack_count = 0, pack_bytes = 0;
   double pack_ms = 0;
   uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
@@ -762,6 +825,7 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303
 }
 
 constexpr size_t kTimingPairs = 64;
+constexpr size_t kMaxIntervals = 1 << 16;  // stamped packs whose (start, stop) are kept
 
 void harvest(dora_node* n, TimingPair& p) {
   if (!p.pending) return;
@@ -771,7 +835,15 @@ void harvest(dora_node* n, TimingPair& p) {
     n->pack_ms += ms;
     ++n->pack_count;
     n->pack_bytes += p.bytes;
+    float a = 0, b = 0;
+    if (n->timing_ref && n->intervals.size() < 2 * kMaxIntervals &&
+        hipEventElapsedTime(&a, n->timing_ref, p.start) == hipSuccess &&
+        hipEventElapsedTime(&b, n->timing_ref, p.stop) == hipSuccess) {
+      n->intervals.push_back(a);
+      n->intervals.push_back(b);
+    }
   }
+  (void)hipGetLastError();
   p.pending = false;
 }
 
@@ -781,6 +853,7 @@ void harvest_all(dora_node* n) {
 
 int ensure_timing(dora_node* n) {
   if (!n->timing.empty()) return DORA_OK;
+  DORA_HIP(hipEventCreate(&n->timing_ref));
   n->timing.resize(kTimingPairs);
   for (auto& p : n->timing) {
     DORA_HIP(hipEventCreate(&p.start));
@@ -798,9 +871,8 @@ TimingPair* next_timing_pair(dora_node* n, uint64_t bytes) {
   return &p;
 }
 
-// Tell receivers when the fill enqueued on the node stream is complete.
-hipError_t order_fill(dora_node* n, dora_sample* s) {
-  hipStream_t st = n->core->stream;
+// Tell receivers when the fill enqueued on stream `st` is complete.
+hipError_t order_fill(dora_node* n, dora_sample* s, hipStream_t st) {
   if (s->slot->flag >= 0) {
     // async: the stream writes the send epoch into the slot's fill flag once the fill has
     // completed; the receiver polls it, the sender moves on
@@ -827,9 +899,10 @@ bool kernel_signal() {
   return v;
 }
 
-// Launch the fill of sample `s` (segments into its slot) and order its completion signal.
+// Launch the fill of sample `s` (segments into its slot) on stream `st` and order its
+// completion signal.
 int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
-                ArrowDeviceType dev, hipEvent_t t_start, hipEvent_t t_stop) {
+                ArrowDeviceType dev, hipStream_t st, hipEvent_t t_start, hipEvent_t t_stop) {
   FillSignal sig{};
   const FillSignal* sp = nullptr;
   if (s->slot->flag >= 0 && n->core->fill_done && kernel_signal()) {
@@ -839,15 +912,15 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     sp = &sig;
   }
   bool signalled = false;
-  int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), n->core->stream,
-                       t_start, t_stop, sp, &signalled);
+  int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start,
+                       t_stop, sp, &signalled);
   if (rc != DORA_OK) return rc;
   if (signalled) {
     s->epoch = sig.epoch;
     s->fill = FILL_FLAG;
     return DORA_OK;
   }
-  hipError_t e = order_fill(n, s);
+  hipError_t e = order_fill(n, s, st);
   if (e != hipSuccess) return fail(DORA_ERR_HIP, "fill signal: %s", hipGetErrorString(e));
   return DORA_OK;
 }
@@ -873,16 +946,17 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
     Segment seg{in->ptr, 0, len};
     if (in->remote_device >= 0 && peer_copy_mode() == PEER_SDMA) {
       rc = enqueue_peer_copy(n->core.get(), s->slot->ptr, in->ptr, in->remote_device, len);
-      hipError_t e = rc == DORA_OK ? order_fill(n, s) : hipSuccess;
+      hipError_t e = rc == DORA_OK ? order_fill(n, s, n->core->stream) : hipSuccess;
       if (rc == DORA_OK && e != hipSuccess)
         rc = fail(DORA_ERR_HIP, "forward: %s", hipGetErrorString(e));
     } else {
-      // the pack kernel, reading the peer's HBM over xGMI for a cross-GPU input
+      // the pack kernel, reading the peer's HBM over xGMI for a cross-GPU input; on the node
+      // stream, which the input's destructor drains before its token goes back
       rc = in->remote_device >= 0 ? ensure_peer_access(n->core.get(), in->remote_device)
                                   : DORA_OK;
       if (rc == DORA_OK)
         rc = fill_sample(n, s, &seg, 1, device_src ? ARROW_DEVICE_ROCM : ARROW_DEVICE_CPU,
-                         nullptr, nullptr);
+                         n->core->stream, nullptr, nullptr);
     }
     if (rc == DORA_OK && in->remote_device >= 0) {
       n->core->peer_copies.fetch_add(1, std::memory_order_relaxed);
@@ -917,11 +991,21 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   } else if (plan->size) {
     // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
     // every `timing_sample()`-th pack is stamped (DORA_GPU_TIMING_SAMPLE, default 8).
+    const uint64_t period = n->timing_period ? n->timing_period : timing_sample();
     const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU &&
-                       (n->timing_seq++ % timing_sample()) == 0;
+                       (n->timing_seq++ % period) == 0;
     TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
+    hipEvent_t t_start = tp ? tp->start : nullptr, t_stop = tp ? tp->stop : nullptr;
+    if (n->region_armed && plan->dev != ARROW_DEVICE_CPU) {
+      if (!n->region_started && !tp) {  // first pack of the region: its start is the origin
+        t_start = n->region_start;
+        n->region_started = true;
+      }
+      ++n->region_packs;
+      n->region_bytes += plan->size;
+    }
     rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
-                     tp ? tp->start : nullptr, tp ? tp->stop : nullptr);
+                     n->core->next_fill_stream(), t_start, t_stop);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
@@ -982,6 +1066,18 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   if (device >= 0) {  // device < 0: host-only node (control plane + inline Vec samples only)
     DORA_HIP(hipSetDevice(device));
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
+    if (dora::fill_stream_count() > 1 && dora::async_sends()) {
+      DORA_HIP(hipEventCreateWithFlags(&core->node_ev, hipEventDisableTiming));
+      for (size_t i = 0; i < dora::fill_stream_count(); ++i) {
+        hipStream_t s = nullptr;
+        hipEvent_t e = nullptr;
+        DORA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        core->fill_streams.push_back(s);
+        DORA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        core->fill_events.push_back(e);
+      }
+      core->fill_dirty.assign(core->fill_streams.size(), 0);
+    }
     if (dora::async_sends()) {
       // host-register the control region so this node's stream can write fill epochs into it
       void* dev = nullptr;
@@ -1079,10 +1175,17 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     (void)hipEventDestroy(p.start);
     (void)hipEventDestroy(p.stop);
   }
+  if (n->timing_ref) (void)hipEventDestroy(n->timing_ref);
+  if (n->region_start) (void)hipEventDestroy(n->region_start);
+  for (hipEvent_t e : n->region_stop) (void)hipEventDestroy(e);
   delete n;
 }
 
-dora_stream_t dora_node_stream(dora_node* n) { return n ? n->core->stream : nullptr; }
+dora_stream_t dora_node_stream(dora_node* n) {
+  if (!n) return nullptr;
+  n->core->fence_fills();  // work the caller queues next runs after every fill so far
+  return n->core->stream;
+}
 
 int dora_node_allocate_data_sample(dora_node* n, size_t len, dora_sample** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
@@ -1286,6 +1389,58 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
   return DORA_OK;
 }
 
+int dora_node_set_timing_period(dora_node* n, uint64_t period) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  n->timing_period = period;
+  return DORA_OK;
+}
+
+int dora_node_region_begin(dora_node* n) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
+  if (!n->region_start) {
+    DORA_HIP(hipEventCreate(&n->region_start));
+    const size_t k = std::max<size_t>(1, n->core->fill_streams.size());
+    n->region_stop.resize(k + 1);
+    for (auto& e : n->region_stop) DORA_HIP(hipEventCreate(&e));
+  }
+  n->region_armed = true;
+  n->region_started = false;
+  n->region_packs = n->region_bytes = 0;
+  return DORA_OK;
+}
+
+int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_t* bytes) {
+  if (!n || !span_ms) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (!n->region_armed) return dora::fail(DORA_ERR_INVALID, "no region begun");
+  n->region_armed = false;
+  *span_ms = 0;
+  if (packs) *packs = n->region_packs;
+  if (bytes) *bytes = n->region_bytes;
+  if (!n->region_started) return DORA_OK;
+  // stop = the end of the last pack on each fill stream (and the node stream)
+  std::vector<hipStream_t> ss = n->core->fill_streams;
+  ss.push_back(n->core->stream);
+  for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i)
+    DORA_HIP(hipEventRecord(n->region_stop[i], ss[i]));
+  for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i) {
+    DORA_HIP(hipEventSynchronize(n->region_stop[i]));
+    float ms = 0;
+    DORA_HIP(hipEventElapsedTime(&ms, n->region_start, n->region_stop[i]));
+    *span_ms = std::max<double>(*span_ms, ms);
+  }
+  return DORA_OK;
+}
+
+int dora_node_pack_intervals(dora_node* n, double* out_ms, size_t cap, size_t* count) {
+  if (!n || !count || (!out_ms && cap)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  dora::harvest_all(n);
+  const size_t pairs = n->intervals.size() / 2;
+  *count = pairs;
+  for (size_t i = 0; i < 2 * std::min(cap, pairs); ++i) out_ms[i] = n->intervals[i];
+  return DORA_OK;
+}
+
 int dora_node_peer_stats(dora_node* n, uint64_t* copies, uint64_t* bytes) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (copies) *copies = n->core->peer_copies.load();
@@ -1310,6 +1465,12 @@ int dora_node_set_profiling(dora_node* n, int enable) {
   }
   dora::harvest_all(n);
   n->profile = enable != 0;
+  n->intervals.clear();
+  if (enable) {
+    // time origin of dora_node_pack_intervals
+    DORA_HIP(hipEventRecord(n->timing_ref, n->core->stream));
+    DORA_HIP(hipEventSynchronize(n->timing_ref));
+  }
   for (auto& x : n->phase_ns) x = 0;
   n->phase_count = 0;
   n->pack_count = 0;

@@ -227,6 +227,27 @@ class Node:
     def set_profiling(self, enable: bool = True):
         call("dora_node_set_profiling", self.handle, int(enable))
 
+    def set_timing_period(self, period: int):
+        """Stamp every `period`-th pack launch (0: DORA_GPU_TIMING_SAMPLE, default 8)."""
+        call("dora_node_set_timing_period", self.handle, int(period))
+
+    def pack_intervals(self, cap: int = 1 << 16):
+        """[(start_ms, stop_ms)] of the stamped packs since profiling was enabled."""
+        out, n = (c_double * (2 * cap))(), c_size_t()
+        call("dora_node_pack_intervals", self.handle, out, cap, byref(n))
+        k = min(n.value, cap)
+        return [(out[2 * i], out[2 * i + 1]) for i in range(k)]
+
+    def region_begin(self):
+        """Start a device-timed run of sends (dora_node_region_begin)."""
+        call("dora_node_region_begin", self.handle)
+
+    def region_end(self) -> dict:
+        """Device span of the sends since region_begin: first pack start -> last pack end."""
+        ms, packs, b = c_double(), c_uint64(), c_uint64()
+        call("dora_node_region_end", self.handle, byref(ms), byref(packs), byref(b))
+        return {"span_ms": ms.value, "packs": packs.value, "bytes": b.value}
+
     def pack_stats(self) -> dict:
         c, ms, b = c_uint64(), c_double(), c_uint64()
         call("dora_node_pack_stats", self.handle, byref(c), byref(ms), byref(b))

@@ -229,8 +229,11 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
 int dora_node_init_from_env(dora_node** out);
 /* Drop for DoraNode (mod.rs:384-431): close outputs, wait <= 10 s for drop tokens, done. */
 void dora_node_free(dora_node* node);
-/* The HIP stream the node packs on; consumers must run their kernels on it so the drop token
- * is only returned after they have read the sample. */
+/* The node's HIP stream; consumers must run their kernels on it so the drop token is only
+ * returned after they have read the sample.  Sends spread their fills over the node's fill
+ * streams (DORA_GPU_FILL_STREAMS, default 3): a fill runs after the work queued on this stream
+ * when the send is made, and the call orders every fill launched so far before the work the
+ * caller queues on the returned stream next (a device source may be rewritten there). */
 dora_stream_t dora_node_stream(dora_node* node);
 
 /* allocate_data_sample (mod.rs:303-346): a device slot of `len` bytes (best-fit from the
@@ -299,9 +302,20 @@ int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hi
  * engines (DORA_GPU_PEER_COPY=sdma).  Counts and bytes of such pulls.  DORA_GPU_EDGE_COPY=1
  * forces the path on same-GPU edges. */
 int dora_node_peer_stats(dora_node* node, uint64_t* copies, uint64_t* bytes);
-/* Pack-kernel timing on the node stream (HIP events around every pack launch). */
+/* Pack-kernel timing: hipExtLaunchKernel start/stop stamps of every n-th pack launch
+ * (dora_node_set_timing_period; 0 = DORA_GPU_TIMING_SAMPLE, default 8). */
 int dora_node_set_profiling(dora_node* node, int enable);
+int dora_node_set_timing_period(dora_node* node, uint64_t period);
 int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);
+/* (start, stop) of each stamped pack in ms after profiling was enabled, `cap` pairs at most
+ * (kernels on different fill streams overlap: their union is the pack busy time). */
+int dora_node_pack_intervals(dora_node* node, double* out_ms, size_t cap, size_t* count);
+/* Device span of a run of sends: from the start of the first pack launched after
+ * region_begin (hipExtLaunchKernel start stamp) to the end of the last pack on every fill
+ * stream (HIP events recorded by region_end, which waits for them); packs and sample bytes
+ * launched in between. */
+int dora_node_region_begin(dora_node* node);
+int dora_node_region_end(dora_node* node, double* span_ms, uint64_t* packs, uint64_t* bytes);
 /* Mean host time (µs) per send phase since profiling was (re)enabled: [0] allocate incl.
  * backpressure, [1] pack launch, [2] fill event record / stream sync, [3] descriptor send. */
 int dora_node_send_profile(dora_node* node, double* out_us, size_t n_out, uint64_t* count);
