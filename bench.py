@@ -38,7 +38,7 @@ LADDER = [4096, 16384, 40960, 65536, 409600, 1 << 20, 4096000, 4 << 20, 16 << 20
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=40960000)
     ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--lat-n", type=int, default=50, help="latency-mode messages per size")
     ap.add_argument("--lat-gap-us", type=int, default=1000)
     ap.add_argument("--no-ladder", action="store_true")
+    ap.add_argument("--tp-n", type=int, default=200,
+                    help="throughput ladder: back-to-back messages per size (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
     ap.add_argument("--no-cross-gpu", action="store_true",
@@ -367,6 +369,37 @@ def main():
         for b in ladder_bufs.values():
             b.free()
 
+    # ---- throughput ladder (reference throughput mode: back-to-back messages per size) ----
+    tp_ladder = {}
+    if not args.no_ladder and args.tp_n > 0 and args.workload == "c2":
+        for size in LADDER:
+            nb = max(1, min(16, (640 << 20) // size))
+            bufs = [device.DeviceBuffer(size) for _ in range(nb)]
+            for b in bufs:
+                device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
+            stream.sync()
+            for k in range(8):  # warm the slot cache for this size
+                node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, {"seq": seq})
+                seq += 1
+            node.send_output("throughput", b"", {"seq": seq, "ack": True})
+            wait_ack(seq)
+            seq += 1
+            t_a = time.perf_counter()
+            for k in range(args.tp_n):
+                node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, {"seq": seq})
+                seq += 1
+            node.send_output("throughput", b"", {"seq": seq, "ack": True})
+            wait_ack(seq)
+            seq += 1
+            dt = time.perf_counter() - t_a
+            tp_ladder[str(size)] = {"GBps": round(args.tp_n * size / dt / 1e9, 2),
+                                    "msgs_per_s": round(args.tp_n / dt, 1),
+                                    "us_per_msg": round(dt / args.tp_n * 1e6, 2),
+                                    "hbm_frac_2S": round(2 * args.tp_n * size / dt / 1e9 /
+                                                         HBM_PEAK_GBPS, 4)}
+            for b in bufs:
+                b.free()
+
     # ---- timed region: K back-to-back steps, closed by the sink's ack ----
     barrier()
     device.set_device(local_rank)
@@ -454,6 +487,7 @@ def main():
                    "msg_bytes": S, "parallelism": f"dp{world} (one dataflow per GPU)",
                    "sources_rotated": nsrc},
         "latency_us": lat,
+        "throughput_per_size": tp_ladder,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic[1] if traffic else None,
