@@ -271,6 +271,8 @@ struct TiNode {
   uint64_t len = 0, null_count = 0, offset = 0;
   bool has_validity = false;
   std::vector<uint8_t> validity;
+  bool in_sample = false;  // tag 2: bitmap at sample[voff, voff + vlen)
+  uint64_t voff = 0, vlen = 0;
   std::vector<std::pair<uint64_t, uint64_t>> bufs;
   std::vector<TiNode> children;
 };
@@ -282,12 +284,18 @@ void decode_ti(Cursor& c, TiNode& t) {
   c.i += sl;
   t.len = c.u64();
   t.null_count = c.u64();
-  t.has_validity = c.u8() != 0;
-  if (t.has_validity) {
+  const uint8_t tag = c.u8();
+  if (tag > 2) throw std::invalid_argument("unknown validity tag in type info");
+  t.has_validity = tag != 0;
+  t.in_sample = tag == 2;
+  if (tag == 1) {
     const uint64_t vl = c.u64();
     c.need(vl);
     t.validity.assign(c.p + c.i, c.p + c.i + vl);
     c.i += vl;
+  } else if (tag == 2) {
+    t.voff = c.u64();
+    t.vlen = c.u64();
   }
   t.offset = c.u64();
   const uint32_t nb = c.u32();
@@ -302,7 +310,8 @@ void decode_ti(Cursor& c, TiNode& t) {
 
 // buffer_into_arrow_array (event.rs:61-91) on a device sample.
 void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sample,
-                       uint64_t sample_len, const std::shared_ptr<void>& keep, ArrowArray* out) {
+                       uint64_t sample_len, uint64_t ext_len, const std::shared_ptr<void>& keep,
+                       ArrowArray* out) {
   Layout l = layout_of(s->format);
   const size_t nbuf = (l.can_null ? 1 : 0) + t.bufs.size();
   if (t.bufs.size() != l.specs.size())
@@ -312,7 +321,12 @@ void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sam
   try {
     size_t bi = 0;
     if (l.can_null) {
-      if (t.has_validity) {
+      if (t.in_sample) {
+        // the bitmap travelled in the slot's tail: zero-copy like the buffers
+        if (t.voff < sample_len || t.voff + t.vlen > ext_len)
+          throw std::invalid_argument("in-sample validity outside the slot's tail");
+        p->buffers[0] = sample + t.voff;
+      } else if (t.has_validity) {
         void* d = nullptr;
         hip_ok(hipMalloc(&d, t.validity.size() ? t.validity.size() : 1), "hipMalloc validity");
         p->dev_owned.push_back(d);
@@ -337,14 +351,15 @@ void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sam
     if (s->dictionary) {
       if (t.children.size() != 1) throw std::invalid_argument("dictionary needs one child");
       p->dictionary = new ArrowArray();
-      build_from_sample(t.children[0], s->dictionary, sample, sample_len, keep, p->dictionary);
+      build_from_sample(t.children[0], s->dictionary, sample, sample_len, ext_len, keep,
+                        p->dictionary);
     } else {
       if (t.children.size() != size_t(s->n_children))
         throw std::invalid_argument("type info child count does not match the data type");
       for (size_t k = 0; k < t.children.size(); ++k) {
         auto* ch = new ArrowArray();
         p->children.push_back(ch);
-        build_from_sample(t.children[k], kids[k], sample, sample_len, keep, ch);
+        build_from_sample(t.children[k], kids[k], sample, sample_len, ext_len, keep, ch);
       }
     }
   } catch (...) {
@@ -406,7 +421,9 @@ int guarded(const std::function<void()>& fn) {
 }  // namespace
 
 int import_sample(const void* sample, uint64_t sample_len, const uint8_t* ti, size_t ti_len,
-                  std::shared_ptr<void> keep, ArrowArray* out_array, ArrowSchema* out_schema) {
+                  std::shared_ptr<void> keep, ArrowArray* out_array, ArrowSchema* out_schema,
+                  uint64_t ext_len) {
+  if (ext_len < sample_len) ext_len = sample_len;
   return guarded([&] {
     Cursor c{ti, ti_len};
     TiNode root;
@@ -418,13 +435,85 @@ int import_sample(const void* sample, uint64_t sample_len, const uint8_t* ti, si
       if (sample_len == 0) {
         build_empty(out_schema, out_array);  // event.rs:65-67
       } else {
-        build_from_sample(root, out_schema, static_cast<const uint8_t*>(sample), sample_len, keep,
-                          out_array);
+        build_from_sample(root, out_schema, static_cast<const uint8_t*>(sample), sample_len,
+                          ext_len, keep, out_array);
       }
     } catch (...) {
       release_schema(out_schema);
       throw;
     }
+  });
+}
+
+namespace {
+
+void copy_bytes(Cursor& c, std::vector<uint8_t>& o, size_t k) {
+  c.need(k);
+  o.insert(o.end(), c.p + c.i, c.p + c.i + k);
+  c.i += k;
+}
+
+void put64(std::vector<uint8_t>& o, uint64_t v) {
+  for (int i = 0; i < 8; ++i) o.push_back(static_cast<uint8_t>(v >> (8 * i)));
+}
+
+// One type-info node (serialize_type_info's layout) copied to `o` with tag-2 bitmaps inlined.
+void inline_ti(Cursor& c, std::vector<uint8_t>& o, const uint8_t* sample, uint64_t ext_len) {
+  Cursor sc = c;
+  const uint32_t sl = sc.u32();
+  copy_bytes(c, o, 4 + size_t(sl) + 16);  // schema, len, null_count
+  const uint8_t tag = c.u8();
+  if (tag == 2) {
+    const uint64_t off = c.u64(), vl = c.u64();
+    if (off + vl > ext_len) throw std::invalid_argument("in-sample validity outside the slot");
+    o.push_back(1);
+    put64(o, vl);
+    const size_t at = o.size();
+    o.resize(at + vl);
+    if (vl) hip_ok(hipMemcpy(o.data() + at, sample + off, vl, hipMemcpyDeviceToHost),
+                   "validity read-back");
+  } else {
+    o.push_back(tag);
+    if (tag == 1) {
+      Cursor vc = c;
+      copy_bytes(c, o, 8 + size_t(vc.u64()));
+    } else if (tag != 0) {
+      throw std::invalid_argument("unknown validity tag in type info");
+    }
+  }
+  Cursor bc = c;
+  bc.u64();
+  const uint32_t nb = bc.u32();
+  copy_bytes(c, o, 8 + 4 + 16 * size_t(nb));  // offset, buffer offsets
+  const uint32_t nch = c.u32();
+  for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(nch >> (8 * i)));
+  for (uint32_t k = 0; k < nch; ++k) inline_ti(c, o, sample, ext_len);
+}
+
+bool has_in_sample(const TiNode& t) {
+  if (t.in_sample) return true;
+  for (auto& ch : t.children)
+    if (has_in_sample(ch)) return true;
+  return false;
+}
+
+}  // namespace
+
+int inline_type_info(const uint8_t* ti, size_t ti_len, const void* sample, uint64_t ext_len,
+                     std::vector<uint8_t>* out, bool* changed) {
+  return guarded([&] {
+    *changed = false;
+    Cursor c{ti, ti_len};
+    TiNode root;
+    decode_ti(c, root);
+    if (!has_in_sample(root)) return;
+    if (!sample) throw std::invalid_argument("in-sample validity without sample data");
+    Cursor w{ti, ti_len};
+    std::vector<uint8_t> o;
+    o.reserve(ti_len + 4096);
+    inline_ti(w, o, static_cast<const uint8_t*>(sample), ext_len);
+    out->swap(o);
+    *changed = true;
   });
 }
 

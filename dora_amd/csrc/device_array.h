@@ -4,14 +4,22 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <vector>
 
 #include "dora_gpu.h"
 
 namespace dora {
 
 // `keep` is held by every imported ArrowArray node until released (the received slot).
+// `ext_len` (>= sample_len, 0 = sample_len): readable bytes of the slot incl. the validity tail
+// that type infos with in-sample bitmaps (tag 2) point into.
 int import_sample(const void* sample, uint64_t sample_len, const uint8_t* type_info,
                   size_t type_info_len, std::shared_ptr<void> keep, ArrowArray* out_array,
-                  ArrowSchema* out_schema);
+                  ArrowSchema* out_schema, uint64_t ext_len = 0);
+
+// The reference (inline) form of a type info: in-sample bitmaps (tag 2) read back from the
+// device sample into tag-1 bytes.  `*changed` = false (out untouched) when there were none.
+int inline_type_info(const uint8_t* type_info, size_t type_info_len, const void* sample,
+                     uint64_t ext_len, std::vector<uint8_t>* out, bool* changed);
 
 }  // namespace dora

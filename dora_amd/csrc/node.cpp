@@ -90,6 +90,19 @@ size_t fill_stream_count() {
   return v;
 }
 
+// Validity bitmaps of device arrays travel in the sample's tail (DORA_GPU_VALIDITY=inline:
+// in the metadata, as the reference's ArrowTypeInfo carries them).  Sending a device array then
+// reads nothing back to the host: the plan is a host walk and one pack launch copies buffers
+// and bitmaps; receivers import the bitmaps zero-copy (C3: 125 KB per cloud no longer crosses
+// PCIe twice and the control plane once per message).
+bool validity_in_sample() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_VALIDITY");
+    return !(e && std::string(e) == "inline");
+  }();
+  return v;
+}
+
 uint64_t timing_sample() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_TIMING_SAMPLE");
@@ -300,6 +313,7 @@ struct InputData {
   std::shared_ptr<NodeCore> core;
   const void* ptr = nullptr;
   uint64_t len = 0;
+  uint64_t ext_len = 0;       // bytes of the sample incl. its validity tail (>= len)
   bool has_token = false;
   DropToken token{};
   std::vector<uint8_t> vec;   // inline (Vec) samples stay on the host
@@ -327,6 +341,7 @@ struct dora_sample {
   dora::Slot* slot = nullptr;
   std::vector<uint8_t> vec;  // zero-length samples (Vec path)
   uint64_t len = 0;
+  uint64_t ext_len = 0;      // slot bytes filled: len + the validity tail (0: len)
   uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
   uint64_t epoch = 0;
 };
@@ -348,6 +363,10 @@ struct dora_event {
   std::string error;
   bool pending = false;  // device input not yet completed (fill wait / cross-GPU pull)
   dora::DeviceIpc ipc{};
+  // dora_event_type_info's reference (inline-validity) form, built on first request when the
+  // type info points into the sample's validity tail
+  mutable bool ti_checked = false;
+  mutable std::vector<uint8_t> ti_inline;
 };
 
 struct dora_node {
@@ -490,11 +509,13 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         in->vec = std::move(d.vec);
         in->ptr = in->vec.data();
         in->len = in->vec.size();
+        in->ext_len = in->len;
       } else if (d.kind == DATA_DEVICE_IPC) {
         in->has_token = true;  // set first: a mapping failure still returns the token
         in->token = d.ipc.token;
         trace(TP_POPPED, in->token);
         in->len = d.ipc.len;
+        in->ext_len = std::max(d.ipc.ext_len, d.ipc.len);
         void* base = nullptr;
         if (d.ipc.owner_pid == getpid()) {
           std::lock_guard<std::mutex> g(own_slots().mu);
@@ -654,11 +675,12 @@ int ensure_local(InputData* in) {
   if (!in || in->remote_device < 0) return DORA_OK;
   NodeCore* c = in->core.get();
   uint64_t cap = 0;
-  void* local = c->recv_pool_get(in->len, &cap);
-  if (!local) return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->len);
+  void* local = c->recv_pool_get(in->ext_len, &cap);
+  if (!local)
+    return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->ext_len);
   int rc;
   if (peer_copy_mode() == PEER_SDMA) {
-    rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->len);
+    rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->ext_len);
     if (rc == DORA_OK) {
       hipError_t e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "cross-GPU pull: %s", hipGetErrorString(e));
@@ -666,7 +688,7 @@ int ensure_local(InputData* in) {
   } else {
     // the pack kernel reads the peer's HBM over xGMI; wait on its own completion flag
     rc = ensure_peer_access(c, in->remote_device);
-    Segment seg{in->ptr, 0, in->len};
+    Segment seg{in->ptr, 0, in->ext_len};
     if (rc == DORA_OK) rc = launch_pack_wait(&seg, 1, static_cast<uint8_t*>(local), c->stream);
   }
   if (rc != DORA_OK) {
@@ -681,7 +703,7 @@ int ensure_local(InputData* in) {
   trace(TP_RELEASED, in->token);
   in->has_token = false;
   c->peer_copies.fetch_add(1, std::memory_order_relaxed);
-  c->peer_bytes.fetch_add(in->len, std::memory_order_relaxed);
+  c->peer_bytes.fetch_add(in->ext_len, std::memory_order_relaxed);
   return DORA_OK;
 }
 
@@ -751,6 +773,7 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.ipc.slot_id = slot->id;
       d.ipc.offset = 0;
       d.ipc.len = sample->len;
+      d.ipc.ext_len = std::max(sample->len, sample->ext_len);
       d.ipc.token = generate_drop_token();
       d.ipc.fill = sample->fill;
       if (sample->fill == FILL_FLAG) {
@@ -784,7 +807,9 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
 
 constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
 
-int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303-319
+// `ext_len` > len: the slot also holds a validity tail (plans with in-sample bitmaps).
+int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
+                 uint64_t ext_len = 0) {  // mod.rs:303-319
   if (n->core->device < 0) {
     // host-only node (no GPU): only the reference's inline `DataMessage::Vec` path exists
     if (len >= kZeroCopyThreshold)
@@ -814,7 +839,8 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out) {  // mod.rs:303
       handle_finished_drop_tokens(n);
       if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
     }
-    int rc = allocate_slot(n, len, &s->slot);
+    s->ext_len = std::max(len, ext_len);
+    int rc = allocate_slot(n, s->ext_len, &s->slot);
     if (rc != DORA_OK) {
       delete s;
       return rc;
@@ -932,8 +958,9 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
                   size_t params_len) {
   InputData* in = ev->data.get();
   const uint64_t len = in->len;
+  const uint64_t ext = std::max(in->ext_len, len);  // the validity tail travels along
   dora_sample* s = nullptr;
-  int rc = alloc_sample(n, len, &s);
+  int rc = alloc_sample(n, len, &s, ext);
   if (rc != DORA_OK) return rc;
   const bool device_src = in->has_token || in->local;
   if (len && !s->slot) {
@@ -943,9 +970,9 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
     }
     std::memcpy(s->vec.data(), in->ptr, len);
   } else if (len) {
-    Segment seg{in->ptr, 0, len};
+    Segment seg{in->ptr, 0, ext};
     if (in->remote_device >= 0 && peer_copy_mode() == PEER_SDMA) {
-      rc = enqueue_peer_copy(n->core.get(), s->slot->ptr, in->ptr, in->remote_device, len);
+      rc = enqueue_peer_copy(n->core.get(), s->slot->ptr, in->ptr, in->remote_device, ext);
       hipError_t e = rc == DORA_OK ? order_fill(n, s, n->core->stream) : hipSuccess;
       if (rc == DORA_OK && e != hipSuccess)
         rc = fail(DORA_ERR_HIP, "forward: %s", hipGetErrorString(e));
@@ -960,7 +987,7 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
     }
     if (rc == DORA_OK && in->remote_device >= 0) {
       n->core->peer_copies.fetch_add(1, std::memory_order_relaxed);
-      n->core->peer_bytes.fetch_add(len, std::memory_order_relaxed);
+      n->core->peer_bytes.fetch_add(ext, std::memory_order_relaxed);
     }
     if (rc != DORA_OK) {
       add_to_cache(n, s->slot);
@@ -977,7 +1004,7 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
                   size_t params_len) {
   dora_sample* s = nullptr;
   const uint64_t t0 = mono_ns();
-  int rc = alloc_sample(n, plan->size, &s);
+  int rc = alloc_sample(n, plan->size, &s, plan->fill_size());
   if (rc != DORA_OK) return rc;
   const uint64_t t1 = mono_ns();
   uint64_t t2 = t1, t3 = t1;
@@ -1226,7 +1253,9 @@ int dora_node_send_output(dora_node* n, const char* output_id, const struct Arro
   dora_plan* plan = nullptr;
   int rc = (n->compact && device_type == ARROW_DEVICE_ROCM)
                ? dora::build_plan_compact(array, schema, device_type, &plan)
-               : dora::build_plan(array, schema, device_type, &plan);
+               : dora::build_plan(array, schema, device_type, &plan,
+                                  device_type == ARROW_DEVICE_ROCM && n->core->device >= 0 &&
+                                      dora::validity_in_sample());
   if (rc != DORA_OK) return rc;
   rc = dora::pack_and_send(n, output_id, plan, params, params_len);
   delete plan;
@@ -1324,8 +1353,21 @@ int dora_event_is_device(const dora_event* e) {
 
 int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
   if (!e || !ti || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  *ti = e->meta.type_info.data();
-  *len = e->meta.type_info.size();
+  if (!e->ti_checked && e->type == DORA_EVENT_INPUT && e->data && e->data->ext_len > e->data->len) {
+    // bitmaps in the sample's tail: restore the reference's inline ArrowTypeInfo bytes
+    DORA_GUARD_BEGIN
+    int rc = dora::ensure_local(e->data.get());
+    if (rc != DORA_OK) return rc;
+    bool changed = false;
+    rc = dora::inline_type_info(e->meta.type_info.data(), e->meta.type_info.size(),
+                                e->data->ptr, e->data->ext_len, &e->ti_inline, &changed);
+    if (rc != DORA_OK) return rc;
+    DORA_GUARD_END
+  }
+  e->ti_checked = true;
+  const std::vector<uint8_t>& t = e->ti_inline.empty() ? e->meta.type_info : e->ti_inline;
+  *ti = t.data();
+  *len = t.size();
   return DORA_OK;
 }
 
@@ -1353,7 +1395,8 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
     return dora::fail(DORA_ERR_INVALID, "inline (host Vec) sample: read it with dora_event_data");
   std::shared_ptr<void> keep = e->data;
   return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
-                             e->meta.type_info.size(), keep, out_array, out_schema);
+                             e->meta.type_info.size(), keep, out_array, out_schema,
+                             e->data->ext_len);
 }
 
 void dora_event_free(dora_event* e) { delete e; }

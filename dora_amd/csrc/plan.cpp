@@ -165,6 +165,9 @@ struct Reader {
   mutable uint64_t total = 0;
   mutable size_t cursor = 0;
   const uint8_t* staged = nullptr;
+  // validity bitmaps of device arrays with a known null count go to the sample's tail
+  bool defer_validity = false;
+  mutable std::vector<const void*> deferred;  // their sources, in walk (DFS pre-order) order
 
   void read(void* dst, const void* src, size_t n) const {
     if (n == 0) return;
@@ -307,14 +310,25 @@ void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t&
   }
 
   if (l.can_null && a->n_buffers > 0 && a->buffers[0]) {
-    std::vector<uint8_t> v((total + 7) / 8);
-    rd.read(v.data(), a->buffers[0], v.size());
-    uint64_t nc = a->null_count >= 0 ? static_cast<uint64_t>(a->null_count)
-                                     : count_nulls(v, off, len);
-    if (nc != 0) {
-      ti.has_validity = true;
-      ti.validity = std::move(v);
-      ti.null_count = nc;
+    if (rd.defer_validity && rd.dev == ARROW_DEVICE_ROCM && a->null_count >= 0) {
+      // the same bytes the inline form would carry, copied on the device (no read-back)
+      if (a->null_count != 0) {
+        ti.has_validity = true;
+        ti.validity_in_sample = true;
+        ti.validity_len = (total + 7) / 8;
+        ti.null_count = static_cast<uint64_t>(a->null_count);
+        rd.deferred.push_back(a->buffers[0]);
+      }
+    } else {
+      std::vector<uint8_t> v((total + 7) / 8);
+      rd.read(v.data(), a->buffers[0], v.size());
+      uint64_t nc = a->null_count >= 0 ? static_cast<uint64_t>(a->null_count)
+                                       : count_nulls(v, off, len);
+      if (nc != 0) {
+        ti.has_validity = true;
+        ti.validity = std::move(v);
+        ti.null_count = nc;
+      }
     }
   }
 
@@ -468,8 +482,12 @@ void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& o) {
   o.insert(o.end(), t.schema.begin(), t.schema.end());
   put_u64(o, t.len);
   put_u64(o, t.null_count);
-  put_u8(o, t.has_validity ? 1 : 0);
-  if (t.has_validity) {
+  // validity tag: 0 none, 1 inline bytes (the reference's Option<Vec<u8>>), 2 in the sample
+  put_u8(o, !t.has_validity ? 0 : t.validity_in_sample ? 2 : 1);
+  if (t.has_validity && t.validity_in_sample) {
+    put_u64(o, t.validity_off);
+    put_u64(o, t.validity_len);
+  } else if (t.has_validity) {
     put_u64(o, t.validity.size());
     o.insert(o.end(), t.validity.begin(), t.validity.end());
   }
@@ -512,8 +530,24 @@ int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, Arrow
   return DORA_OK;
 }
 
+namespace {
+
+// Validity tail of a plan with deferred bitmaps: 64-B aligned after the sample, in walk order.
+void place_validity(TypeInfoNode& t, const std::vector<const void*>& src, size_t& k,
+                    uint64_t& next, std::vector<Segment>& segs) {
+  if (t.validity_in_sample) {
+    next = (next + 63) / 64 * 64;
+    t.validity_off = next;
+    segs.push_back({src.at(k++), next, t.validity_len});
+    next += t.validity_len;
+  }
+  for (auto& c : t.children) place_validity(c, src, k, next, segs);
+}
+
+}  // namespace
+
 int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
-               dora_plan** out) {
+               dora_plan** out, bool validity_in_sample) {
   if (!out) return fail(DORA_ERR_INVALID, "out is NULL");
   *out = nullptr;
   if (dev != ARROW_DEVICE_CPU && dev != ARROW_DEVICE_ROCM && dev != ARROW_DEVICE_ROCM_HOST)
@@ -523,6 +557,7 @@ int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceTy
   try {
     Reader rd;
     rd.dev = dev;
+    rd.defer_validity = validity_in_sample;
     uint64_t next = 0;
     if (dev == ARROW_DEVICE_ROCM) {
       rd.mode = Reader::COLLECT;
@@ -535,9 +570,15 @@ int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceTy
         rd.mode = Reader::DIRECT;
       }
       next = 0;
+      rd.deferred.clear();
     }
     walk(array, schema, rd, next, p->segs, p->root);
     p->size = next;
+    if (!rd.deferred.empty()) {
+      size_t k = 0;
+      place_validity(p->root, rd.deferred, k, next, p->segs);
+      p->ext_size = next;
+    }
   } catch (const std::domain_error& e) {
     delete p;
     return fail(DORA_ERR_UNSUPPORTED, "%s", e.what());

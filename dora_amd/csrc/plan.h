@@ -32,6 +32,12 @@ struct TypeInfoNode {
   uint64_t null_count = 0;
   bool has_validity = false;
   std::vector<uint8_t> validity;
+  // Node sends of device arrays: the bitmap travels in the sample itself, in the slot's tail
+  // past the reference layout's `size` bytes ([validity_off, +validity_len)), instead of inline
+  // in the metadata; receivers import it zero-copy and dora_event_type_info restores the
+  // inline form on demand.
+  bool validity_in_sample = false;
+  uint64_t validity_off = 0, validity_len = 0;
   uint64_t offset = 0;
   std::vector<std::pair<uint64_t, uint64_t>> bufs;  // BufferOffset {offset, len}
   std::vector<TypeInfoNode> children;
@@ -86,7 +92,7 @@ std::string schema_sig(const ArrowSchema* s);
 uint64_t metadata_len(const char* meta);
 Layout layout_of(const std::string& format);
 int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
-               dora_plan** out);
+               dora_plan** out, bool validity_in_sample = false);
 int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
                        dora_plan** out);
 
@@ -95,7 +101,9 @@ int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, Arrow
 struct dora_plan {
   ArrowDeviceType dev = ARROW_DEVICE_ROCM;
   bool compact = false;  // built by dora_gpu_plan_compact (carries transform segments)
-  uint64_t size = 0;
+  uint64_t size = 0;      // required_data_size: the reference sample
+  uint64_t ext_size = 0;  // bytes to allocate and fill incl. a validity tail (0: == size)
   std::vector<dora::Segment> segs;
   dora::TypeInfoNode root;
+  uint64_t fill_size() const { return ext_size > size ? ext_size : size; }
 };

@@ -52,6 +52,7 @@ struct DeviceIpc {
   uint64_t slot_id;    // unique per owner process
   uint64_t offset;     // sample offset inside the slot allocation
   uint64_t len;
+  uint64_t ext_len;    // bytes filled from `offset`: len + the validity tail (>= len)
   DropToken token;
   // How the receiver learns that the fill is complete:
   //   FILL_DONE  the sender synchronised before sending;
@@ -107,6 +108,7 @@ class WBuf {
       u64(d.ipc.slot_id);
       u64(d.ipc.offset);
       u64(d.ipc.len);
+      u64(d.ipc.ext_len);
       token(d.ipc.token);
       u8(d.ipc.fill);
       if (d.ipc.fill == FILL_FLAG) {
@@ -192,6 +194,8 @@ class RBuf {
       d.ipc.slot_id = u64();
       d.ipc.offset = u64();
       d.ipc.len = u64();
+      d.ipc.ext_len = u64();
+      if (d.ipc.ext_len < d.ipc.len) throw std::invalid_argument("sample ext_len < len");
       d.ipc.token = token();
       d.ipc.fill = u8();
       if (d.ipc.fill == FILL_FLAG) {

@@ -52,6 +52,9 @@ class ArrowTypeInfo:
     child_data: List["ArrowTypeInfo"] = field(default_factory=list)
     schema: Optional[SchemaNode] = None
     raw: bytes = b""                   # the serialized form this was decoded from
+    # tag 2 (node sends of device arrays): the bitmap is sample[off, off + len) of the slot's
+    # validity tail; dora_event_type_info hands receivers the inline form (validity bytes)
+    validity_in_sample: Optional[tuple] = None
 
     @staticmethod
     def byte_array(data_len: int) -> "ArrowTypeInfo":   # metadata.rs:74-87
@@ -123,12 +126,19 @@ def _type_info(r: _Reader, raw_all: bytes) -> ArrowTypeInfo:
     schema = _schema(_Reader(r.s()))
     n = r.u64()
     null_count = r.u64()
-    validity = r.take(r.u64()) if r.u8() else None
+    tag = r.u8()
+    validity, in_sample = None, None
+    if tag == 1:
+        validity = r.take(r.u64())
+    elif tag == 2:
+        in_sample = (r.u64(), r.u64())
+    elif tag != 0:
+        raise ValueError(f"unknown validity tag {tag}")
     offset = r.u64()
     bufs = [BufferOffset(r.u64(), r.u64()) for _ in range(r.u32())]
     children = [_type_info(r, raw_all) for _ in range(r.u32())]
     return ArrowTypeInfo(schema.signature(), n, null_count, validity, offset, bufs, children,
-                         schema, raw_all[start:r.i])
+                         schema, raw_all[start:r.i], in_sample)
 
 
 def decode(raw: bytes) -> ArrowTypeInfo:
