@@ -19,7 +19,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
 LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp",
-               "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp"]
+               "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp", "aql.cpp"]
+AQL_KERNELS = "aql_kernels.hip"  # standalone gfx950 code object embedded in the library
 LIB_NAME = "libdora_gpu.so"
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
@@ -63,13 +64,43 @@ def _compile_all(sources, verbose):
     return objs
 
 
+def _aql_blob(verbose):
+    """The AQL pack kernels as a raw gfx950 code object (no offload bundle), wrapped into an
+    object file with .incbin (symbols dora_aql_code_object[_end], aql.cpp)."""
+    os.makedirs(OBJ, exist_ok=True)
+    src = os.path.join(CSRC, AQL_KERNELS)
+    co = os.path.join(OBJ, "aql_kernels.co")
+    if _newer(co, [src, *_headers()]):
+        cmd = [HIPCC, "--genco", f"--offload-arch={ARCH}", "--offload-device-only",
+               "--no-gpu-bundle-output", "-O3", "-std=c++17", f"-I{INCLUDE}", f"-I{CSRC}", src,
+               "-o", co]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    asm = os.path.join(OBJ, "aql_blob.S")
+    with open(asm, "w") as f:
+        f.write(".section .rodata\n.p2align 12\n.globl dora_aql_code_object\n"
+                "dora_aql_code_object:\n"
+                f'.incbin "{co}"\n'
+                ".globl dora_aql_code_object_end\ndora_aql_code_object_end:\n"
+                '.section .note.GNU-stack,"",@progbits\n')
+    obj = os.path.join(OBJ, "aql_blob.o")
+    if _newer(obj, [co]):
+        cmd = [HIPCC, "-c", "-x", "assembler-with-cpp", asm, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return obj
+
+
 def build(verbose: bool = False) -> str:
     os.makedirs(LIB, exist_ok=True)
-    objs = _compile_all(LIB_SOURCES, verbose)
+    objs = _compile_all(LIB_SOURCES, verbose) + [_aql_blob(verbose)]
     out = os.path.join(LIB, LIB_NAME)
     if _newer(out, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
-               "-Wl,-soname," + LIB_NAME, "-lpthread", "-lrt"]
+               "-Wl,-soname," + LIB_NAME, "-L/opt/rocm/lib", "-lhsa-runtime64", "-lpthread",
+               "-lrt"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

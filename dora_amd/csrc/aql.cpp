@@ -1,0 +1,351 @@
+// Direct AQL dispatch of signalling packs (see aql.h): one HSA queue per device per process,
+// kernel arguments in a device-memory ring, the pack kernels from the code object embedded in
+// this library (aql_kernels.hip, aql_blob.S).
+#include "aql.h"
+
+#include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+extern "C" const char dora_aql_code_object[];
+extern "C" const char dora_aql_code_object_end[];
+
+namespace dora {
+
+// kernels.hip: the AQL kernels' argument block for `n` segments (<= aql_max_segments()).
+int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
+                   uint8_t* out, size_t cap, uint32_t* grid, int* unroll);
+size_t aql_args_size();
+
+namespace {
+
+constexpr uint32_t kQueuePackets = 4096;
+constexpr uint32_t kRingSlots = 512;
+constexpr uint32_t kSlotBytes = 512;
+constexpr uint32_t kProfileSignals = 4096;
+constexpr uint32_t kProfilePrealloc = 2048;  // created when profiling is first enabled
+
+struct Use {
+  const std::atomic<uint64_t>* flag = nullptr;
+  uint64_t epoch = 0;
+};
+
+}  // namespace
+
+struct AqlQueue {
+  std::mutex mu;
+  hsa_agent_t gpu{};
+  hsa_queue_t* q = nullptr;
+  uint64_t kobj[2] = {0, 0};  // u4, u8
+  uint32_t group[2] = {0, 0}, priv[2] = {0, 0};
+  uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
+  uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
+  uint64_t next = 0;
+  Use uses[kRingSlots];
+  std::atomic<bool> failed{false};
+  bool profiling = false;
+  std::vector<hsa_signal_t> free_sigs, used_sigs;
+  uint64_t ts_freq = 0;
+};
+
+namespace {
+
+struct Agents {
+  uint32_t bdf = 0, domain = 0;
+  hsa_agent_t gpu{}, cpu{};
+  bool gpu_ok = false, cpu_ok = false;
+  hsa_amd_memory_pool_t pool{};
+  bool pool_ok = false, pool_fine = false;
+};
+
+hsa_status_t on_agent(hsa_agent_t a, void* p) {
+  Agents* f = static_cast<Agents*>(p);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_GPU && !f->gpu_ok) {
+    uint32_t bdf = 0, dom = 0;
+    hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+    hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+    if (bdf == f->bdf && dom == f->domain) {
+      f->gpu = a;
+      f->gpu_ok = true;
+    }
+  } else if (t == HSA_DEVICE_TYPE_CPU && !f->cpu_ok) {
+    f->cpu = a;
+    f->cpu_ok = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t on_pool(hsa_amd_memory_pool_t pool, void* p) {
+  Agents* f = static_cast<Agents*>(p);
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  bool alloc = false;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+  if (!alloc) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  const bool fine = flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED;
+  if (!f->pool_ok || (fine && !f->pool_fine)) {
+    f->pool = pool;
+    f->pool_ok = true;
+    f->pool_fine = fine;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
+  const char* m = nullptr;
+  hsa_status_string(st, &m);
+  std::fprintf(stderr, "dora-gpu: AQL pack queue error: %s\n", m ? m : "?");
+  static_cast<AqlQueue*>(data)->failed.store(true);
+}
+
+bool aql_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// Set up the queue of HIP device `device`; nullptr (and a note on stderr when DORA_GPU_TRACE
+// is set) when anything is missing.
+AqlQueue* create(int device) {
+  auto note = [&](const char* what) {
+    if (std::getenv("DORA_GPU_TRACE"))
+      std::fprintf(stderr, "dora-gpu: AQL dispatch off on device %d: %s\n", device, what);
+    return nullptr;
+  };
+  int bus = 0, dev = 0, dom = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
+    return note("PCI location");
+  if (hsa_init() != HSA_STATUS_SUCCESS) return note("hsa_init");
+  Agents f;
+  f.bdf = (uint32_t(bus) << 8) | (uint32_t(dev) << 3);
+  f.domain = uint32_t(dom);
+  hsa_iterate_agents(on_agent, &f);
+  if (!f.gpu_ok || !f.cpu_ok) return note("agent");
+  hsa_amd_agent_iterate_memory_pools(f.gpu, on_pool, &f);
+  if (!f.pool_ok) return note("device memory pool");
+  auto* a = new AqlQueue();
+  a->gpu = f.gpu;
+  hsa_amd_hdp_flush_t hdp{};
+  if (hsa_agent_get_info(f.gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
+                         &hdp) != HSA_STATUS_SUCCESS ||
+      !hdp.HDP_MEM_FLUSH_CNTL) {
+    delete a;
+    return note("HDP flush register");
+  }
+  a->hdp = hdp.HDP_MEM_FLUSH_CNTL;
+  // code object
+  hsa_code_object_reader_t reader;
+  hsa_executable_t exe;
+  const size_t co_size = size_t(dora_aql_code_object_end - dora_aql_code_object);
+  if (hsa_code_object_reader_create_from_memory(dora_aql_code_object, co_size, &reader) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT,
+                                nullptr, &exe) != HSA_STATUS_SUCCESS ||
+      hsa_executable_load_agent_code_object(exe, f.gpu, reader, nullptr, nullptr) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS) {
+    delete a;
+    return note("code object");
+  }
+  const char* names[2] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd"};
+  for (int k = 0; k < 2; ++k) {
+    hsa_executable_symbol_t sym;
+    uint32_t ka = 0;
+    if (hsa_executable_get_symbol_by_name(exe, names[k], &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT,
+                                       &a->kobj[k]) != HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE,
+                                       &ka) != HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE,
+                                       &a->group[k]) != HSA_STATUS_SUCCESS ||
+        hsa_executable_symbol_get_info(
+            sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &a->priv[k]) !=
+            HSA_STATUS_SUCCESS ||
+        ka != aql_args_size() || ka > kSlotBytes) {
+      delete a;
+      return note("kernel symbol / argument size");  // no hidden arguments expected
+    }
+  }
+  // argument ring: device memory the host writes through the BAR
+  void* ring = nullptr;
+  if (hsa_amd_memory_pool_allocate(f.pool, size_t(kRingSlots) * kSlotBytes, 0, &ring) !=
+          HSA_STATUS_SUCCESS ||
+      hsa_amd_agents_allow_access(1, &f.cpu, nullptr, ring) != HSA_STATUS_SUCCESS) {
+    delete a;
+    return note("argument ring");
+  }
+  a->ring = static_cast<uint8_t*>(ring);
+  // every slot starts out as a valid no-op pack (no segments, no flag), made visible with a
+  // read-back once: a dispatch can never see uninitialised arguments
+  std::vector<uint8_t> zero(kSlotBytes, 0);
+  for (uint32_t r = 0; r < kRingSlots; ++r)
+    std::memcpy(a->ring + size_t(r) * kSlotBytes, zero.data(), kSlotBytes);
+  __builtin_ia32_sfence();
+  (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
+  if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
+                       UINT32_MAX, UINT32_MAX, &a->q) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(ring);
+    delete a;
+    return note("queue");
+  }
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &a->ts_freq);
+  return a;
+}
+
+}  // namespace
+
+AqlQueue* aql_queue(int device) {
+  static std::mutex mu;
+  static AqlQueue* queues[64] = {};
+  static bool tried[64] = {};
+  if (!aql_enabled() || device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!tried[device]) {
+    tried[device] = true;
+    queues[device] = create(device);
+  }
+  AqlQueue* q = queues[device];
+  return (q && !q->failed.load()) ? q : nullptr;
+}
+
+size_t aql_max_segments() { return 8; }
+
+int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
+             const std::atomic<uint64_t>* flag_host, bool profile) {
+  if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
+  std::lock_guard<std::mutex> g(a->mu);
+  // the argument slot of the dispatch kRingSlots back must have completed
+  const uint64_t r = a->next % kRingSlots;
+  Use& u = a->uses[r];
+  if (u.flag && u.flag->load(std::memory_order_acquire) < u.epoch) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (u.flag->load(std::memory_order_acquire) < u.epoch) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+        return fail(DORA_ERR_TIMEOUT, "AQL argument slot still in use after 5 s");
+    }
+  }
+  uint8_t args[kSlotBytes];
+  uint32_t grid = 0;
+  int unroll = 4;
+  int rc = build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll);
+  if (rc != DORA_OK) return rc;
+  hsa_signal_t done{0};
+  if (profile && a->profiling) {
+    if (a->free_sigs.empty() && a->used_sigs.size() < kProfileSignals) {
+      hsa_signal_t s;
+      if (hsa_signal_create(1, 0, nullptr, &s) == HSA_STATUS_SUCCESS) a->free_sigs.push_back(s);
+    }
+    if (!a->free_sigs.empty()) {
+      done = a->free_sigs.back();
+      a->free_sigs.pop_back();
+      hsa_signal_store_relaxed(done, 1);
+      a->used_sigs.push_back(done);
+    }
+  }
+  uint8_t* slot = a->ring + r * kSlotBytes;
+  std::memcpy(slot, args, aql_args_size());
+  // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both are
+  // posted writes ordered before the doorbell
+  __builtin_ia32_sfence();
+  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
+  __builtin_ia32_sfence();
+  const uint64_t idx = hsa_queue_add_write_index_relaxed(a->q, 1);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (idx - hsa_queue_load_read_index_scacquire(a->q) >= a->q->size) {
+    __builtin_ia32_pause();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
+  }
+  auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(a->q->base_address) +
+            (idx & (a->q->size - 1));
+  const int k = unroll == 8 ? 1 : 0;
+  p->workgroup_size_x = 256;
+  p->workgroup_size_y = 1;
+  p->workgroup_size_z = 1;
+  p->reserved0 = 0;
+  p->grid_size_x = grid * 256u;
+  p->grid_size_y = 1;
+  p->grid_size_z = 1;
+  p->private_segment_size = a->priv[k];
+  p->group_segment_size = a->group[k];
+  p->kernel_object = a->kobj[k];
+  p->kernarg_address = slot;
+  p->reserved2 = 0;
+  p->completion_signal = done;
+  // agent-scope fences: the pack reads device memory of this GPU and publishes its sample
+  // itself (write-through stores + fill flag); no barrier bit, so packs overlap
+  const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                          (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                          (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
+                   __ATOMIC_RELEASE);
+  hsa_signal_store_relaxed(a->q->doorbell_signal, hsa_signal_value_t(idx));
+  u.flag = flag_host;
+  u.epoch = sig.epoch;
+  ++a->next;
+  return DORA_OK;
+}
+
+int aql_profile_enable(AqlQueue* a, bool on) {
+  if (!a) return DORA_OK;
+  std::lock_guard<std::mutex> g(a->mu);
+  if (hsa_amd_profiling_set_profiler_enabled(a->q, on ? 1 : 0) != HSA_STATUS_SUCCESS)
+    return fail(DORA_ERR_HIP, "hsa_amd_profiling_set_profiler_enabled");
+  // completion signals are created here, not per dispatch inside a timed region
+  while (on && a->free_sigs.size() + a->used_sigs.size() < kProfilePrealloc) {
+    hsa_signal_t s;
+    if (hsa_signal_create(1, 0, nullptr, &s) != HSA_STATUS_SUCCESS) break;
+    a->free_sigs.push_back(s);
+  }
+  a->profiling = on;
+  return DORA_OK;
+}
+
+int aql_profile_take(AqlQueue* a, uint64_t* first_start, uint64_t* last_end, uint64_t* count) {
+  *first_start = *last_end = *count = 0;
+  if (!a) return DORA_OK;
+  std::lock_guard<std::mutex> g(a->mu);
+  const double to_ns = a->ts_freq ? 1e9 / double(a->ts_freq) : 1.0;
+  int rc = DORA_OK;
+  for (hsa_signal_t s : a->used_sigs) {
+    if (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, 10ull * 1000000000ull,
+                                  HSA_WAIT_STATE_ACTIVE) != 0) {
+      rc = fail(DORA_ERR_TIMEOUT, "profiled AQL pack did not complete");
+      continue;
+    }
+    hsa_amd_profiling_dispatch_time_t t{};
+    if (hsa_amd_profiling_get_dispatch_time(a->gpu, s, &t) == HSA_STATUS_SUCCESS) {
+      const uint64_t st = uint64_t(double(t.start) * to_ns), en = uint64_t(double(t.end) * to_ns);
+      if (*count == 0 || st < *first_start) *first_start = st;
+      if (en > *last_end) *last_end = en;
+      ++*count;
+    }
+    a->free_sigs.push_back(s);
+  }
+  a->used_sigs.clear();
+  return rc;
+}
+
+}  // namespace dora

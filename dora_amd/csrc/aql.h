@@ -1,0 +1,43 @@
+// Direct AQL dispatch of signalling packs on a node-owned HSA queue (aql.cpp).
+//
+// hipLaunchKernel costs ~2.5 us of host time per pack (profiles/r01_launch_probe.jsonl): its
+// kernel arguments go to device memory and are made visible with a PCIe read-back, and every
+// dispatch acquires at system scope.  Below ~16 MB a send is bound by that host time.  A node
+// instead writes the pack's arguments into a device-memory ring (write-combined stores, one HDP
+// flush instead of the read-back) and a raw kernel-dispatch packet into its own HSA queue:
+// ~1.5 us per send, agent-scope acquire/release (pack sources are device memory of this GPU;
+// the pack writes its sample through to device scope and signals the fill flag itself), no
+// barrier bit, so consecutive packs overlap (profiles/r01_aql_probe.jsonl).
+#pragma once
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+
+#include "plan.h"
+
+namespace dora {
+
+struct AqlQueue;
+
+// The process's AQL queue for HIP device `device`, created on first use; nullptr when HSA or
+// the code object cannot be set up (callers then launch through HIP).  DORA_GPU_AQL=0 disables.
+AqlQueue* aql_queue(int device);
+
+// Dispatch one signalling pack of `n` (<= 8) device-source copy segments into `dst`; the launch
+// stores `sig.epoch` into `sig.flag` when the sample is complete.  `flag_host` is the host view
+// of that flag (kernarg slots are recycled once the launch that used them has signalled).
+// With `profile`, the packet carries a completion signal whose dispatch times
+// aql_profile_take() reports.
+int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
+             const std::atomic<uint64_t>* flag_host, bool profile);
+
+// Segments one AQL dispatch takes.
+size_t aql_max_segments();
+
+// Enable per-packet timestamps (regions) and collect them: start/end of every profiled dispatch
+// since the last take, in ns, after waiting for them to complete.
+int aql_profile_enable(AqlQueue* q, bool on);
+int aql_profile_take(AqlQueue* q, uint64_t* first_start, uint64_t* last_end, uint64_t* count);
+
+}  // namespace dora

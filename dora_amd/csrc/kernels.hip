@@ -1,13 +1,7 @@
-// HIP kernels of the data plane (gfx950): the batched segmented pack that replaces
-// `copy_array_into_sample` (apis/rust/node/src/node/arrow_utils.rs:23-71), the csum64 parity
-// reduction and the splitmix64 payload generator.
-//
-// Pack = pure HBM streaming: read S bytes + write S bytes, no MFMA, no LDS.  Every chunk of a
-// segment is one 256-thread workgroup.  The destination is written with 16-byte aligned
-// `global_store_dwordx4`; the source is read with 16-byte aligned `global_load_dwordx4` and,
-// when source and destination disagree mod 16 (e.g. C3's x buffer at sample offset 68), two
-// aligned loads are funnel-shifted with v_alignbyte_b32.  The shift is uniform per segment, so
-// the per-segment loop is specialised on it and no lane diverges.
+// HIP kernels of the data plane (gfx950): launches of the batched segmented pack (device code in
+// pack_device.h) that replaces `copy_array_into_sample` (apis/rust/node/src/node/
+// arrow_utils.rs:23-71), the compacting transforms, the csum64 parity reduction and the
+// splitmix64 payload generator.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -21,233 +15,19 @@
 #include <vector>
 
 #include "common.h"
+#include "pack_device.h"
 #include "plan.h"
 
 namespace dora {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kMaxSegs = 32;
-// Workgroups of a signalling pack (r01 sweep, profiles/r01_signal_sweep.jsonl: 1024 beats 512
-// and 2048-4096 at 16-40 MB, flat at 4 MB).
-constexpr uint32_t kSignalGrid = 1024;
-
-
-struct PackSeg {
-  const uint8_t* src;
-  uint64_t dst_off;
-  uint64_t len;
-};
-
-struct PackArgs {
-  uint8_t* dst;
-  uint64_t* flag;        // fill flag to signal at the end (null: none)
-  uint32_t* done;        // per workgroup: epoch (low 32 bits) once its stores are complete
-  uint64_t epoch;
-  uint32_t n_chunks;     // chunks of this launch (>= grid size)
-  uint32_t nseg;
-  uint32_t chunk_bytes;  // multiple of 16
-  uint32_t chunk_end[kMaxSegs];
-  PackSeg seg[kMaxSegs];
-};
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// Memory policy NT: 0 plain, 1 non-temporal loads and stores, 2/3 non-temporal loads and stores
-// written through to device (sc1) / system (sc0 sc1) scope — no L2 write-back needed before a
-// fill signal.
-template <int NT>
-__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-  if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  return *reinterpret_cast<const u32x4*>(p);
-}
-template <int NT>
-__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
-  } else if constexpr (NT == 3) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
-  } else if constexpr (NT == 1) {
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-  } else {
-    *reinterpret_cast<u32x4*>(p) = v;
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
-  if constexpr (NT >= 2) {
-    const uint32_t w = v;
-    asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-  } else {
-    *p = v;
-  }
-}
-
-// Bytes [4Q + b, 4Q + b + 16) of the 32-byte little-endian concatenation lo|hi.
-template <int Q>
-__device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
-  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  u32x4 o;
-  o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], b);
-  o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], b);
-  o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], b);
-  o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], b);
-  return o;
-}
-
-// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned.  U loads of
-// 16 B per lane in flight before the stores.
-template <int U, int NT>
-__device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
-  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) v[u] = ld16<NT>(sp + 16 * i);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16<NT>(dp + 16 * i, v[u]);
-    }
-  }
-}
-
-template <int U, int NT, int Q>
-__device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
-                                             uint64_t nunits) {
-  // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
-  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
-    u32x4 lo[U], hi[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) {
-        lo[u] = ld16<NT>(sbase + 16 * i);
-        hi[u] = ld16<NT>(sbase + 16 * i + 16);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16<NT>(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
-    }
-  }
-}
-
-template <int U, int NT>
-__device__ __forceinline__ void pack_chunk(const PackArgs& args, uint32_t chunk) {
-  uint32_t s = 0;
-  while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
-  const PackSeg sg = args.seg[s];
-  const uint32_t c = chunk - (s ? args.chunk_end[s - 1] : 0u);
-
-  // 16-byte alignment is taken on absolute addresses (the sample base may be unaligned).
-  const uint64_t base = reinterpret_cast<uintptr_t>(args.dst);
-  const uint64_t d0 = sg.dst_off, d1 = sg.dst_off + sg.len;
-  const uint64_t A0 = (base + d0 + 15) & ~uint64_t(15);
-  const uint64_t A1 = (base + d1) & ~uint64_t(15);
-  const uint64_t a0 = A0 - base;
-  const uint64_t a1 = A1 > A0 ? A1 - base : a0;  // body [a0, a1) empty unless A1 > A0
-  uint8_t* const dst = args.dst;
-  const uint8_t* const src = sg.src;  // source byte of sample offset d is src[d - d0]
-
-  if (c == 0) {
-    // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1), byte by byte (< 16 each).
-    const uint64_t hend = a0 < d1 ? a0 : d1;
-    const uint64_t nhead = hend - d0;
-    if (threadIdx.x < nhead) st1<NT>(dst + d0 + threadIdx.x, src[threadIdx.x]);
-    if (a0 < d1) {
-      const uint64_t t0 = a1 > a0 ? a1 : a0;
-      const uint64_t ntail = d1 - t0;
-      if (threadIdx.x >= 64 && threadIdx.x - 64 < ntail) {
-        const uint64_t d = t0 + (threadIdx.x - 64);
-        st1<NT>(dst + d, src[d - d0]);
-      }
-    }
-  }
-  if (a0 >= a1) return;
-  const uint64_t b0 = a0 + uint64_t(c) * args.chunk_bytes;
-  if (b0 >= a1) return;
-  const uint64_t b1 = (a1 - b0) > args.chunk_bytes ? b0 + args.chunk_bytes : a1;
-  const uint64_t nunits = (b1 - b0) >> 4;
-  uint8_t* dp = dst + b0;
-  const uint8_t* sp = src + (b0 - d0);
-  const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
-  if (r == 0) {
-    copy_aligned<U, NT>(dp, sp, nunits);
-    return;
-  }
-  const uint8_t* sbase = sp - r;
-  const uint32_t b = r & 3;
-  switch (r >> 2) {
-    case 0: copy_shifted<U, NT, 0>(dp, sbase, b, nunits); break;
-    case 1: copy_shifted<U, NT, 1>(dp, sbase, b, nunits); break;
-    case 2: copy_shifted<U, NT, 2>(dp, sbase, b, nunits); break;
-    default: copy_shifted<U, NT, 3>(dp, sbase, b, nunits); break;
-  }
-}
-
-// In-kernel fill signal.  A signalling launch writes the sample through to device scope (sc1:
-// no dirty lines left in the per-XCD L2s, so no cache write-back is needed), every workgroup
-// waits for its stores to complete and publishes the epoch in its own done word, and
-// workgroup 0 — dispatched first — polls all done words and then stores the epoch into the
-// host fill flag with a system-scope release.  No same-address atomics (those serialise at
-// ~0.1 us each across XCDs) and no L2 write-back per workgroup (~0.1 us each, serial per
-// XCD): this replaces the stream write-value packet, a ~4 us blit kernel plus a kernel
-// boundary per message on ROCm 7.
-template <int U, int NT>
-__device__ __forceinline__ void signal_fill(const PackArgs& a) {
-  const uint32_t e = static_cast<uint32_t>(a.epoch);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores are complete
-  __syncthreads();
-  if (gridDim.x == 1) {  // nothing to wait for but this workgroup's own stores
-    if (threadIdx.x == 0)
-      __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, e, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x != 0) return;
-  // Poll every done word at once per round (up to kMaxSignalWgs / kThreads = 16 independent
-  // loads in flight per lane), so completion is seen one load round trip after the last
-  // workgroup.  Bounded (~seconds): a lost workgroup must not hang the device; the flag then
-  // stays unset and the receiver reports the fill as failed.
-  constexpr int kPer = kMaxSignalWgs / kThreads;
-  bool ok = false;
-  for (uint32_t round = 0; round < (1u << 22); ++round) {
-    uint32_t v[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = threadIdx.x + k * kThreads;
-      v[k] = i < gridDim.x ? __hip_atomic_load(a.done + i, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : e;
-    }
-    bool mine = true;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) mine &= v[k] == e;
-    if (__syncthreads_and(mine)) {
-      ok = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  // Relaxed: everything this store publishes is already written through (sample stores and done
-  // words are device-scope write-through and complete), and it issues only after every done
-  // word was observed; a release would write back this XCD's whole L2 for nothing.
-  if (threadIdx.x == 0 && ok)
-    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+using namespace pack;
 
 template <int U, int NT>
 __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   // grid = chunks (one chunk per workgroup), or fewer workgroups striding over the chunks when
   // the launch signals its fill (fewer workgroups to count in)
-  for (uint32_t c = blockIdx.x; c < args.n_chunks; c += gridDim.x) pack_chunk<U, NT>(args, c);
-  if constexpr (NT >= 2) signal_fill<U, NT>(args);
+  pack_body<U, NT>(args, blockIdx.x, gridDim.x);
 }
 
 // Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
@@ -500,6 +280,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
       if (grid > cap) grid = cap;
       kern = var.unroll == 8 ? pack_kernel<8, 2> : pack_kernel<4, 2>;
     }
+    a.grid = static_cast<uint32_t>(grid);
     if (ev_start || ev_stop) {
       hipExtLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream,
                             first ? ev_start : nullptr, last ? ev_stop : nullptr, 0, a);
@@ -589,6 +370,51 @@ int launch_pack_wait(const Segment* segs, size_t n, uint8_t* dst, hipStream_t st
     if (*f >= sig.epoch) return DORA_OK;
   }
   DORA_HIP(hipStreamSynchronize(stream));
+  return DORA_OK;
+}
+
+size_t aql_args_size() { return sizeof(AqlPackArgs); }
+
+// Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
+// grid as launch_pack's last launch.
+int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
+                   uint8_t* out, size_t cap, uint32_t* grid_out, int* unroll_out) {
+  if (n == 0 || n > size_t(kMaxAqlSegs)) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
+  if (cap < sizeof(AqlPackArgs)) return fail(DORA_ERR_INVALID, "AQL pack: argument buffer");
+  AqlPackArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.dst = dst;
+  uint64_t body = 0;
+  for (size_t k = 0; k < n; ++k) {
+    if (segs[k].op != SEG_COPY) return fail(DORA_ERR_INVALID, "AQL pack: transform segment");
+    body += segs[k].len;
+  }
+  Variant var = pack_variant();
+  if (var.unroll == 0) var.unroll = (body >= (8u << 20) && body < (32u << 20)) ? 8 : 4;
+  a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
+  uint64_t chunks = 0;
+  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  for (size_t k = 0; k < n; ++k) {
+    const Segment& s = segs[k];
+    a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
+    const uint64_t A0 = (base + s.dst_off + 15) & ~uint64_t(15);
+    const uint64_t A1 = (base + s.dst_off + s.len) & ~uint64_t(15);
+    const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
+    chunks += std::max<uint64_t>(1, (bodyb + a.chunk_bytes - 1) / a.chunk_bytes);
+    if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
+    a.chunk_end[k] = static_cast<uint32_t>(chunks);
+  }
+  a.nseg = static_cast<uint32_t>(n);
+  a.n_chunks = static_cast<uint32_t>(chunks);
+  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
+  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  a.flag = sig.flag;
+  a.done = sig.done;
+  a.epoch = sig.epoch;
+  std::memcpy(out, &a, sizeof(a));
+  *grid_out = a.grid;
+  *unroll_out = var.unroll == 8 ? 8 : 4;
   return DORA_OK;
 }
 

@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "aql.h"
 #include "common.h"
 #include "device_array.h"
 #include "dora_gpu.h"
@@ -99,6 +100,17 @@ bool validity_in_sample() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_VALIDITY");
     return !(e && std::string(e) == "inline");
+  }();
+  return v;
+}
+
+// Packs below this many bytes are dispatched on the process's own AQL queue (aql.h) instead of
+// hipLaunchKernel (DORA_GPU_AQL_MAX_BYTES; DORA_GPU_AQL=0 disables).  Larger packs are
+// GPU-bound and keep the fill streams (3 hardware queues, profiles/r01_stream_probe.jsonl).
+uint64_t aql_max_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_MAX_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(16) << 20;
   }();
   return v;
 }
@@ -186,6 +198,8 @@ struct NodeCore {
   std::vector<uint8_t> fill_dirty;
   hipEvent_t node_ev = nullptr;
   size_t fill_next = 0;
+  // fills dispatched on the AQL queue and not yet seen complete (fence_fills waits for them)
+  std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>> aql_pending;
   RingWriter req;
   RingReader ev;
   RingReader drops;
@@ -279,8 +293,28 @@ struct NodeCore {
     return s;
   }
 
+  const std::atomic<uint64_t>* flag_host(int i) const {
+    return &region->hdr()->nodes[idx].fill[i].epoch;
+  }
+
+  void note_aql_fill(const std::atomic<uint64_t>* f, uint64_t epoch) {
+    if (aql_pending.size() >= 64) {
+      size_t k = 0;
+      for (auto& x : aql_pending)
+        if (x.first->load(std::memory_order_acquire) < x.second) aql_pending[k++] = x;
+      aql_pending.resize(k);
+    }
+    aql_pending.push_back({f, epoch});
+  }
+
   // Order every fill launched so far before work queued on the node stream from now on.
   void fence_fills() {
+    // AQL fills are on no HIP stream: wait for their flags on the host
+    const uint64_t t0 = mono_ns();
+    for (auto& x : aql_pending)
+      while (x.first->load(std::memory_order_acquire) < x.second && mono_ns() - t0 < 10000000000ull)
+        __builtin_ia32_pause();
+    aql_pending.clear();
     for (size_t i = 0; i < fill_streams.size(); ++i) {
       if (!fill_dirty[i]) continue;
       fill_dirty[i] = 0;
@@ -389,6 +423,7 @@ struct dora_node {
   // Timed region (dora_node_region_begin/end): the first pack after begin stamps its start;
   // end records a stop event on every fill stream once the packs queued there have finished.
   bool region_armed = false, region_started = false;
+  uint64_t region_aql = 0;  // packs of the region dispatched on the AQL queue
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
   uint64_t region_packs = 0, region_bytes = 0;
@@ -937,6 +972,24 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     sig.done = n->core->fill_done + size_t(s->slot->flag) * kMaxSignalWgs;
     sp = &sig;
   }
+  if (sp && !st && !t_start && !t_stop && dev == ARROW_DEVICE_ROCM &&
+      nseg <= aql_max_segments() && std::max(s->len, s->ext_len) < aql_max_bytes() &&
+      std::all_of(segs, segs + nseg, [](const Segment& g) { return g.op == SEG_COPY; }) &&
+      hipStreamQuery(n->core->stream) != hipErrorNotReady) {
+    // host-bound size: one raw AQL packet instead of hipLaunchKernel (aql.h)
+    if (AqlQueue* q = aql_queue(n->core->device)) {
+      const std::atomic<uint64_t>* fh = n->core->flag_host(s->slot->flag);
+      if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
+                   n->region_armed) == DORA_OK) {
+        n->core->note_aql_fill(fh, sig.epoch);
+        if (n->region_armed) ++n->region_aql;
+        s->epoch = sig.epoch;
+        s->fill = FILL_FLAG;
+        return DORA_OK;
+      }
+    }
+  }
+  if (!st) st = n->core->next_fill_stream();
   bool signalled = false;
   int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start,
                        t_stop, sp, &signalled);
@@ -1031,8 +1084,8 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       ++n->region_packs;
       n->region_bytes += plan->size;
     }
-    rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
-                     n->core->next_fill_stream(), t_start, t_stop);
+    rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev, nullptr, t_start,
+                     t_stop);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
@@ -1449,7 +1502,14 @@ int dora_node_region_begin(dora_node* n) {
   }
   n->region_armed = true;
   n->region_started = false;
-  n->region_packs = n->region_bytes = 0;
+  n->region_packs = n->region_bytes = n->region_aql = 0;
+  if (dora::AqlQueue* q = dora::aql_queue(n->core->device)) {
+    // AQL packs of the region carry completion signals with dispatch timestamps
+    uint64_t a = 0, b = 0, c = 0;
+    (void)dora::aql_profile_take(q, &a, &b, &c);
+    int rc = dora::aql_profile_enable(q, true);
+    if (rc != DORA_OK) return rc;
+  }
   return DORA_OK;
 }
 
@@ -1460,6 +1520,20 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
   *span_ms = 0;
   if (packs) *packs = n->region_packs;
   if (bytes) *bytes = n->region_bytes;
+  if (dora::AqlQueue* q = dora::aql_queue(n->core->device)) {
+    uint64_t first = 0, last = 0, count = 0;
+    int rc = dora::aql_profile_take(q, &first, &last, &count);
+    (void)dora::aql_profile_enable(q, false);
+    if (rc != DORA_OK) return rc;
+    if (count && n->region_aql) {
+      // packs on the AQL queue: first dispatch start -> last end of their own timestamps (the
+      // region's HIP-launched packs, if any, are not in this span)
+      *span_ms = double(last - first) / 1e6;
+      if (packs) *packs = count;
+      if (bytes && n->region_packs) *bytes = n->region_bytes / n->region_packs * count;
+      return DORA_OK;
+    }
+  }
   if (!n->region_started) return DORA_OK;
   // stop = the end of the last pack on each fill stream (and the node stream)
   std::vector<hipStream_t> ss = n->core->fill_streams;

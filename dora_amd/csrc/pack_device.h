@@ -1,0 +1,262 @@
+// Device code of the pack (replaces `copy_array_into_sample`, apis/rust/node/src/node/
+// arrow_utils.rs:23-71), shared by the HIP-launched kernels (kernels.hip) and the AQL code
+// object dispatched on a node's own HSA queue (aql_kernels.hip, aql.cpp).
+//
+// Pack = pure HBM streaming: read S bytes + write S bytes, no MFMA, no LDS.  Every chunk of a
+// segment is one 256-thread workgroup.  The destination is written with 16-byte aligned
+// `global_store_dwordx4`; the source is read with 16-byte aligned `global_load_dwordx4` and,
+// when source and destination disagree mod 16 (e.g. C3's x buffer at sample offset 68), two
+// aligned loads are funnel-shifted with v_alignbyte_b32.  The shift is uniform per segment, so
+// the per-segment loop is specialised on it and no lane diverges.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "plan.h"
+
+namespace dora {
+namespace pack {
+
+constexpr int kThreads = 256;
+constexpr int kMaxSegs = 32;       // segments of a HIP-launched pack
+constexpr int kMaxAqlSegs = 8;     // segments of an AQL-dispatched pack (smaller kernargs)
+// Workgroups of a signalling pack (r01 sweep, profiles/r01_signal_sweep.jsonl: 1024 beats 512
+// and 2048-4096 at 16-40 MB, flat at 4 MB).
+constexpr uint32_t kSignalGrid = 1024;
+
+struct PackSeg {
+  const uint8_t* src;
+  uint64_t dst_off;
+  uint64_t len;
+};
+
+template <int MAXSEG>
+struct PackArgsT {
+  uint8_t* dst;
+  uint64_t* flag;        // fill flag to signal at the end (null: none)
+  uint32_t* done;        // per workgroup: epoch (low 32 bits) once its stores are complete
+  uint64_t epoch;
+  uint32_t n_chunks;     // chunks of this launch (>= grid size)
+  uint32_t nseg;
+  uint32_t chunk_bytes;  // multiple of 16
+  uint32_t grid;         // workgroups launched (AQL kernels cannot read gridDim)
+  uint32_t chunk_end[MAXSEG];
+  PackSeg seg[MAXSEG];
+};
+using PackArgs = PackArgsT<kMaxSegs>;
+using AqlPackArgs = PackArgsT<kMaxAqlSegs>;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Memory policy NT: 0 plain, 1 non-temporal loads and stores, 2/3 non-temporal loads and stores
+// written through to device (sc1) / system (sc0 sc1) scope — no L2 write-back needed before a
+// fill signal.
+template <int NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return *reinterpret_cast<const u32x4*>(p);
+}
+template <int NT>
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  if constexpr (NT == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (NT == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (NT == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  } else {
+    *reinterpret_cast<u32x4*>(p) = v;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void st1(uint8_t* p, uint8_t v) {
+  if constexpr (NT >= 2) {
+    const uint32_t w = v;
+    asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+  } else {
+    *p = v;
+  }
+}
+
+// Bytes [4Q + b, 4Q + b + 16) of the 32-byte little-endian concatenation lo|hi.
+template <int Q>
+__device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], b);
+  o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], b);
+  o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], b);
+  o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], b);
+  return o;
+}
+
+// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned.  U loads of
+// 16 B per lane in flight before the stores.
+template <int U, int NT>
+__device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) v[u] = ld16<NT>(sp + 16 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) st16<NT>(dp + 16 * i, v[u]);
+    }
+  }
+}
+
+template <int U, int NT, int Q>
+__device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
+                                             uint64_t nunits) {
+  // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
+  for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
+    u32x4 lo[U], hi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) {
+        lo[u] = ld16<NT>(sbase + 16 * i);
+        hi[u] = ld16<NT>(sbase + 16 * i + 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + uint64_t(u) * kThreads;
+      if (i < nunits) st16<NT>(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
+    }
+  }
+}
+
+template <int U, int NT, class A>
+__device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
+  uint32_t s = 0;
+  while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
+  const PackSeg sg = args.seg[s];
+  const uint32_t c = chunk - (s ? args.chunk_end[s - 1] : 0u);
+
+  // 16-byte alignment is taken on absolute addresses (the sample base may be unaligned).
+  const uint64_t base = reinterpret_cast<uintptr_t>(args.dst);
+  const uint64_t d0 = sg.dst_off, d1 = sg.dst_off + sg.len;
+  const uint64_t A0 = (base + d0 + 15) & ~uint64_t(15);
+  const uint64_t A1 = (base + d1) & ~uint64_t(15);
+  const uint64_t a0 = A0 - base;
+  const uint64_t a1 = A1 > A0 ? A1 - base : a0;  // body [a0, a1) empty unless A1 > A0
+  uint8_t* const dst = args.dst;
+  const uint8_t* const src = sg.src;  // source byte of sample offset d is src[d - d0]
+
+  if (c == 0) {
+    // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1), byte by byte (< 16 each).
+    const uint64_t hend = a0 < d1 ? a0 : d1;
+    const uint64_t nhead = hend - d0;
+    if (threadIdx.x < nhead) st1<NT>(dst + d0 + threadIdx.x, src[threadIdx.x]);
+    if (a0 < d1) {
+      const uint64_t t0 = a1 > a0 ? a1 : a0;
+      const uint64_t ntail = d1 - t0;
+      if (threadIdx.x >= 64 && threadIdx.x - 64 < ntail) {
+        const uint64_t d = t0 + (threadIdx.x - 64);
+        st1<NT>(dst + d, src[d - d0]);
+      }
+    }
+  }
+  if (a0 >= a1) return;
+  const uint64_t b0 = a0 + uint64_t(c) * args.chunk_bytes;
+  if (b0 >= a1) return;
+  const uint64_t b1 = (a1 - b0) > args.chunk_bytes ? b0 + args.chunk_bytes : a1;
+  const uint64_t nunits = (b1 - b0) >> 4;
+  uint8_t* dp = dst + b0;
+  const uint8_t* sp = src + (b0 - d0);
+  const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
+  if (r == 0) {
+    copy_aligned<U, NT>(dp, sp, nunits);
+    return;
+  }
+  const uint8_t* sbase = sp - r;
+  const uint32_t b = r & 3;
+  switch (r >> 2) {
+    case 0: copy_shifted<U, NT, 0>(dp, sbase, b, nunits); break;
+    case 1: copy_shifted<U, NT, 1>(dp, sbase, b, nunits); break;
+    case 2: copy_shifted<U, NT, 2>(dp, sbase, b, nunits); break;
+    default: copy_shifted<U, NT, 3>(dp, sbase, b, nunits); break;
+  }
+}
+
+// In-kernel fill signal.  A signalling launch writes the sample through to device scope (sc1:
+// no dirty lines left in the per-XCD L2s, so no cache write-back is needed), every workgroup
+// waits for its stores to complete and publishes the epoch in its own done word, and
+// workgroup 0 — dispatched first — polls all done words and then stores the epoch into the
+// host fill flag with a system-scope release.  No same-address atomics (those serialise at
+// ~0.1 us each across XCDs) and no L2 write-back per workgroup (~0.1 us each, serial per
+// XCD): this replaces the stream write-value packet, a ~4 us blit kernel plus a kernel
+// boundary per message on ROCm 7.
+// `blk`/`nblk`: this workgroup and the launch's workgroup count, passed in so that the AQL
+// kernels need no hidden kernel arguments.
+template <class A>
+__device__ __forceinline__ void signal_fill(const A& a, uint32_t blk, uint32_t nblk) {
+  const uint32_t e = static_cast<uint32_t>(a.epoch);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores are complete
+  __syncthreads();
+  if (nblk == 1) {  // nothing to wait for but this workgroup's own stores
+    if (threadIdx.x == 0)
+      __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.done + blk, e, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+  if (blk != 0) return;
+  // Poll every done word at once per round (up to kMaxSignalWgs / kThreads = 16 independent
+  // loads in flight per lane), so completion is seen one load round trip after the last
+  // workgroup.  Bounded (~seconds): a lost workgroup must not hang the device; the flag then
+  // stays unset and the receiver reports the fill as failed.  The workgroup vote goes through
+  // one LDS word (__syncthreads_and would read the workgroup size from hidden arguments).
+  constexpr int kPer = kMaxSignalWgs / kThreads;
+  __shared__ uint32_t missing;
+  bool ok = false;
+  for (uint32_t round = 0; round < (1u << 22); ++round) {
+    if (threadIdx.x == 0) missing = 0;
+    __syncthreads();
+    uint32_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = threadIdx.x + k * kThreads;
+      v[k] = i < nblk ? __hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : e;
+    }
+    bool mine = true;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) mine &= v[k] == e;
+    if (!mine) missing = 1;
+    __syncthreads();
+    const bool all = missing == 0;
+    __syncthreads();
+    if (all) {
+      ok = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // Relaxed: everything this store publishes is already written through (sample stores and done
+  // words are device-scope write-through and complete), and it issues only after every done
+  // word was observed; a release would write back this XCD's whole L2 for nothing.
+  if (threadIdx.x == 0 && ok)
+    __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A pack launch: its workgroups stride over the chunks; a signalling launch (NT >= 2) then
+// signals the fill flag.
+template <int U, int NT, class A>
+__device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t nblk) {
+  for (uint32_t c = blk; c < args.n_chunks; c += nblk) pack_chunk<U, NT>(args, c);
+  if constexpr (NT >= 2) {
+    if (args.flag) signal_fill(args, blk, nblk);  // all-zero arguments are a no-op
+  }
+}
+
+}  // namespace pack
+}  // namespace dora

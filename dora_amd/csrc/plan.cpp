@@ -559,20 +559,23 @@ int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceTy
     rd.dev = dev;
     rd.defer_validity = validity_in_sample;
     uint64_t next = 0;
+    bool done = false;
     if (dev == ARROW_DEVICE_ROCM) {
       rd.mode = Reader::COLLECT;
-      dora_plan scratch;
-      walk(array, schema, rd, next, scratch.segs, scratch.root);
-      if (!rd.reqs.empty()) {
+      walk(array, schema, rd, next, p->segs, p->root);
+      // no device bytes read (e.g. fixed-width / nested arrays with in-sample validity): the
+      // collecting walk is the plan; otherwise replay it with the gathered bytes
+      done = rd.reqs.empty();
+      if (!done) {
         rd.staged = gather_to_host(rd.reqs, rd.total);
         rd.mode = Reader::REPLAY;
-      } else {
-        rd.mode = Reader::DIRECT;
+        next = 0;
+        rd.deferred.clear();
+        p->segs.clear();
+        p->root = TypeInfoNode();
       }
-      next = 0;
-      rd.deferred.clear();
     }
-    walk(array, schema, rd, next, p->segs, p->root);
+    if (!done) walk(array, schema, rd, next, p->segs, p->root);
     p->size = next;
     if (!rd.deferred.empty()) {
       size_t k = 0;
