@@ -401,6 +401,7 @@ def main():
                 b.free()
 
     # ---- timed region: K back-to-back steps, closed by the sink's ack ----
+    node.set_profiling(False)  # resets the per-phase send timers: they cover the timed steps
     barrier()
     device.set_device(local_rank)
     from dora_amd._lib import call
@@ -419,6 +420,7 @@ def main():
     barrier()
     stats = node.stats()
     stats["send_phase_us"] = {k: round(v, 2) for k, v in node.send_profile().items()}
+    stats["fill_paths"] = node.fill_paths()
     # ---- stamped window (untimed): every pack's own start/stop ----
     intervals = []
     if not args.no_kernel_timing and args.stamp_window > 0:

@@ -115,6 +115,7 @@ _SIGS = {
                                 POINTER(c_uint64)]),
     "dora_node_set_profiling": (c_int, [c_void_p, c_int]),
     "dora_node_set_timing_period": (c_int, [c_void_p, c_uint64]),
+    "dora_node_fill_paths": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_region_begin": (c_int, [c_void_p]),
     "dora_node_region_end": (c_int, [c_void_p, POINTER(c_double), POINTER(c_uint64),
                                      POINTER(c_uint64)]),

@@ -424,6 +424,7 @@ struct dora_node {
   // end records a stop event on every fill stream once the packs queued there have finished.
   bool region_armed = false, region_started = false;
   uint64_t region_aql = 0;  // packs of the region dispatched on the AQL queue
+  uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
   uint64_t region_packs = 0, region_bytes = 0;
@@ -983,6 +984,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
                    n->region_armed) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
+        ++n->aql_packs;
         s->epoch = sig.epoch;
         s->fill = FILL_FLAG;
         return DORA_OK;
@@ -990,6 +992,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     }
   }
   if (!st) st = n->core->next_fill_stream();
+  ++n->hip_packs;
   bool signalled = false;
   int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start,
                        t_stop, sp, &signalled);
@@ -1180,6 +1183,8 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     }
   }
 
+  // the AQL pack queues (aql.h) are set up here, not on the first send
+  if (device >= 0) (void)dora::aql_queue(device);
   auto* n = new dora_node();
   n->core = core;
   n->id = node_id;
@@ -1482,6 +1487,13 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
   if (count) *count = n->pack_count;
   if (total_ms) *total_ms = n->pack_ms;
   if (bytes) *bytes = n->pack_bytes;
+  return DORA_OK;
+}
+
+int dora_node_fill_paths(dora_node* n, uint64_t* aql_packs, uint64_t* hip_packs) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (aql_packs) *aql_packs = n->aql_packs;
+  if (hip_packs) *hip_packs = n->hip_packs;
   return DORA_OK;
 }
 

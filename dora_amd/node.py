@@ -227,6 +227,12 @@ class Node:
     def set_profiling(self, enable: bool = True):
         call("dora_node_set_profiling", self.handle, int(enable))
 
+    def fill_paths(self) -> dict:
+        """Fills by dispatch path: raw AQL packets vs hipLaunchKernel (dora_node_fill_paths)."""
+        a, h = c_uint64(), c_uint64()
+        call("dora_node_fill_paths", self.handle, byref(a), byref(h))
+        return {"aql": a.value, "hip": h.value}
+
     def set_timing_period(self, period: int):
         """Stamp every `period`-th pack launch (0: DORA_GPU_TIMING_SAMPLE, default 8)."""
         call("dora_node_set_timing_period", self.handle, int(period))

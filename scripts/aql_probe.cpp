@@ -179,6 +179,11 @@ int main() {
     return 2;
   }
   // queue and kernarg ring
+  const int nq = std::getenv("Q") ? std::atoi(std::getenv("Q")) : 1;
+  std::vector<hsa_queue_t*> qs(nq);
+  for (int i = 1; i < nq; ++i)
+    HSA(hsa_queue_create(f.gpu, 1024, HSA_QUEUE_TYPE_SINGLE, queue_error, nullptr, UINT32_MAX,
+                         UINT32_MAX, &qs[i]));
   hsa_queue_t* q = nullptr;
   HSA(hsa_queue_create(f.gpu, 1024, HSA_QUEUE_TYPE_SINGLE, queue_error, nullptr, UINT32_MAX,
                        UINT32_MAX, &q));
@@ -256,11 +261,13 @@ int main() {
     a->grid = unsigned(std::min<unsigned long long>(std::max<unsigned long long>(nch, 1), 1024));
     ring_epoch[r] = epoch;
     ring_flag[r] = slot;
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-    while (idx - hsa_queue_load_read_index_relaxed(q) >= q->size) {
+    qs[0] = q;
+    hsa_queue_t* const qq = qs[epoch % nq];
+    const uint64_t idx = hsa_queue_add_write_index_relaxed(qq, 1);
+    while (idx - hsa_queue_load_read_index_relaxed(qq) >= qq->size) {
     }
     hsa_kernel_dispatch_packet_t* p =
-        static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
+        static_cast<hsa_kernel_dispatch_packet_t*>(qq->base_address) + (idx & (qq->size - 1));
     p->workgroup_size_x = 256;
     p->workgroup_size_y = 1;
     p->workgroup_size_z = 1;
@@ -290,7 +297,7 @@ int main() {
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
                      __ATOMIC_RELEASE);
-    hsa_signal_store_relaxed(q->doorbell_signal, idx);
+    hsa_signal_store_relaxed(qq->doorbell_signal, idx);
     return epoch;
   };
   auto wait_flag = [&](int slot, uint64_t e) {
@@ -358,7 +365,7 @@ int main() {
     std::printf("{\"path\": \"aql-%s-f%d\", \"size\": %zu, \"dispatch_host_us_p50\": %.3f, "
                 "\"isolated_flag_latency_us_p50\": %.2f, \"b2b_us_per_msg\": %.3f, "
                 "\"b2b_host_us\": %.3f, \"TBps_2S\": %.3f}\n",
-                hdp ? "devka-hdp" : dev_ka ? "devka" : "hostka", acq2 * 10 + rel, S, host_cost[host_cost.size() / 2], lat[lat.size() / 2], us, hc / N,
+                hdp ? (nq == 1 ? "devka-hdp" : nq == 2 ? "devka-hdp-q2" : "devka-hdp-q3") : dev_ka ? "devka" : "hostka", acq2 * 10 + rel, S, host_cost[host_cost.size() / 2], lat[lat.size() / 2], us, hc / N,
                 2.0 * S / (us * 1e-6) / 1e12);
     std::fflush(stdout);
   }

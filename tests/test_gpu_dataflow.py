@@ -54,6 +54,7 @@ def test_bench_sink_bit_exact_c2(launcher, tmp_path):
                                               {"csum": to_i64(c), "verify": True, "seq": k})
             buf.free()
         stats = node.stats()
+        paths = node.fill_paths()
         node.close()
         codes = df.wait(60)
         log = df.log("sink")
@@ -66,6 +67,8 @@ def test_bench_sink_bit_exact_c2(launcher, tmp_path):
         assert got[size]["verified"] == 5
         assert got[size]["mismatches"] == 0
     assert stats["slots_created"] <= 5 * len(sizes), stats
+    # sizes below 16 MiB went through raw AQL packets, 40.96 MB through hipLaunchKernel
+    assert paths == {"aql": 25, "hip": 5}, paths
 
 
 def test_slots_recycle_through_drop_tokens(launcher, tmp_path):
