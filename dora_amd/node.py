@@ -92,6 +92,21 @@ class _EventHandle:
         self.free()
 
 
+class _Event(dict):
+    """Event dict whose "type_info" (the input's ArrowTypeInfo, reference inline form) is
+    decoded on first access: restoring bitmaps that travelled in the sample's validity tail
+    reads them back from HBM, and a receiver that only uses "value" never pays for it."""
+
+    def __missing__(self, key):
+        if key != "type_info" or "_event" not in self:
+            raise KeyError(key)
+        p, n = ctypes.POINTER(c_uint8)(), c_size_t()
+        call("dora_event_type_info", self["_event"].ptr, byref(p), byref(n))
+        ti = decode(ctypes.string_at(p, n.value))
+        self["type_info"] = ti
+        return ti
+
+
 class Node:
     def __init__(self, node_id: Optional[str] = None, dataflow: Optional[str] = None,
                  device: Optional[int] = None):
@@ -171,7 +186,7 @@ class Node:
         if kind == "ALL_INPUTS_CLOSED":
             ev.free()
             return None
-        out = {"type": kind, "id": self._lib.dora_event_id(ev.ptr).decode()}
+        out = _Event(type=kind, id=self._lib.dora_event_id(ev.ptr).decode())
         if kind == "ERROR":
             out["error"] = self._lib.dora_event_error(ev.ptr).decode()
         if kind == "INPUT":
@@ -179,16 +194,14 @@ class Node:
             call("dora_event_parameters", ev.ptr, byref(p), byref(n))
             out["metadata"] = decode_parameters(ctypes.string_at(p, n.value) if n.value else b"")
             out["timestamp_ns"] = self._lib.dora_event_timestamp_ns(ev.ptr)
-            call("dora_event_type_info", ev.ptr, byref(p), byref(n))
-            ti = decode(ctypes.string_at(p, n.value))
-            out["type_info"] = ti
+            out["_event"] = ev  # "type_info" is decoded on first access (_Event)
             dp, dn = c_void_p(), c_size_t()
             call("dora_event_data", ev.ptr, byref(dp), byref(dn))
             out["data_ptr"], out["data_len"] = dp.value, dn.value
             out["on_device"] = bool(self._lib.dora_event_is_device(ev.ptr))
             if dn.value == 0:       # RawData::Vec(empty) -> ArrayData::new_empty(data_type)
                 import pyarrow as pa
-                out["value"] = pa.array([], type=ti.arrow_type())
+                out["value"] = pa.array([], type=out["type_info"].arrow_type())
             elif out["on_device"]:
                 a, s = ArrowArray(), ArrowSchema()
                 call("dora_event_array", ev.ptr, byref(a), byref(s))

@@ -109,3 +109,27 @@ def test_decode_rejects_truncated():
     assert decode(raw).data_type == "+l[item:!i]"
     with pytest.raises(ValueError):
         decode(raw[:-3])
+
+
+def test_type_info_validity_tag_2_decodes():
+    """Validity tag 2 (bitmap in the sample's validity tail, node sends of device arrays): the
+    Python decoder reads (offset, len) in place of the inline bytes; everything else of the
+    serialized ArrowTypeInfo is unchanged."""
+    import struct
+    arr = pa.array([1, None, 3, None, 5], type=pa.int32())
+    with Plan.of(arr) as p:
+        raw = p.type_info().raw
+    slen = struct.unpack_from("<I", raw, 0)[0]
+    tag_at = 4 + slen + 16
+    assert raw[tag_at] == 1
+    vlen = struct.unpack_from("<Q", raw, tag_at + 1)[0]
+    rest = raw[tag_at + 1 + 8 + vlen:]
+    tagged = raw[:tag_at] + bytes([2]) + struct.pack("<QQ", 64, vlen) + rest
+    a, b = decode(raw), decode(tagged)
+    assert a.validity is not None and a.validity_in_sample is None
+    assert b.validity is None and b.validity_in_sample == (64, vlen)
+    ja, jb = a.to_json(), b.to_json()
+    ja.pop("validity"), jb.pop("validity")
+    assert ja == jb
+    with pytest.raises(ValueError):
+        decode(raw[:tag_at] + bytes([3]) + raw[tag_at + 1:])
