@@ -70,6 +70,7 @@ struct Agents {
   uint32_t bdf = 0, domain = 0;
   hsa_agent_t gpu{}, cpu{};
   bool gpu_ok = false, cpu_ok = false;
+  int matches = 0;  // GPU agents at this PCI location (> 1: a partitioned GPU)
   hsa_amd_memory_pool_t pool{};
   bool pool_ok = false, pool_fine = false;
 };
@@ -79,13 +80,14 @@ hsa_status_t on_agent(hsa_agent_t a, void* p) {
   hsa_device_type_t t;
   if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS)
     return HSA_STATUS_SUCCESS;
-  if (t == HSA_DEVICE_TYPE_GPU && !f->gpu_ok) {
+  if (t == HSA_DEVICE_TYPE_GPU) {
     uint32_t bdf = 0, dom = 0;
     hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
     hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
     if (bdf == f->bdf && dom == f->domain) {
       f->gpu = a;
       f->gpu_ok = true;
+      ++f->matches;
     }
   } else if (t == HSA_DEVICE_TYPE_CPU && !f->cpu_ok) {
     f->cpu = a;
@@ -147,6 +149,8 @@ AqlQueue* create(int device) {
   f.domain = uint32_t(dom);
   hsa_iterate_agents(on_agent, &f);
   if (!f.gpu_ok || !f.cpu_ok) return note("agent");
+  // a partitioned GPU (several agents at one PCI location) cannot be told apart here
+  if (f.matches != 1) return note("several GPU agents at the device's PCI location");
   hsa_amd_agent_iterate_memory_pools(f.gpu, on_pool, &f);
   if (!f.pool_ok) return note("device memory pool");
   auto* a = new AqlQueue();
