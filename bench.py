@@ -226,6 +226,39 @@ def run_cross_gpu(n_gpus, launcher, timeout=240.0, runs=None, **desc_kw):
     return out
 
 
+NATIVE_SIZES = [4096, 65536, 1 << 20, 4096000, 16 << 20, 40960000]
+
+
+def run_native_ladder(launcher, gpu, n=1000, timeout=120.0):
+    """Throughput mode of the native benchmark node (dora-gpu-bench-source -> -sink, one GPU,
+    zero-copy edge) per size: the data plane through its C ABI, as a Rust node would bind it,
+    without the Python node's per-send cost.  Reported, never raised."""
+    from dora_amd.dataflow import Dataflow
+    out = {}
+    for size in NATIVE_SIZES:
+        tmp = tempfile.mkdtemp(prefix="dora-native-")
+        try:
+            desc = c4_descriptor(2, tmp, "kernel", tp_n=n, gpu=lambda g: gpu)
+            desc["nodes"][0]["env"].update({
+                "DORA_BENCH_TP_SIZE": str(size), "DORA_BENCH_LAT_SIZES": str(size),
+                "DORA_BENCH_LAT_N": "5", "DORA_BENCH_LAT_GAP_US": "1000"})
+            df = Dataflow(desc, launcher=launcher).start()
+            try:
+                codes = df.wait(timeout)
+            finally:
+                df.stop()
+            r = _load(os.path.join(tmp, "source.json")) or {}
+            gbps = r.get("tp_delivered_GBps")
+            out[str(size)] = {"GBps": gbps, "msgs": n,
+                              "us_per_msg": round(size / (gbps * 1e3), 3) if gbps else None,
+                              "hbm_frac_2S": round(2 * gbps / HBM_PEAK_GBPS, 4) if gbps else None,
+                              "send_phase_us": r.get("send_phase_us"), "ok": r.get("ok"),
+                              "exit_codes": codes}
+        except Exception as e:  # noqa: BLE001 — reported in the JSON line
+            out[str(size)] = {"error": repr(e)}
+    return out
+
+
 def summarize_cross(name, src, sinks, codes, logs):
     lat, verified, mismatches, dropped, errors = {}, 0, 0, 0, 0
     for sname, r in sinks.items():
@@ -269,9 +302,12 @@ def main():
         base = cpu_baseline(affinity)
 
     launcher = None
-    if world > 1 and rank == 0 and not args.no_cross_gpu:
+    native_ladder = (world == 1 and rank == 0 and not args.no_ladder and args.tp_n > 0
+                     and args.workload == "c2")
+    if (world > 1 and rank == 0 and not args.no_cross_gpu) or native_ladder:
         from dora_amd.launcher import Launcher
-        launcher = Launcher()  # spawns the cross-GPU stages after this process touched HIP
+        # spawns the cross-GPU stages / native ladder nodes after this process touched HIP
+        launcher = Launcher()
 
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
@@ -442,8 +478,12 @@ def main():
     t_max = max_over_ranks(elapsed)
     total_bytes = sum_over_ranks(float(args.steps * S))
     cross = None
+    native = None
     if launcher is not None:
-        cross = run_cross_gpu(world, launcher)
+        if world > 1:
+            cross = run_cross_gpu(world, launcher)
+        if native_ladder:
+            native = run_native_ladder(launcher, local_rank)
         launcher.close()
     barrier()
     value = total_bytes / t_max / 1e9
@@ -490,6 +530,7 @@ def main():
                    "sources_rotated": nsrc},
         "latency_us": lat,
         "throughput_per_size": tp_ladder,
+        "throughput_per_size_native": native,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic[1] if traffic else None,
