@@ -93,12 +93,13 @@ _SIGS = {
     "dora_sample_data": (c_void_p, [c_void_p]),
     "dora_sample_len": (c_size_t, [c_void_p]),
     "dora_sample_discard": (None, [c_void_p, c_void_p]),
-    "dora_node_send_output_sample": (c_int, [c_void_p, c_char_p, POINTER(c_uint8), c_size_t,
-                                             POINTER(c_uint8), c_size_t, c_void_p]),
+    # parameter / type-info byte strings go in as c_char_p (bytes objects, no copy)
+    "dora_node_send_output_sample": (c_int, [c_void_p, c_char_p, c_char_p, c_size_t,
+                                             c_char_p, c_size_t, c_void_p]),
     "dora_node_send_output": (c_int, [c_void_p, c_char_p, POINTER(ArrowArray),
-                                      POINTER(ArrowSchema), c_int32, POINTER(c_uint8), c_size_t]),
+                                      POINTER(ArrowSchema), c_int32, c_char_p, c_size_t]),
     "dora_node_send_output_bytes": (c_int, [c_void_p, c_char_p, c_void_p, c_size_t, c_int32,
-                                            POINTER(c_uint8), c_size_t]),
+                                            c_char_p, c_size_t]),
     "dora_node_close_outputs": (c_int, [c_void_p, POINTER(c_char_p), c_size_t]),
     "dora_node_next_event": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
     "dora_event_type": (c_int, [c_void_p]),
@@ -122,7 +123,7 @@ _SIGS = {
     "dora_node_pack_intervals": (c_int, [c_void_p, POINTER(c_double), c_size_t,
                                          POINTER(c_size_t)]),
     "dora_node_peer_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
-    "dora_node_forward": (c_int, [c_void_p, c_char_p, c_void_p, c_void_p, c_size_t]),
+    "dora_node_forward": (c_int, [c_void_p, c_char_p, c_void_p, c_char_p, c_size_t]),
     "dora_node_send_profile": (c_int, [c_void_p, POINTER(c_double), c_size_t, POINTER(c_uint64)]),
     "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),
                                      POINTER(c_uint64)]),

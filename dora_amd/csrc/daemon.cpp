@@ -87,7 +87,15 @@ class Daemon {
     uint64_t last_liveness = 0;
     std::vector<uint8_t> payload;
     RegionHdr* h = region_->hdr();
+    bool placed = false;
     for (;;) {
+      if (!placed) {  // move next to the GPU of the first node that started (numa_hint)
+        const int32_t numa = h->numa_hint.load(std::memory_order_relaxed);
+        if (numa >= 0) {
+          placed = true;
+          (void)pin_to_numa(numa);
+        }
+      }
       bool work = false;
       for (size_t i = 0; i < nodes_.size(); ++i) {
         uint32_t kind;

@@ -115,6 +115,28 @@ uint64_t aql_max_bytes() {
   return v;
 }
 
+bool numa_pinning() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_PIN");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// NUMA node of HIP device `device` (sysfs of its PCI function), -1 when unknown.
+int gpu_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  for (char* p = bus; *p; ++p) *p = char(std::tolower(*p));
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return -1;
+  int numa = -1;
+  if (std::fscanf(f, "%d", &numa) != 1) numa = -1;
+  std::fclose(f);
+  return numa;
+}
+
 uint64_t timing_sample() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_TIMING_SAMPLE");
@@ -774,15 +796,16 @@ void drain_events(dora_node* n) {
   if (got) drop_oldest_inputs(n);
 }
 
-std::vector<uint8_t> encode_metadata(const std::vector<uint8_t>& ti, const uint8_t* params,
-                                     size_t params_len, uint64_t ts) {
-  Metadata m;
-  m.timestamp_ns = ts;
-  m.type_info = ti;
-  if (params && params_len) m.parameters.assign(params, params + params_len);
-  WBuf w;
-  w.metadata(m);
-  return w.b;
+// The Metadata of a send as WBuf::bytes(WBuf::metadata(m)) would write it, straight into `w`
+// (no Metadata copy of the type info and parameters per send).
+void put_metadata(WBuf& w, const std::vector<uint8_t>& ti, const uint8_t* params,
+                  size_t params_len, uint64_t ts) {
+  const uint64_t n = 2 + 8 + 8 + ti.size() + 8 + (params ? params_len : 0);
+  w.u64(n);
+  w.u16(0);  // metadata version
+  w.u64(ts);
+  w.bytes(ti.data(), ti.size());
+  w.bytes(params, params ? params_len : 0);
 }
 
 int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
@@ -825,8 +848,9 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     delete sample;
   }
   WBuf w;
+  w.b.reserve(256 + ti.size() + params_len);
   w.str(output_id);
-  w.bytes(encode_metadata(ti, params, params_len, ts));
+  put_metadata(w, ti, params, params_len, ts);
   w.data(d);
   int rc = n->core->request(REQ_SEND_MESSAGE, w.b);
   if (rc != DORA_OK) {
@@ -1148,6 +1172,17 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   dora::trace_set_name(node_id);
   if (device >= 0) {  // device < 0: host-only node (control plane + inline Vec samples only)
     DORA_HIP(hipSetDevice(device));
+    // NUMA placement: the send/receive path writes the GPU's BAR (AQL arguments, doorbells)
+    // and polls host memory the GPU writes (fill flags); keep this thread next to its GPU and
+    // tell the daemon where that is (DORA_GPU_PIN=0: leave the affinity alone)
+    if (dora::numa_pinning()) {
+      const int numa = dora::gpu_numa_node(device);
+      if (numa >= 0) {
+        (void)dora::pin_to_numa(numa);
+        int32_t none = -1;
+        core->region->hdr()->numa_hint.compare_exchange_strong(none, numa);
+      }
+    }
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
     if (dora::fill_stream_count() > 1 && dora::async_sends()) {
       DORA_HIP(hipEventCreateWithFlags(&core->node_ev, hipEventDisableTiming));

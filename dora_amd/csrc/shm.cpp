@@ -3,6 +3,7 @@
 
 #include <fcntl.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -10,6 +11,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -43,6 +45,35 @@ uint64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+bool pin_to_numa(int numa) {
+  if (numa < 0) return false;
+  char path[96];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", numa);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[4096];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  cpu_set_t want, cur;
+  CPU_ZERO(&want);
+  for (char* p = buf; *p;) {  // "0-63,128-191"
+    char* end = nullptr;
+    const long a = std::strtol(p, &end, 10);
+    if (end == p) break;
+    long b = a;
+    p = end;
+    if (*p == '-') b = std::strtol(p + 1, &p, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(int(c), &want);
+    while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+  }
+  if (sched_getaffinity(0, sizeof(cur), &cur) != 0) return false;
+  cpu_set_t both;
+  CPU_AND(&both, &want, &cur);
+  if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return false;
+  return sched_setaffinity(0, sizeof(both), &both) == 0;
 }
 
 int64_t spin_budget_us() {
@@ -108,6 +139,7 @@ Region* Region::create(const std::string& name, const std::vector<std::string>& 
   std::memset(static_cast<void*>(h), 0, sizeof(RegionHdr));
   h->version = kRegionVersion;
   h->n_nodes = static_cast<uint32_t>(node_ids.size());
+  h->numa_hint.store(-1);
   h->ring_cap = ring_cap;
   h->total_size = total;
   new (&h->doorbell) std::atomic<uint32_t>(0);

@@ -20,7 +20,7 @@
 namespace dora {
 
 constexpr uint64_t kRegionMagic = 0x444f5241474d5358ull;  // "DORAGMSX"
-constexpr uint32_t kRegionVersion = 1;
+constexpr uint32_t kRegionVersion = 2;
 constexpr uint32_t kMaxNodes = 64;
 constexpr size_t kIdLen = 64;
 
@@ -64,6 +64,8 @@ struct RegionHdr {
   alignas(64) std::atomic<uint32_t> doorbell;  // futex word the daemon sleeps on
   std::atomic<uint32_t> daemon_sleeping;
   std::atomic<uint32_t> shutdown;
+  // NUMA node of the first GPU node to start (-1: none yet): the daemon moves next to it
+  std::atomic<int32_t> numa_hint;
   char dataflow_id[kIdLen];
   NodeEntry nodes[kMaxNodes];
 };
@@ -130,5 +132,8 @@ void futex_wake(std::atomic<uint32_t>* w);
 int64_t spin_budget_us();
 uint64_t now_ns();           // CLOCK_REALTIME (timestamps that cross processes)
 uint64_t mono_ns();          // CLOCK_MONOTONIC
+// Restrict the calling thread (and threads it starts later) to the CPUs of NUMA node `numa`
+// within its current affinity; false when that would leave none or changes nothing.
+bool pin_to_numa(int numa);
 
 }  // namespace dora
