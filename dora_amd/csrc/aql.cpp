@@ -247,6 +247,22 @@ AqlQueue* aql_queue(int device) {
 
 size_t aql_max_segments() { return 8; }
 
+void aql_forget_flags(int device, const void* base, size_t size) {
+  AqlQueue* a = aql_queue(device);
+  if (!a) return;
+  std::lock_guard<std::mutex> g(a->mu);
+  const auto* lo = static_cast<const uint8_t*>(base);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (Use& u : a->uses) {
+    const auto* f = reinterpret_cast<const uint8_t*>(u.flag);
+    if (!u.flag || f < lo || f >= lo + size) continue;
+    while (u.flag->load(std::memory_order_acquire) < u.epoch &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+      __builtin_ia32_pause();
+    u.flag = nullptr;  // the slot is free; the flag's region goes away
+  }
+}
+
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");

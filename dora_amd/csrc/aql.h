@@ -32,6 +32,10 @@ AqlQueue* aql_queue(int device);
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile);
 
+// Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
+// region about to be unmapped), after waiting (bounded) for those fills to signal.
+void aql_forget_flags(int device, const void* base, size_t size);
+
 // Segments one AQL dispatch takes.
 size_t aql_max_segments();
 

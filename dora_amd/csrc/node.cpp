@@ -348,6 +348,8 @@ struct NodeCore {
   }
 
   ~NodeCore() {
+    // AQL argument slots must not keep pointing at this region's fill flags once it is unmapped
+    if (device >= 0 && region) aql_forget_flags(device, region->base(), region->size());
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
     for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
     for (hipStream_t s : fill_streams) {

@@ -1,8 +1,13 @@
 // Runtime plumbing of the C ABI: errors, devices, streams, events, memory.
 #include <hip/hip_runtime_api.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -27,6 +32,38 @@ int fail(int code, const char* fmt, ...) {
 }
 
 void clear_error() { std::strcpy(g_last_error, "no error"); }
+
+namespace {
+
+struct sigaction g_prev_segv;
+
+void on_segv(int sig, siginfo_t* info, void* ctx) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  char head[128];
+  const int k = std::snprintf(head, sizeof(head), "dora-gpu: signal %d at address %p, backtrace:\n",
+                              sig, info ? info->si_addr : nullptr);
+  if (k > 0) (void)!write(2, head, size_t(k));
+  backtrace_symbols_fd(frames, n, 2);
+  sigaction(SIGSEGV, &g_prev_segv, nullptr);  // then whatever handled it before (faulthandler)
+  raise(sig);
+}
+
+// DORA_GPU_SEGV_TRACE=1: print a native backtrace on SIGSEGV (debugging aid on the GPU box,
+// where no debugger may attach).
+struct SegvTrace {
+  SegvTrace() {
+    const char* e = std::getenv("DORA_GPU_SEGV_TRACE");
+    if (!e || *e != '1') return;
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = on_segv;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+  }
+} g_segv_trace;
+
+}  // namespace
 
 }  // namespace dora
 

@@ -137,6 +137,97 @@ def test_python_receiver_c3_point_clouds(launcher):
     assert results[0]["arrow_equal_len"] == 4
 
 
+@pytest.mark.parametrize("peer_copy", ["kernel", "sdma"])
+def test_c3_validity_tail_through_pulls_and_relay(launcher, peer_copy):
+    """Point clouds (validity in the sample's tail) through a relay and a receiver with the
+    cross-GPU pull path forced (DORA_GPU_EDGE_COPY=1): every pull and the relay's forward move
+    the tail with the sample (ext_len), and the receiver's inline ArrowTypeInfo — restored from
+    its local copy — checksums to the oracle's regions."""
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from dora_amd.verify import to_u64
+    from dora_amd.workloads import point_cloud
+    from oracle.arrow_ffi import import_array
+    from oracle.checksum_ref import regions_csum
+    from oracle.pack_ref import node_regions
+    env = {"DORA_GPU_EDGE_COPY": "1", "DORA_GPU_PEER_COPY": peer_copy}
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["pc"], "inputs": {"result": "recv/result"}},
+        {"id": "relay", "path": "dora-gpu-relay", "outputs": ["pc"], "env": env,
+         "inputs": {"pc": {"source": "src/pc", "queue_size": 100}}},
+        {"id": "recv", "path": sys.executable, "env": env,
+         "args": [os.path.join(ROOT, "examples", "verify_receiver.py")],
+         "inputs": {"pc": {"source": "relay/pc", "queue_size": 100}}, "outputs": ["result"]},
+    ]}
+    clouds = [point_cloud(37, 4, 7), point_cloud(20000, 16, 11), point_cloud(300000, 16, 3)]
+    with Dataflow(desc, launcher=launcher) as df:
+        node = Node("src", dataflow=df.shm, device=0)
+        want = []
+        for seq, pc in enumerate(clouds):
+            want.append(regions_csum(node_regions(import_array(pc))))
+            with DeviceArray.from_pyarrow(pc) as da:
+                node.send_output("pc", da, {"seq": seq})
+        results = {}
+        deadline = time.time() + 120
+        while len(results) < len(clouds) and time.time() < deadline:
+            ev = node.next(timeout=5)
+            if ev is None:
+                break
+            if ev["type"] == "INPUT":
+                results[ev["metadata"]["seq"]] = ev["metadata"]
+        node.close()
+        codes = df.wait(60)
+        log = df.log("recv") + df.log("relay")
+    assert codes["recv"] == 0 and codes["relay"] == 0, log
+    for seq in range(len(clouds)):
+        assert to_u64(results[seq]["csum"]) == want[seq], seq
+    assert results[0]["arrow_equal_len"] == 4
+
+
+def test_many_small_sends_bit_exact(launcher, tmp_path):
+    """More sends than the AQL argument ring holds (512 slots): every argument slot is reused
+    after its launch signalled; 1200 messages of odd sizes from unaligned sources, each
+    checksummed by the sink."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    sizes = [4096, 5003, 65537, 262139]
+    n_msgs = 1200
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        s = device.Stream()
+        srcs = []
+        for k in range(3):
+            b = device.DeviceBuffer(262139 + 64)
+            device.fill_splitmix(b.ptr, b.size, 0x5EED + k, s)
+            srcs.append(b)
+        s.sync()
+        sums = {}
+        for i in range(n_msgs):
+            key = (i % 3, (5 * i) % 13, sizes[i % len(sizes)])
+            if key not in sums:
+                b = srcs[key[0]]
+                sums[key] = device.csum64(b.ptr + key[1], key[2], s)
+            b = srcs[key[0]]
+            node.send_output_device_bytes("data", b.ptr + key[1], key[2],
+                                          {"csum": to_i64(sums[key]), "verify": True, "seq": i})
+        paths = node.fill_paths()
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+        for b in srcs:
+            b.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(x["verified"] for x in out["series"]) == n_msgs
+    assert sum(x["mismatches"] for x in out["series"]) == 0
+    assert paths["aql"] == n_msgs, paths
+
+
 def test_host_pyarrow_send_to_device_receiver(launcher):
     """A Python node sending a host pyarrow array (reference Python path) -> device sample."""
     import pyarrow as pa
