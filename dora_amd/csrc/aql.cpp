@@ -305,8 +305,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both are
   // posted writes ordered before the doorbell
   __builtin_ia32_sfence();
-  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
-  __builtin_ia32_sfence();
+  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
   hsa_queue_t* const q = a->qs[a->next % uint64_t(a->nq)];
   const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
   const auto t0 = std::chrono::steady_clock::now();

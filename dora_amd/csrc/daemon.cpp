@@ -123,6 +123,7 @@ class Daemon {
         continue;
       }
       h->daemon_sleeping.store(1, std::memory_order_seq_cst);
+      std::atomic_thread_fence(std::memory_order_seq_cst);  // pairs with ring_doorbell's fence
       const uint32_t bell = h->doorbell.load(std::memory_order_seq_cst);
       bool empty = true;
       for (auto& r : req_) empty &= r.empty();

@@ -104,13 +104,14 @@ bool validity_in_sample() {
   return v;
 }
 
-// Packs below this many bytes are dispatched on the process's own AQL queue (aql.h) instead of
-// hipLaunchKernel (DORA_GPU_AQL_MAX_BYTES; DORA_GPU_AQL=0 disables).  Larger packs are
-// GPU-bound and keep the fill streams (3 hardware queues, profiles/r01_stream_probe.jsonl).
+// Packs below this many bytes (32 MiB) are dispatched on the process's own AQL queues (aql.h)
+// instead of hipLaunchKernel (DORA_GPU_AQL_MAX_BYTES; DORA_GPU_AQL=0 disables).  Larger packs
+// are GPU-bound and keep the fill streams (3 hardware queues; 40.96 MB: 13.2 us per pack there
+// vs 13.4 on two AQL queues, 16 MB: 6.0 vs 5.7, profiles/r01_stream_probe.jsonl, r01_aql_probe).
 uint64_t aql_max_bytes() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_MAX_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(16) << 20;
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
   }();
   return v;
 }
@@ -276,9 +277,15 @@ struct NodeCore {
   }
 
   void ring_doorbell() {
+    // the daemon sets `daemon_sleeping` before it reads the doorbell and re-checks the rings;
+    // the fence orders the request's head store before our load of the flag (shm.cpp's ring
+    // wake-up argument), so the doorbell is only bumped for a sleeping daemon
     RegionHdr* h = region->hdr();
-    h->doorbell.fetch_add(1, std::memory_order_seq_cst);
-    if (h->daemon_sleeping.load(std::memory_order_seq_cst)) futex_wake(&h->doorbell);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (h->daemon_sleeping.load(std::memory_order_relaxed)) {
+      h->doorbell.fetch_add(1, std::memory_order_seq_cst);
+      futex_wake(&h->doorbell);
+    }
   }
 
   int request(uint32_t kind, const std::vector<uint8_t>& payload) {

@@ -225,8 +225,14 @@ bool RingWriter::try_push(uint32_t kind, const uint8_t* payload, size_t n) {
   std::memcpy(data + off + 8, &n64, 8);
   if (n) std::memcpy(data + off + 16, payload, n);
   h_->head.store(head + rec, std::memory_order_release);
-  h_->seq.fetch_add(1, std::memory_order_seq_cst);
-  if (h_->waiters.load(std::memory_order_seq_cst)) futex_wake(&h_->seq);
+  // Wake only a reader that sleeps: it announces itself in `waiters` before it reads `seq` and
+  // re-checks for data, and the fence orders our head store before the `waiters` load, so
+  // either we see it or it sees the record (no seq bump, no shared RMW, on the common path).
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (h_->waiters.load(std::memory_order_relaxed)) {
+    h_->seq.fetch_add(1, std::memory_order_seq_cst);
+    futex_wake(&h_->seq);
+  }
   return true;
 }
 

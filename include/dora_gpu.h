@@ -296,7 +296,7 @@ int dora_node_forward(dora_node* node, const char* output_id, const dora_event* 
 int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs);
 /* Fills (packs of sends) by dispatch path: raw AQL packets on the process's HSA queue (device
- * sources below DORA_GPU_AQL_MAX_BYTES, default 16 MiB, <= 8 segments) or hipLaunchKernel on
+ * sources below DORA_GPU_AQL_MAX_BYTES, default 32 MiB, <= 8 segments) or hipLaunchKernel on
  * the node's fill streams (larger, host sources, compacting transforms, relays). */
 int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_packs);
 /* Cross-GPU edges: an input whose slot lives on another GPU is pulled over xGMI

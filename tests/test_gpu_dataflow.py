@@ -67,8 +67,11 @@ def test_bench_sink_bit_exact_c2(launcher, tmp_path):
         assert got[size]["verified"] == 5
         assert got[size]["mismatches"] == 0
     assert stats["slots_created"] <= 5 * len(sizes), stats
-    # sizes below 16 MiB went through raw AQL packets, 40.96 MB through hipLaunchKernel
-    assert paths == {"aql": 25, "hip": 5}, paths
+    # sizes below 32 MiB went through raw AQL packets, 40.96 MB through hipLaunchKernel
+    if os.environ.get("DORA_GPU_AQL", "1") != "0":
+        assert paths == {"aql": 25, "hip": 5}, paths  # 40.96 MB: fill streams
+    else:
+        assert paths == {"aql": 0, "hip": 30}, paths
 
 
 def test_slots_recycle_through_drop_tokens(launcher, tmp_path):
@@ -225,7 +228,8 @@ def test_many_small_sends_bit_exact(launcher, tmp_path):
     assert out["errors"] == 0
     assert sum(x["verified"] for x in out["series"]) == n_msgs
     assert sum(x["mismatches"] for x in out["series"]) == 0
-    assert paths["aql"] == n_msgs, paths
+    if os.environ.get("DORA_GPU_AQL", "1") != "0":
+        assert paths["aql"] == n_msgs, paths
 
 
 def test_host_pyarrow_send_to_device_receiver(launcher):
