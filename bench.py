@@ -128,8 +128,8 @@ def cpu_baseline(rank_cores):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     cores = ",".join(str(c) for c in rank_cores[:3])
     sizes = "4096,40960,409600,4096000,40960000"
-    out = subprocess.run([exe, "--sizes", sizes, "--lat-n", "20", "--lat-gap-us", "10000",
-                          "--tp-n", "40", "--cores", cores], capture_output=True, text=True,
+    out = subprocess.run([exe, "--sizes", sizes, "--lat-n", "100", "--lat-gap-us", "10000",
+                          "--tp-n", "200", "--cores", cores], capture_output=True, text=True,
                          timeout=300, check=True).stdout
     return json.loads(out)
 
@@ -294,6 +294,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # DORA_BENCH_GPUS=k: rehearsal on a k-GPU box (rank / stage g runs on GPU g % k); unset on
+    # the real node, where every rank and cross-GPU stage has a GPU of its own
+    vis = int(os.environ.get("DORA_BENCH_GPUS", "0"))
+    gpu_of = (lambda g: g % vis) if vis > 0 else (lambda g: g)
+    local_rank = gpu_of(local_rank)
     affinity = sorted(os.sched_getaffinity(0))
 
     # ---- CPU-only work and process spawning first: nothing below touches HIP until Node() ----
@@ -481,7 +486,7 @@ def main():
     native = None
     if launcher is not None:
         if world > 1:
-            cross = run_cross_gpu(world, launcher)
+            cross = run_cross_gpu(world, launcher, gpu=gpu_of)
         if native_ladder:
             native = run_native_ladder(launcher, local_rank)
         launcher.close()
@@ -561,8 +566,8 @@ def main():
         line["cpu_baseline"] = {
             "value": tp[0]["GBps"] if tp else None, "unit": "GB/s", "cores": 3, "kind": "port",
             "sample": "reference shm path restated in C++ (sender/daemon/sink pinned to 3 cores,"
-                      " TCP control, F8 daemon copy): 20 latency + 40 throughput msgs per size "
-                      "in {4096, 40960, 409600, 4096000, 40960000}",
+                      " TCP control, F8 daemon copy): 100 latency (10 ms apart) + 200 throughput "
+                      "msgs per size in {4096, 40960, 409600, 4096000, 40960000}",
             "latency_us": {str(s["size"]): {"p50_us": s["p50_us"], "p99_us": s["p99_us"]}
                            for s in base["series"] if s["mode"] == "latency"},
             "wall_s": base["wall_s"], "nproc": base["nproc"], "cores_used": base["cores"]}
