@@ -231,9 +231,14 @@ AqlQueue* create(int device) {
 
 }  // namespace
 
+namespace {
+std::mutex g_queues_mu;
+AqlQueue* g_queues[64] = {};
+}  // namespace
+
 AqlQueue* aql_queue(int device) {
-  static std::mutex mu;
-  static AqlQueue* queues[64] = {};
+  static std::mutex& mu = g_queues_mu;
+  static AqlQueue** queues = g_queues;
   static bool tried[64] = {};
   if (!aql_enabled() || device < 0 || device >= 64) return nullptr;
   std::lock_guard<std::mutex> g(mu);
@@ -246,6 +251,23 @@ AqlQueue* aql_queue(int device) {
 }
 
 size_t aql_max_segments() { return 8; }
+
+void aql_fence_all() {
+  AqlQueue* qs[64];
+  {
+    std::lock_guard<std::mutex> g(g_queues_mu);
+    std::copy(g_queues, g_queues + 64, qs);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (AqlQueue* a : qs) {
+    if (!a) continue;
+    std::lock_guard<std::mutex> g(a->mu);
+    for (Use& u : a->uses)
+      while (u.flag && u.flag->load(std::memory_order_acquire) < u.epoch &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
+        __builtin_ia32_pause();
+  }
+}
 
 void aql_forget_flags(int device, const void* base, size_t size) {
   AqlQueue* a = aql_queue(device);

@@ -36,6 +36,11 @@ int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const Fil
 // region about to be unmapped), after waiting (bounded) for those fills to signal.
 void aql_forget_flags(int device, const void* base, size_t size);
 
+// Wait (bounded) until every AQL pack dispatched so far in this process has signalled: HIP's
+// hipFree waits for the HIP streams of the device, not for these queues, so the library's own
+// frees of device memory (dora_gpu_free, device array release) call this first.
+void aql_fence_all();
+
 // Segments one AQL dispatch takes.
 size_t aql_max_segments();
 

@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "aql.h"
 #include "common.h"
 #include "device_array.h"
 #include "plan.h"
@@ -57,6 +58,7 @@ void release_array(ArrowArray* a) {
     if (p->dictionary->release) p->dictionary->release(p->dictionary);
     delete p->dictionary;
   }
+  if (!p->dev_owned.empty()) aql_fence_all();  // AQL packs may still read these buffers
   for (void* d : p->dev_owned) (void)hipFree(d);
   for (void* h : p->host_owned) std::free(h);
   delete p;

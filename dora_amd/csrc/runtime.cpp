@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "aql.h"
 #include "common.h"
 
 namespace dora {
@@ -120,6 +121,7 @@ int dora_gpu_malloc(void** out, size_t nbytes) {
 }
 
 int dora_gpu_free(void* ptr) {
+  dora::aql_fence_all();  // packs dispatched on the AQL queues may still read `ptr`
   DORA_HIP(hipFree(ptr));
   return DORA_OK;
 }
