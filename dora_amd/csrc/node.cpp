@@ -1227,8 +1227,6 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     }
   }
 
-  // the AQL pack queues (aql.h) are set up here, not on the first send
-  if (device >= 0) (void)dora::aql_queue(device);
   auto* n = new dora_node();
   n->core = core;
   n->id = node_id;
