@@ -221,6 +221,7 @@ struct NodeCore {
   std::vector<uint8_t> fill_dirty;
   hipEvent_t node_ev = nullptr;
   size_t fill_next = 0;
+  bool fill_streams_tried = false;
   // fills dispatched on the AQL queue and not yet seen complete (fence_fills waits for them)
   std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>> aql_pending;
   RingWriter req;
@@ -309,7 +310,29 @@ struct NodeCore {
   }
 
   // The stream the next fill runs on (round robin), ordered after the node stream's queued work.
+  void ensure_fill_streams() {
+    if (!fill_streams.empty() || fill_streams_tried) return;
+    fill_streams_tried = true;
+    if (fill_stream_count() > 1 && async_sends() &&
+        hipEventCreateWithFlags(&node_ev, hipEventDisableTiming) == hipSuccess) {
+      for (size_t i = 0; i < fill_stream_count(); ++i) {
+        hipStream_t s = nullptr;
+        hipEvent_t e = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+          (void)hipStreamDestroy(s);
+          break;
+        }
+        fill_streams.push_back(s);
+        fill_events.push_back(e);
+      }
+      fill_dirty.assign(fill_streams.size(), 0);
+    }
+    (void)hipGetLastError();
+  }
+
   hipStream_t next_fill_stream() {
+    ensure_fill_streams();
     if (fill_streams.empty()) return stream;
     const size_t i = fill_next++ % fill_streams.size();
     hipStream_t s = fill_streams[i];
@@ -1193,18 +1216,11 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
       }
     }
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
-    if (dora::fill_stream_count() > 1 && dora::async_sends()) {
-      DORA_HIP(hipEventCreateWithFlags(&core->node_ev, hipEventDisableTiming));
-      for (size_t i = 0; i < dora::fill_stream_count(); ++i) {
-        hipStream_t s = nullptr;
-        hipEvent_t e = nullptr;
-        DORA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        core->fill_streams.push_back(s);
-        DORA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        core->fill_events.push_back(e);
-      }
-      core->fill_dirty.assign(core->fill_streams.size(), 0);
-    }
+    // A node with outputs creates its fill streams now, right after the node stream and before
+    // anything touches the null stream: HIP maps a process's streams onto its 4 hardware queues
+    // in creation order, and fill streams created later share one (40.96 MB: 13.2 -> 15.0-15.2
+    // us device time per pack).  A node that only receives keeps its single stream.
+    if (e.outputs[0] != 0) core->ensure_fill_streams();
     if (dora::async_sends()) {
       // host-register the control region so this node's stream can write fill epochs into it
       void* dev = nullptr;
@@ -1548,12 +1564,7 @@ int dora_node_set_timing_period(dora_node* n, uint64_t period) {
 int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
-  if (!n->region_start) {
-    DORA_HIP(hipEventCreate(&n->region_start));
-    const size_t k = std::max<size_t>(1, n->core->fill_streams.size());
-    n->region_stop.resize(k + 1);
-    for (auto& e : n->region_stop) DORA_HIP(hipEventCreate(&e));
-  }
+  if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
   n->region_armed = true;
   n->region_started = false;
   n->region_packs = n->region_bytes = n->region_aql = 0;
@@ -1592,6 +1603,11 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
   // stop = the end of the last pack on each fill stream (and the node stream)
   std::vector<hipStream_t> ss = n->core->fill_streams;
   ss.push_back(n->core->stream);
+  while (n->region_stop.size() < ss.size()) {  // fill streams are created lazily
+    hipEvent_t e = nullptr;
+    DORA_HIP(hipEventCreate(&e));
+    n->region_stop.push_back(e);
+  }
   for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i)
     DORA_HIP(hipEventRecord(n->region_stop[i], ss[i]));
   for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i) {
