@@ -71,7 +71,16 @@ class Ranks:
         if world > 1:
             import torch.distributed as dist
             if not dist.is_initialized():
-                dist.init_process_group("gloo")
+                # gloo prints "[Gloo] Rank r is connected to ..." on fd 1: keep stdout for the
+                # one JSON line (the banner goes to stderr instead)
+                sys.stdout.flush()
+                saved = os.dup(1)
+                os.dup2(2, 1)
+                try:
+                    dist.init_process_group("gloo")
+                finally:
+                    os.dup2(saved, 1)
+                    os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -146,17 +155,22 @@ def _source_env(result, lat_sizes, tp_size, tp_n, acks, lat_n=30, gap_us=33333):
             "DORA_BENCH_ACKS": str(acks)}
 
 
-def c4_descriptor(n_gpus, tmp, peer_copy="kernel", tp_n=200, gpu=lambda g: g, env=None):
-    """C4: one producer on GPU 0, a consumer on every other GPU (1 -> n_gpus-1 fan-out).  Each
-    consumer pulls the frame from the producer's slot over its own xGMI link (no collective:
-    every receiver keeps its own queue and drop-oldest policy)."""
+def c4_descriptor(n_gpus, tmp, peer_copy="kernel", tp_n=200, gpu=lambda g: g, env=None,
+                  fanout="pull"):
+    """C4: one producer on GPU 0, a consumer on every other GPU (1 -> n_gpus-1 fan-out).
+    fanout="pull": each consumer pulls the frame from the producer's slot over its own xGMI link
+    (every receiver keeps its own queue and drop-oldest policy); fanout="rccl": the producer
+    broadcasts each frame over an RCCL group of the output's receivers."""
     sinks = [f"sink{g}" for g in range(1, n_gpus)]
     env = dict(env or {}, DORA_GPU_PEER_COPY=peer_copy)
+    src_env = _source_env(os.path.join(tmp, "source.json"), [C4_FRAME], C4_FRAME, tp_n,
+                          len(sinks))
+    if fanout == "rccl":
+        src_env["DORA_GPU_FANOUT"] = "rccl"
     nodes = [{"id": "source", "path": "dora-gpu-bench-source",
               "outputs": ["latency", "throughput"],
               "inputs": {f"ack{k}": f"{s}/ack" for k, s in enumerate(sinks)},
-              "env": _source_env(os.path.join(tmp, "source.json"), [C4_FRAME], C4_FRAME, tp_n,
-                                 len(sinks)),
+              "env": src_env,
               "_unstable_deploy": {"gpu": gpu(0)}}]
     for g, s in zip(range(1, n_gpus), sinks):
         nodes.append({"id": s, "path": "dora-gpu-bench-sink", "outputs": ["ack"],
@@ -205,15 +219,18 @@ def run_cross_gpu(n_gpus, launcher, timeout=240.0, runs=None, **desc_kw):
     must not depend on them."""
     from dora_amd.dataflow import Dataflow
     out = {}
-    runs = runs or [("c4_fanout_kernel", c4_descriptor, "kernel"),
-                    ("c4_fanout_sdma", c4_descriptor, "sdma"),
-                    ("c5_chain_kernel", c5_descriptor, "kernel")]
-    for name, fn, mode in runs:
+    runs = runs or [("c4_fanout_kernel", c4_descriptor, "kernel", {}),
+                    ("c4_fanout_sdma", c4_descriptor, "sdma", {}),
+                    ("c5_chain_kernel", c5_descriptor, "kernel", {}),
+                    # last: RCCL runs only on distinct GPUs, so this is its first exercise on a
+                    # real node; a shorter limit keeps a stuck group from holding the line back
+                    ("c4_fanout_rccl", c4_descriptor, "kernel", {"fanout": "rccl"})]
+    for name, fn, mode, kw in runs:
         tmp = tempfile.mkdtemp(prefix=f"dora-{name}-")
         try:
-            df = Dataflow(fn(n_gpus, tmp, mode, **desc_kw), launcher=launcher).start()
+            df = Dataflow(fn(n_gpus, tmp, mode, **kw, **desc_kw), launcher=launcher).start()
             try:
-                codes = df.wait(timeout)
+                codes = df.wait(timeout if not kw else min(timeout, 120.0))
                 logs = {k: df.log(k)[-400:] for k, c in codes.items() if c not in (0, None)}
             finally:
                 df.stop()
@@ -283,7 +300,14 @@ def summarize_cross(name, src, sinks, codes, logs):
                         "unit": "GB/s", "frac": round(per_rx / XGMI_LINK_GBPS, 4)},
            "latency_us": lat, "parity": {"verified_msgs": verified, "mismatches": mismatches},
            "dropped_inputs": dropped, "errors": errors, "exit_codes": codes,
-           "source_send_phase_us": src.get("send_phase_us")}
+           "source_send_phase_us": src.get("send_phase_us"),
+           # transfer path actually taken: pulls per receiver, or RCCL broadcast group traffic
+           "pulls": sum((r or {}).get("pulls", 0) for r in sinks.values()),
+           "bcast": {"groups": src.get("bcast_groups", 0), "sent": src.get("bcast_sent", 0),
+                     "received": sum((r or {}).get("bcast_received", 0) for r in sinks.values()),
+                     "error": src.get("bcast_error") or next(
+                         (r.get("bcast_error") for r in sinks.values()
+                          if r and r.get("bcast_error")), "")}}
     if logs:
         res["logs"] = logs
     return res

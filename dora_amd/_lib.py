@@ -123,6 +123,9 @@ _SIGS = {
     "dora_node_pack_intervals": (c_int, [c_void_p, POINTER(c_double), c_size_t,
                                          POINTER(c_size_t)]),
     "dora_node_peer_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_node_bcast_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64),
+                                      POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                      POINTER(c_char_p)]),
     "dora_node_forward": (c_int, [c_void_p, c_char_p, c_void_p, c_char_p, c_size_t]),
     "dora_node_send_profile": (c_int, [c_void_p, POINTER(c_double), c_size_t, POINTER(c_uint64)]),
     "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),

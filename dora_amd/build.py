@@ -18,7 +18,7 @@ INCLUDE = os.path.join(ROOT, "include")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
-LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp",
+LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp", "bcast.cpp",
                "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp", "aql.cpp"]
 AQL_KERNELS = "aql_kernels.hip"  # standalone gfx950 code object embedded in the library
 LIB_NAME = "libdora_gpu.so"
@@ -99,7 +99,7 @@ def build(verbose: bool = False) -> str:
     out = os.path.join(LIB, LIB_NAME)
     if _newer(out, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
-               "-Wl,-soname," + LIB_NAME, "-L/opt/rocm/lib", "-lhsa-runtime64", "-lpthread",
+               "-Wl,-soname," + LIB_NAME, "-L/opt/rocm/lib", "-lhsa-runtime64", "-ldl", "-lpthread",
                "-lrt"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -24,6 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "bcast.h"
 #include "common.h"
 #include "dora_gpu.h"
 #include "shm.h"
@@ -47,7 +48,7 @@ struct DNode {
   bool done = false;
   bool all_closed_sent = false;
   std::deque<std::pair<uint32_t, std::vector<uint8_t>>> ev_overflow;    // events not yet in ring
-  std::deque<std::vector<uint8_t>> drop_overflow;
+  std::deque<std::pair<uint32_t, std::vector<uint8_t>>> drop_overflow;
 };
 
 struct TokenInfo {
@@ -204,13 +205,17 @@ class Daemon {
   }
 
   void push_drop(int node, const DropToken& t) {
-    DNode& n = nodes_[node];
-    if (n.done) return;
     WBuf w;
     w.token(t);
-    if (n.drop_overflow.empty() && drop_[node].try_push(DROP_OUTPUT_DROPPED, w.b.data(), w.b.size()))
+    push_drop_record(node, DROP_OUTPUT_DROPPED, std::move(w.b));
+  }
+
+  void push_drop_record(int node, uint32_t kind, std::vector<uint8_t> payload) {
+    DNode& n = nodes_[node];
+    if (n.done) return;
+    if (n.drop_overflow.empty() && drop_[node].try_push(kind, payload.data(), payload.size()))
       return;
-    n.drop_overflow.push_back(std::move(w.b));
+    n.drop_overflow.emplace_back(kind, std::move(payload));
   }
 
   bool flush_overflow() {
@@ -225,7 +230,7 @@ class Daemon {
       }
       while (!n.drop_overflow.empty()) {
         auto& f = n.drop_overflow.front();
-        if (!drop_[i].try_push(DROP_OUTPUT_DROPPED, f.data(), f.size())) break;
+        if (!drop_[i].try_push(f.first, f.second.data(), f.second.size())) break;
         n.drop_overflow.pop_front();
         any = true;
       }
@@ -277,6 +282,13 @@ class Daemon {
       case REQ_OUTPUTS_DONE:
         node_done(i);
         break;
+      case REQ_BCAST_GROUP: {
+        const std::string output = r.str();
+        uint8_t uid[kBcastIdBytes];
+        r.raw(uid, sizeof(uid));
+        bcast_group(i, output, uid);
+        break;
+      }
       default:
         break;
     }
@@ -309,6 +321,44 @@ class Daemon {
       ti.owner = i;
       check_drop_token(data.ipc.token);
     }
+  }
+
+  // REQ_BCAST_GROUP (bcast.h): admit an RCCL group for output `output` of node `i` when every
+  // receiver runs on its own GPU and none on the producer's (one rank per device), then tell the
+  // receivers their ranks and the producer the group size (0: no group, receivers pull).
+  void bcast_group(int i, const std::string& output, const uint8_t* uid) {
+    RegionHdr* h = region_->hdr();
+    const int32_t root_dev = h->nodes[i].device.load();
+    std::set<int32_t> devs{root_dev};
+    std::vector<Receiver> members;
+    bool ok = root_dev >= 0 && nodes_[i].outputs.count(output);
+    auto it = mappings_.find({i, output});
+    if (ok && it != mappings_.end()) {
+      for (const Receiver& rc : it->second) {
+        const DNode& rn = nodes_[rc.node];
+        const int32_t d = h->nodes[rc.node].device.load();
+        if (!rn.subscribed || rn.done || !rn.open_inputs.count(rc.input) || d < 0 ||
+            !devs.insert(d).second) {
+          ok = false;
+          break;
+        }
+        members.push_back(rc);
+      }
+    }
+    ok = ok && !members.empty();
+    const uint32_t nranks = ok ? static_cast<uint32_t>(members.size() + 1) : 0;
+    for (uint32_t k = 0; ok && k < members.size(); ++k) {
+      WBuf w;
+      w.str(members[k].input);
+      w.raw(uid, kBcastIdBytes);
+      w.u32(nranks);
+      w.u32(k + 1);
+      push_event(members[k].node, EV_BCAST_JOIN, std::move(w.b));
+    }
+    WBuf a;
+    a.str(output);
+    a.u32(nranks);
+    push_drop_record(i, DROP_BCAST_GROUP, std::move(a.b));
   }
 
   void check_drop_token(const DropToken& t) {

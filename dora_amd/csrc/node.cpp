@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "aql.h"
+#include "bcast.h"
 #include "common.h"
 #include "device_array.h"
 #include "dora_gpu.h"
@@ -168,6 +169,16 @@ bool edge_copy_forced() {
   return v;
 }
 
+// DORA_GPU_FANOUT=rccl: this node's outputs with receivers on other GPUs form RCCL broadcast
+// groups (bcast.h) instead of letting every receiver pull over its own link.
+bool fanout_rccl() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_FANOUT");
+    return e && std::strcmp(e, "rccl") == 0;
+  }();
+  return v;
+}
+
 uint64_t slot_wait_ns() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_SLOT_WAIT_US");
@@ -243,6 +254,13 @@ struct NodeCore {
   static constexpr size_t kMaxPooled = 16;
   std::set<int> peer_enabled;  // peer devices this node's device may access (under ipc_mu)
   std::atomic<uint64_t> peer_copies{0}, peer_bytes{0};  // cross-GPU samples pulled
+
+  // RCCL broadcast groups this node receives on (input id -> communicator); every receive is
+  // posted on bcast_stream in the order the daemon routed the samples
+  std::map<std::string, BcastComm*> bcast_in;
+  hipStream_t bcast_stream = nullptr;
+  std::string bcast_error;
+  uint64_t bcast_recvs = 0, bcast_bytes = 0;
 
   void* recv_pool_get(uint64_t len, uint64_t* cap) {
     {
@@ -378,6 +396,8 @@ struct NodeCore {
   }
 
   ~NodeCore() {
+    for (auto& kv : bcast_in) bcast_close(kv.second, bcast_stream, 10000);
+    if (bcast_stream) (void)hipStreamDestroy(bcast_stream);
     // AQL argument slots must not keep pointing at this region's fill flags once it is unmapped
     if (device >= 0 && region) aql_forget_flags(device, region->base(), region->size());
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
@@ -408,8 +428,13 @@ struct InputData {
   void* local = nullptr;      // cross-GPU edge: local copy in this node's receive pool
   uint64_t local_cap = 0;
   int remote_device = -1;     // >= 0: `ptr` is a peer GPU's slot not yet pulled (ensure_local)
+  hipEvent_t bcast_ev = nullptr;  // broadcast group input: completion of its receive into `local`
   ~InputData() {
     if (!core) return;
+    if (bcast_ev) {
+      (void)hipEventSynchronize(bcast_ev);
+      (void)hipEventDestroy(bcast_ev);
+    }
     if (has_token || local) {
       // consumer reads on the node stream must be complete before the memory is reused
       if (core->stream && hipStreamQuery(core->stream) != hipSuccess)
@@ -489,6 +514,9 @@ struct dora_node {
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
   bool compact = false;                     // send_output uses compacting plans
+  // RCCL broadcast groups of this node's fan-out outputs (rank 0 of each), DORA_GPU_FANOUT=rccl
+  std::map<std::string, dora::BcastComm*> bcast_out;
+  uint64_t bcast_seq = 0;
 };
 
 namespace dora {
@@ -582,6 +610,67 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   return DORA_OK;
 }
 
+// EV_BCAST_JOIN: become rank `rank` of the producer's broadcast group for input `input`.
+void join_bcast_group(dora_node* n, const std::string& input, const uint8_t* uid, uint32_t nranks,
+                      uint32_t rank) {
+  NodeCore* c = n->core.get();
+  if (c->device < 0) {
+    c->bcast_error = "host-only node cannot join a broadcast group";
+    return;
+  }
+  if (!c->bcast_stream && hipStreamCreateWithFlags(&c->bcast_stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    c->bcast_stream = nullptr;
+    c->bcast_error = "broadcast receive stream";
+    return;
+  }
+  BcastComm* comm = nullptr;
+  if (bcast_join(uid, static_cast<int>(nranks), static_cast<int>(rank), 30000, &comm) != DORA_OK) {
+    c->bcast_error = dora_gpu_last_error();
+    return;
+  }
+  auto it = c->bcast_in.find(input);
+  if (it != c->bcast_in.end()) bcast_close(it->second, c->bcast_stream, 10000);
+  c->bcast_in[input] = comm;
+}
+
+// A FILL_BCAST sample: post this rank's receive of the producer's broadcast into the receive
+// pool right away (at drain time, so every rank issues the group's broadcasts in routing order,
+// whether or not the input is later dropped); the input is complete when `bcast_ev` fires.
+int post_bcast_receive(NodeCore* c, InputData* in, const std::string& input) {
+  auto it = c->bcast_in.find(input);
+  if (it == c->bcast_in.end())
+    return fail(DORA_ERR_INVALID, "input `%s`: broadcast sample but no group joined (%s)",
+                input.c_str(), c->bcast_error.c_str());
+  uint64_t cap = 0;
+  void* local = c->recv_pool_get(in->ext_len, &cap);
+  if (!local)
+    return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->ext_len);
+  int rc = bcast_enqueue(it->second, local, in->ext_len, c->bcast_stream);
+  hipEvent_t e = nullptr;
+  if (rc == DORA_OK) {
+    hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventRecord(e, c->bcast_stream);
+    if (he != hipSuccess) {
+      // the receive is queued: wait for it here rather than lose track of it
+      (void)hipStreamSynchronize(c->bcast_stream);
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  }
+  if (rc != DORA_OK) {
+    c->recv_pool_put(local, cap);
+    return rc;
+  }
+  in->local = local;
+  in->local_cap = cap;
+  in->ptr = local;
+  in->bcast_ev = e;
+  ++c->bcast_recvs;
+  c->bcast_bytes += in->ext_len;
+  return DORA_OK;
+}
+
 void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
   auto ev = std::make_unique<dora_event>();
   RBuf r(p);
@@ -607,7 +696,14 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         in->len = d.ipc.len;
         in->ext_len = std::max(d.ipc.ext_len, d.ipc.len);
         void* base = nullptr;
-        if (d.ipc.owner_pid == getpid()) {
+        if (d.ipc.fill == FILL_BCAST) {
+          // the sample arrives through the output's RCCL group, not the producer's slot
+          if (post_bcast_receive(n->core.get(), in.get(), ev->id) != DORA_OK) {
+            ev->type = DORA_EVENT_ERROR;
+            ev->error = dora_gpu_last_error();
+            in->ptr = nullptr;
+          }
+        } else if (d.ipc.owner_pid == getpid()) {
           std::lock_guard<std::mutex> g(own_slots().mu);
           auto it = own_slots().ptrs.find(d.ipc.slot_id);
           if (it != own_slots().ptrs.end()) base = it->second;
@@ -649,6 +745,15 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
     case EV_STOP:
       ev->type = DORA_EVENT_STOP;
       break;
+    case EV_BCAST_JOIN: {
+      const std::string input = r.str();
+      uint8_t uid[kBcastIdBytes];
+      r.raw(uid, sizeof(uid));
+      const uint32_t nranks = r.u32();
+      const uint32_t rank = r.u32();
+      join_bcast_group(n, input, uid, nranks, rank);
+      return;  // internal: no event for the user
+    }
     default:
       return;  // EV_READY after init is ignored
   }
@@ -664,6 +769,25 @@ void finish_input(dora_node* n, dora_event* ev) {
   InputData* in = ev->data.get();
   const DeviceIpc& d = ev->ipc;
   if (!in || !in->ptr) return;
+  if (d.fill == FILL_BCAST) {
+    // the receive was posted at drain time; hand the input out once it has completed
+    hipError_t e = in->bcast_ev ? hipEventQuery(in->bcast_ev) : hipSuccess;
+    const uint64_t t0 = mono_ns();
+    while (e == hipErrorNotReady && mono_ns() - t0 < 60000000000ull) {
+      if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
+      else __builtin_ia32_pause();
+      e = hipEventQuery(in->bcast_ev);
+    }
+    if (e != hipSuccess) {
+      ev->type = DORA_EVENT_ERROR;
+      ev->error = e == hipErrorNotReady ? "broadcast receive did not complete within 60 s"
+                                        : std::string("broadcast receive: ") + hipGetErrorString(e);
+      in->ptr = nullptr;
+      return;
+    }
+    trace(TP_FILLED, in->token);
+    return;
+  }
   if (d.fill == FILL_FLAG) {
     // the producer's stream writes the epoch into its fill flag after the pack: poll it
     RegionHdr* h = n->core->region->hdr();
@@ -867,12 +991,25 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.ipc.ext_len = std::max(sample->len, sample->ext_len);
       d.ipc.token = generate_drop_token();
       d.ipc.fill = sample->fill;
-      if (sample->fill == FILL_FLAG) {
+      auto g = n->bcast_out.find(output_id);
+      if (g != n->bcast_out.end()) {
+        // fan-out over the output's RCCL group: broadcast the slot on the node stream, after
+        // every fill so far (fills of other streams / the AQL queues are fenced first)
+        if (sample->fill != FILL_DONE) n->core->fence_fills();
+        int rc = bcast_enqueue(g->second, slot->ptr, d.ipc.ext_len, n->core->stream);
+        if (rc != DORA_OK) {
+          add_to_cache(n, slot);
+          delete sample;
+          return rc;
+        }
+        d.ipc.fill = FILL_BCAST;
+        d.ipc.epoch = ++n->bcast_seq;
+      } else if (sample->fill == FILL_FLAG) {
         d.ipc.flag_node = static_cast<uint32_t>(n->core->idx);
         d.ipc.flag_index = static_cast<uint32_t>(slot->flag);
         d.ipc.epoch = sample->epoch;
       }
-      if (sample->fill == FILL_EVENT) std::memcpy(d.ipc.event, &slot->done_handle, 64);
+      if (d.ipc.fill == FILL_EVENT) std::memcpy(d.ipc.event, &slot->done_handle, 64);
     } else {
       d.kind = DATA_VEC;
       d.vec = std::move(sample->vec);
@@ -1020,7 +1157,14 @@ bool kernel_signal() {
 // Launch the fill of sample `s` (segments into its slot) on stream `st` and order its
 // completion signal.
 int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
-                ArrowDeviceType dev, hipStream_t st, hipEvent_t t_start, hipEvent_t t_stop) {
+                ArrowDeviceType dev, hipStream_t st, hipEvent_t t_start, hipEvent_t t_stop,
+                bool signal = true) {
+  if (!signal) {
+    // the caller orders what follows on `st` (a broadcast-group send): no fill flag
+    ++n->hip_packs;
+    return launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start, t_stop,
+                       nullptr, nullptr);
+  }
   FillSignal sig{};
   const FillSignal* sp = nullptr;
   if (s->slot->flag >= 0 && n->core->fill_done && kernel_signal()) {
@@ -1112,6 +1256,57 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
   return send_sample(n, output_id, ev->meta.type_info, params, params_len, s);
 }
 
+// DORA_GPU_FANOUT=rccl, at init: ask the daemon for a broadcast group per output and, when it
+// admits one (receivers each on their own GPU, none on ours), form the communicator as rank 0.
+// Outputs without a group keep the pull path.  Every wait is bounded.
+void form_bcast_groups(dora_node* n) {
+  NodeCore* c = n->core.get();
+  std::string why;
+  if (!bcast_available(&why)) {
+    c->bcast_error = why;
+    return;
+  }
+  for (const std::string& o : n->outputs) {
+    uint8_t uid[kBcastIdBytes];
+    if (bcast_unique_id(uid) != DORA_OK) {
+      c->bcast_error = dora_gpu_last_error();
+      return;
+    }
+    WBuf w;
+    w.str(o);
+    w.raw(uid, sizeof(uid));
+    if (c->request(REQ_BCAST_GROUP, w.b) != DORA_OK) return;
+    uint32_t nranks = 0;
+    bool answered = false;
+    const uint64_t t0 = mono_ns();
+    while (!answered && mono_ns() - t0 < 10000000000ull) {
+      uint32_t kind;
+      std::vector<uint8_t> p;
+      if (!c->drops.try_pop(&kind, &p)) {
+        c->drops.wait(10000);
+        continue;
+      }
+      RBuf r(p);
+      if (kind == DROP_OUTPUT_DROPPED) {
+        on_token(n, r.token());
+      } else if (kind == DROP_BCAST_GROUP && r.str() == o) {
+        nranks = r.u32();
+        answered = true;
+      }
+    }
+    if (nranks < 2) {
+      c->bcast_error = "output `" + o + "`: the daemon admitted no broadcast group (each receiver "
+                       "must run on its own GPU, none on the producer's); receivers pull";
+      continue;
+    }
+    BcastComm* comm = nullptr;
+    if (bcast_join(uid, static_cast<int>(nranks), 0, 30000, &comm) == DORA_OK)
+      n->bcast_out[o] = comm;
+    else
+      c->bcast_error = dora_gpu_last_error();
+  }
+}
+
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
                   size_t params_len) {
   dora_sample* s = nullptr;
@@ -1143,8 +1338,10 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       ++n->region_packs;
       n->region_bytes += plan->size;
     }
-    rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev, nullptr, t_start,
-                     t_stop);
+    // a broadcast-group output packs on the node stream, where its broadcast follows
+    const bool bcast = n->bcast_out.count(output_id) > 0;
+    rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
+                     bcast ? n->core->stream : nullptr, t_start, t_stop, !bcast);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
@@ -1201,6 +1398,7 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   core->ev = dora::RingReader(core->region.get(), &e.events);
   core->drops = dora::RingReader(core->region.get(), &e.drops);
   core->device = device;
+  e.device.store(device < 0 ? -1 : device);
   dora::trace_set_name(node_id);
   if (device >= 0) {  // device < 0: host-only node (control plane + inline Vec samples only)
     DORA_HIP(hipSetDevice(device));
@@ -1275,6 +1473,7 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     }
     core->ev.wait(100000);
   }
+  if (device >= 0 && dora::fanout_rccl() && !n->outputs.empty()) dora::form_bcast_groups(n);
   *out = n;
   return DORA_OK;
   DORA_GUARD_END
@@ -1311,6 +1510,9 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
   }
   (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
+  // broadcasts read the slots: the groups go (after their streams drain, bounded) first
+  for (auto& kv : n->bcast_out) dora::bcast_close(kv.second, n->core->stream, 10000);
+  n->bcast_out.clear();
   for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
   for (auto* s : n->cache) dora::free_slot(n, s);
   dora::harvest_all(n);
@@ -1632,6 +1834,19 @@ int dora_node_peer_stats(dora_node* n, uint64_t* copies, uint64_t* bytes) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (copies) *copies = n->core->peer_copies.load();
   if (bytes) *bytes = n->core->peer_bytes.load();
+  return DORA_OK;
+}
+
+int dora_node_bcast_stats(dora_node* n, uint64_t* groups_out, uint64_t* groups_in,
+                          uint64_t* sent, uint64_t* received, uint64_t* received_bytes,
+                          const char** error) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (groups_out) *groups_out = n->bcast_out.size();
+  if (groups_in) *groups_in = n->core->bcast_in.size();
+  if (sent) *sent = n->bcast_seq;
+  if (received) *received = n->core->bcast_recvs;
+  if (received_bytes) *received_bytes = n->core->bcast_bytes;
+  if (error) *error = n->core->bcast_error.c_str();
   return DORA_OK;
 }
 

@@ -152,6 +152,7 @@ Region* Region::create(const std::string& name, const std::vector<std::string>& 
     std::strncpy(n.id, node_ids[i].c_str(), kIdLen - 1);
     new (&n.pid) std::atomic<int32_t>(0);
     new (&n.state) std::atomic<uint32_t>(0);
+    new (&n.device) std::atomic<int32_t>(-2);
     for (auto& f : n.fill) new (&f.epoch) std::atomic<uint64_t>(0);
     init_ring(n.requests, off, ring_cap);
     off += ring_cap;

@@ -20,7 +20,7 @@
 namespace dora {
 
 constexpr uint64_t kRegionMagic = 0x444f5241474d5358ull;  // "DORAGMSX"
-constexpr uint32_t kRegionVersion = 2;
+constexpr uint32_t kRegionVersion = 3;
 constexpr uint32_t kMaxNodes = 64;
 constexpr size_t kIdLen = 64;
 
@@ -50,6 +50,7 @@ struct NodeEntry {
   char inputs[kListLen];   // "in1=10,in2=1"        (input id = queue_size)
   std::atomic<int32_t> pid;
   std::atomic<uint32_t> state;  // 0 idle, 1 subscribed, 2 done
+  std::atomic<int32_t> device;  // GPU ordinal of the running node (-1 host-only, -2 not started)
   RingHdr requests;
   RingHdr events;
   RingHdr drops;

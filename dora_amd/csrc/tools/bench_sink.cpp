@@ -133,13 +133,19 @@ int main() {
   }
   uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
   dora_node_stats(node, &slots, &hits, &inflight, &dropped);
+  uint64_t pulls = 0, pull_bytes = 0, bgroups = 0, brecv = 0, brecv_bytes = 0;
+  const char* berr = "";
+  dora_node_peer_stats(node, &pulls, &pull_bytes);
+  dora_node_bcast_stats(node, nullptr, &bgroups, nullptr, &brecv, &brecv_bytes, &berr);
   FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
   std::fprintf(f,
                "{\"errors\": %d, \"dropped_inputs\": %llu, \"next_event_us\": %.3f, "
-               "\"free_us\": %.3f, \"series\": [",
+               "\"free_us\": %.3f, \"pulls\": %llu, \"bcast_groups\": %llu, "
+               "\"bcast_received\": %llu, \"bcast_error\": \"%s\", \"series\": [",
                errors, (unsigned long long)dropped,
                n_inputs ? double(t_next) / n_inputs / 1000.0 : 0.0,
-               n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0);
+               n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0, (unsigned long long)pulls,
+               (unsigned long long)bgroups, (unsigned long long)brecv, json_safe(berr).c_str());
   bool first = true;
   for (auto& kv : stats) {
     Series& s = kv.second;

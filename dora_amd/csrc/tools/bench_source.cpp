@@ -182,17 +182,22 @@ int main() {
   uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
   dora_node_stats(node, &slots, &hits, &inflight, &dropped);
 
+  uint64_t bgroups = 0, bsent = 0;
+  const char* berr = "";
+  dora_node_bcast_stats(node, &bgroups, nullptr, &bsent, nullptr, nullptr, &berr);
   FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
   const double delivered = double(tp_size) * double(tp_n) * double(acks);
   std::fprintf(f,
                "{\"errors\": %d, \"ok\": %s, \"receivers\": %ld, \"tp_size\": %llu, \"tp_n\": %ld, "
                "\"tp_seconds\": %.6f, \"tp_delivered_GBps\": %.3f, \"tp_per_receiver_GBps\": %.3f, "
                "\"send_phase_us\": {\"alloc_us\": %.2f, \"launch_us\": %.2f, \"fill_us\": %.2f, "
-               "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu}\n",
+               "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu, "
+               "\"bcast_groups\": %llu, \"bcast_sent\": %llu, \"bcast_error\": \"%s\"}\n",
                errors, ok ? "true" : "false", acks, (unsigned long long)tp_size, tp_n, tp_s,
                tp_s > 0 ? delivered / tp_s / 1e9 : 0.0,
                tp_s > 0 ? double(tp_size) * double(tp_n) / tp_s / 1e9 : 0.0, phase[0], phase[1],
-               phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits);
+               phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits,
+               (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str());
   if (f != stdout) std::fclose(f);
   for (auto& kv : src) dora_gpu_free(kv.second.ptr);
   dora_node_free(node);

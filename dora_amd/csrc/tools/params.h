@@ -77,3 +77,11 @@ inline std::map<std::string, Param> decode_params(const uint8_t* p, size_t n) {
   }
   return m;
 }
+
+// A C string as the body of a JSON string literal (quotes, backslashes and control bytes
+// replaced).
+inline std::string json_safe(const char* s) {
+  std::string o;
+  for (; s && *s; ++s) o += (*s == '"' || *s == '\\' || static_cast<unsigned char>(*s) < 0x20) ? ' ' : *s;
+  return o;
+}

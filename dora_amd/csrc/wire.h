@@ -34,12 +34,15 @@ enum : uint32_t {
   REQ_REPORT_DROP_TOKENS = 3,
   REQ_CLOSE_OUTPUTS = 4,
   REQ_OUTPUTS_DONE = 5,
+  REQ_BCAST_GROUP = 6,  // {output, ncclUniqueId}: form an RCCL group of the output's receivers
   EV_READY = 101,
   EV_INPUT = 102,
   EV_INPUT_CLOSED = 103,
   EV_ALL_INPUTS_CLOSED = 104,
   EV_STOP = 105,
+  EV_BCAST_JOIN = 106,  // {input, ncclUniqueId, nranks, rank}: join the producer's group
   DROP_OUTPUT_DROPPED = 201,
+  DROP_BCAST_GROUP = 202,  // {output, nranks}: the daemon's answer to REQ_BCAST_GROUP (0: none)
 };
 
 enum : uint8_t { DATA_NONE = 0, DATA_VEC = 1, DATA_DEVICE_IPC = 2 };
@@ -57,13 +60,15 @@ struct DeviceIpc {
   // How the receiver learns that the fill is complete:
   //   FILL_DONE  the sender synchronised before sending;
   //   FILL_FLAG  poll region node `flag_node`'s FillFlag[flag_index] until >= epoch;
-  //   FILL_EVENT wait on the interprocess event `event` (fallback when no flag is free).
+  //   FILL_EVENT wait on the interprocess event `event` (fallback when no flag is free);
+  //   FILL_BCAST the producer broadcasts the sample over the output's RCCL group: the receiver
+  //              posts the matching receive into local HBM (`epoch` = the group's sequence).
   uint8_t fill = 0;
   uint32_t flag_node = 0, flag_index = 0;
   uint64_t epoch = 0;
   uint8_t event[64];  // hipIpcEventHandle_t
 };
-enum : uint8_t { FILL_DONE = 0, FILL_FLAG = 1, FILL_EVENT = 2 };
+enum : uint8_t { FILL_DONE = 0, FILL_FLAG = 1, FILL_EVENT = 2, FILL_BCAST = 3 };
 
 struct DataMsg {
   uint8_t kind = DATA_NONE;
@@ -117,6 +122,7 @@ class WBuf {
         u64(d.ipc.epoch);
       }
       if (d.ipc.fill == FILL_EVENT) raw(d.ipc.event, 64);
+      if (d.ipc.fill == FILL_BCAST) u64(d.ipc.epoch);
     }
   }
   void metadata(const Metadata& m) {
@@ -204,7 +210,8 @@ class RBuf {
         d.ipc.epoch = u64();
       }
       if (d.ipc.fill == FILL_EVENT) raw(d.ipc.event, 64);
-      if (d.ipc.fill > FILL_EVENT) throw std::invalid_argument("unknown fill kind");
+      if (d.ipc.fill == FILL_BCAST) d.ipc.epoch = u64();
+      if (d.ipc.fill > FILL_BCAST) throw std::invalid_argument("unknown fill kind");
     }
     if (d.kind > DATA_DEVICE_IPC) throw std::invalid_argument("unknown DataMessage kind");
     return d;

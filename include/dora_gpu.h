@@ -306,6 +306,18 @@ int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_pac
  * engines (DORA_GPU_PEER_COPY=sdma).  Counts and bytes of such pulls.  DORA_GPU_EDGE_COPY=1
  * forces the path on same-GPU edges. */
 int dora_node_peer_stats(dora_node* node, uint64_t* copies, uint64_t* bytes);
+/* 1 -> N fan-out over RCCL (no reference counterpart: the reference has no GPU
+ * transport).  A node started with DORA_GPU_FANOUT=rccl asks the daemon at init for a broadcast
+ * group per output; the daemon admits one when each receiver of the output runs on its own GPU
+ * and none on the producer's.  Sends on such an output broadcast the slot over the group
+ * (ncclBroadcast rooted at the producer, on the node stream); receivers post the matching
+ * receive into local HBM as the descriptor arrives and hand the input out once it completes.
+ * Outputs without a group keep the per-receiver pulls.  Groups formed (as producer / as
+ * receiver), samples broadcast / received, bytes received, and the last group error ("" if
+ * none). */
+int dora_node_bcast_stats(dora_node* node, uint64_t* groups_out, uint64_t* groups_in,
+                          uint64_t* sent, uint64_t* received, uint64_t* received_bytes,
+                          const char** error);
 /* Pack-kernel timing: hipExtLaunchKernel start/stop stamps of every n-th pack launch
  * (dora_node_set_timing_period; 0 = DORA_GPU_TIMING_SAMPLE, default 8). */
 int dora_node_set_profiling(dora_node* node, int enable);

@@ -378,8 +378,10 @@ def test_cross_gpu_bench_runs_on_one_gpu(launcher):
     import bench
     out = bench.run_cross_gpu(
         3, launcher, timeout=180,
-        runs=[("c4", bench.c4_descriptor, "kernel"), ("c5", bench.c5_descriptor, "kernel"),
-              ("c5_sdma", bench.c5_descriptor, "sdma")],
+        runs=[("c4", bench.c4_descriptor, "kernel", {}),
+              ("c5", bench.c5_descriptor, "kernel", {}),
+              ("c5_sdma", bench.c5_descriptor, "sdma", {}),
+              ("c4_rccl", bench.c4_descriptor, "kernel", {"fanout": "rccl"})],
         gpu=lambda g: 0, env={"DORA_GPU_EDGE_COPY": "1"}, tp_n=20)
     for name, r in out.items():
         assert r.get("ok"), (name, r)
@@ -387,6 +389,12 @@ def test_cross_gpu_bench_runs_on_one_gpu(launcher):
         assert r["dropped_inputs"] == 0
     assert out["c4"]["receivers"] == 2
     assert set(out["c5"]["latency_us"]) == {"4096", "40960000"}
+    # DORA_GPU_FANOUT=rccl with every receiver on the producer's GPU: the daemon admits no
+    # broadcast group (one RCCL rank per device) and the receivers pull, bit-exact as before
+    rc = out["c4_rccl"]
+    assert rc["bcast"]["groups"] == 0 and rc["bcast"]["received"] == 0, rc
+    assert "admitted no broadcast group" in rc["bcast"]["error"], rc
+    assert rc["pulls"] > 0
 
 
 def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
