@@ -106,7 +106,7 @@ int bcast_join(const uint8_t id[kBcastIdBytes], int nranks, int rank, int64_t ti
   *out = nullptr;
   Rccl& r = rccl();
   if (!r.loaded) return fail(DORA_ERR_UNSUPPORTED, "%s", r.why.c_str());
-  if (nranks < 2 || rank < 0 || rank >= nranks)
+  if (nranks < 1 || rank < 0 || rank >= nranks)
     return fail(DORA_ERR_INVALID, "broadcast group rank %d of %d", rank, nranks);
   ncclUniqueId u;
   std::memcpy(&u, id, kBcastIdBytes);
