@@ -4,10 +4,14 @@
 //
 // Pack = pure HBM streaming: read S bytes + write S bytes, no MFMA, no LDS.  Every chunk of a
 // segment is one 256-thread workgroup.  The destination is written with 16-byte aligned
-// `global_store_dwordx4`; the source is read with 16-byte aligned `global_load_dwordx4` and,
-// when source and destination disagree mod 16 (e.g. C3's x buffer at sample offset 68), two
-// aligned loads are funnel-shifted with v_alignbyte_b32.  The shift is uniform per segment, so
-// the per-segment loop is specialised on it and no lane diverges.
+// `global_store_dwordx4`; the source is read with `global_load_dwordx4` too.  When source and
+// destination disagree mod 16 by whole dwords (C3's x/y/z/intensity at sample offsets 4 mod 16)
+// the load is simply issued at the dword-aligned source address: gfx950 runs in unaligned
+// access mode and the wave's 64 consecutive 16-B loads still coalesce into whole cache lines
+// (profiles/r01_shift_probe.jsonl: 13 MB at src 4 mod 16, 6.02 us vs 5.91 aligned and 6.87 for
+// the two-load funnel).  Byte-granular disagreements funnel-shift two aligned loads with
+// v_alignbyte_b32.  The shift is uniform per segment, so the per-segment loop is specialised
+// on it and no lane diverges.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -49,12 +53,17 @@ using PackArgs = PackArgsT<kMaxSegs>;
 using AqlPackArgs = PackArgsT<kMaxAqlSegs>;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 // Memory policy NT: 0 plain, 1 non-temporal loads and stores, 2/3 non-temporal loads and stores
 // written through to device (sc1) / system (sc0 sc1) scope — no L2 write-back needed before a
 // fill signal.
-template <int NT>
+template <int NT, bool DW = false>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if constexpr (DW) {  // p only 4-byte aligned
+    if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(p));
+    return *reinterpret_cast<const u32x4_a4*>(p);
+  }
   if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
   return *reinterpret_cast<const u32x4*>(p);
 }
@@ -93,16 +102,16 @@ __device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
   return o;
 }
 
-// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned.  U loads of
-// 16 B per lane in flight before the stores.
-template <int U, int NT>
+// Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned (DW: 4-aligned).
+// U loads of 16 B per lane in flight before the stores.
+template <int U, int NT, bool DW = false>
 __device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) v[u] = ld16<NT>(sp + 16 * i);
+      if (i < nunits) v[u] = ld16<NT, DW>(sp + 16 * i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -175,6 +184,10 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
   const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
   if (r == 0) {
     copy_aligned<U, NT>(dp, sp, nunits);
+    return;
+  }
+  if ((r & 3) == 0) {  // whole-dword disagreement: one 16-B load at the source address
+    copy_aligned<U, NT, true>(dp, sp, nunits);
     return;
   }
   const uint8_t* sbase = sp - r;
