@@ -34,6 +34,16 @@ class UnsupportedType(DoraGpuError):
     pass
 
 
+class VecU8(ctypes.Structure):
+    """Vec_uint8_t of include/dora_operator_api.h."""
+    _fields_ = [("ptr", c_void_p), ("len", c_size_t), ("cap", c_size_t)]
+
+
+class DoraResult(ctypes.Structure):
+    """DoraResult_t of include/dora_operator_api.h (error NULL: success)."""
+    _fields_ = [("error", POINTER(VecU8))]
+
+
 # name -> (restype, argtypes); `int` restype means a status code that is checked.
 _SIGS = {
     "dora_gpu_last_error": (c_char_p, []),
@@ -130,6 +140,15 @@ _SIGS = {
     "dora_node_send_profile": (c_int, [c_void_p, POINTER(c_double), c_size_t, POINTER(c_uint64)]),
     "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),
                                      POINTER(c_uint64)]),
+    # shared-library operator helpers (include/dora_operator_api.h; used by operators)
+    "dora_read_input_id": (c_void_p, [c_void_p]),
+    "dora_free_input_id": (None, [c_void_p]),
+    "dora_read_data": (VecU8, [c_void_p]),
+    "dora_free_data": (None, [VecU8]),
+    "dora_send_operator_output": (DoraResult, [c_void_p, c_char_p, c_void_p, c_size_t]),
+    "dora_input_arrow": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "dora_send_operator_output_arrow": (DoraResult, [c_void_p, c_char_p, c_void_p, c_void_p]),
+    "dora_operator_error": (DoraResult, [c_char_p]),
     # daemon
     "dora_daemon_create": (c_int, [c_char_p, c_char_p, c_size_t, POINTER(c_void_p)]),
     "dora_daemon_run": (c_int, [c_void_p, c_int64]),

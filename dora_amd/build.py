@@ -18,7 +18,7 @@ INCLUDE = os.path.join(ROOT, "include")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
-LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp", "bcast.cpp",
+LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp", "bcast.cpp", "operator_api.cpp", "stdout_capture.cpp",
                "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp", "aql.cpp"]
 AQL_KERNELS = "aql_kernels.hip"  # standalone gfx950 code object embedded in the library
 LIB_NAME = "libdora_gpu.so"
@@ -112,6 +112,7 @@ TOOLS = {  # binary name -> sources (linked against libdora_gpu.so, rpath $ORIGI
     "dora-gpu-bench-sink": ["tools/bench_sink.cpp"],
     "dora-gpu-relay": ["tools/relay.cpp"],
     "dora-gpu-bench-source": ["tools/bench_source.cpp"],
+    "dora-gpu-runtime": ["tools/runtime_main.cpp"],
 }
 
 
@@ -123,7 +124,7 @@ def build_tools(verbose: bool = False):
         exe = os.path.join(LIB, name)
         if _newer(exe, objs + [lib]):
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-o", exe, *objs, f"-L{LIB}", "-ldora_gpu",
-                   "-Wl,-rpath,$ORIGIN", "-lpthread", "-lrt"]
+                   "-Wl,-rpath,$ORIGIN", "-ldl", "-lpthread", "-lrt"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)

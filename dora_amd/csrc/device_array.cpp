@@ -11,6 +11,7 @@
 //                              that need CPU memory, e.g. pyarrow, which cannot import ROCm).
 #include <hip/hip_runtime_api.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -311,9 +312,11 @@ void decode_ti(Cursor& c, TiNode& t) {
 }
 
 // buffer_into_arrow_array (event.rs:61-91) on a device sample.
+// `host`: the sample is in host memory (an inline Vec sample): bitmaps from the type info stay
+// on the host.
 void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sample,
                        uint64_t sample_len, uint64_t ext_len, const std::shared_ptr<void>& keep,
-                       ArrowArray* out) {
+                       ArrowArray* out, bool host) {
   Layout l = layout_of(s->format);
   const size_t nbuf = (l.can_null ? 1 : 0) + t.bufs.size();
   if (t.bufs.size() != l.specs.size())
@@ -328,6 +331,12 @@ void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sam
         if (t.voff < sample_len || t.voff + t.vlen > ext_len)
           throw std::invalid_argument("in-sample validity outside the slot's tail");
         p->buffers[0] = sample + t.voff;
+      } else if (t.has_validity && host) {
+        void* h = std::malloc(t.validity.size() ? t.validity.size() : 1);
+        if (!h) throw std::bad_alloc();
+        p->host_owned.push_back(h);
+        if (!t.validity.empty()) std::memcpy(h, t.validity.data(), t.validity.size());
+        p->buffers[0] = h;
       } else if (t.has_validity) {
         void* d = nullptr;
         hip_ok(hipMalloc(&d, t.validity.size() ? t.validity.size() : 1), "hipMalloc validity");
@@ -354,14 +363,14 @@ void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sam
       if (t.children.size() != 1) throw std::invalid_argument("dictionary needs one child");
       p->dictionary = new ArrowArray();
       build_from_sample(t.children[0], s->dictionary, sample, sample_len, ext_len, keep,
-                        p->dictionary);
+                        p->dictionary, host);
     } else {
       if (t.children.size() != size_t(s->n_children))
         throw std::invalid_argument("type info child count does not match the data type");
       for (size_t k = 0; k < t.children.size(); ++k) {
         auto* ch = new ArrowArray();
         p->children.push_back(ch);
-        build_from_sample(t.children[k], kids[k], sample, sample_len, ext_len, keep, ch);
+        build_from_sample(t.children[k], kids[k], sample, sample_len, ext_len, keep, ch, host);
       }
     }
   } catch (...) {
@@ -374,7 +383,7 @@ void build_from_sample(const TiNode& t, const ArrowSchema* s, const uint8_t* sam
 
 // ArrayData::new_empty(data_type) on the device: zero-length buffers, one zero offset for
 // offsets buffers, children empty too.
-void build_empty(const ArrowSchema* s, ArrowArray* out) {
+void build_empty(const ArrowSchema* s, ArrowArray* out, bool host) {
   Layout l = layout_of(s->format);
   if (s->dictionary) l.offsets_first = false;
   const size_t nbuf = (l.can_null ? 1 : 0) + l.specs.size();
@@ -384,19 +393,25 @@ void build_empty(const ArrowSchema* s, ArrowArray* out) {
     for (size_t k = 0; k < l.specs.size(); ++k, ++bi) {
       const uint64_t n = (k == 0 && l.offsets_first) ? l.specs[0].width : 0;
       void* d = nullptr;
-      hip_ok(hipMalloc(&d, n ? n : 16), "hipMalloc empty");
-      p->dev_owned.push_back(d);
-      if (n) hip_ok(hipMemset(d, 0, n), "memset empty offsets");
+      if (host) {
+        d = std::calloc(1, n ? n : 16);
+        if (!d) throw std::bad_alloc();
+        p->host_owned.push_back(d);
+      } else {
+        hip_ok(hipMalloc(&d, n ? n : 16), "hipMalloc empty");
+        p->dev_owned.push_back(d);
+        if (n) hip_ok(hipMemset(d, 0, n), "memset empty offsets");
+      }
       p->buffers[bi] = d;
     }
     if (s->dictionary) {
       p->dictionary = new ArrowArray();
-      build_empty(s->dictionary, p->dictionary);
+      build_empty(s->dictionary, p->dictionary, host);
     } else {
       for (int64_t k = 0; k < s->n_children; ++k) {
         auto* ch = new ArrowArray();
         p->children.push_back(ch);
-        build_empty(s->children[k], ch);
+        build_empty(s->children[k], ch, host);
       }
     }
   } catch (...) {
@@ -424,7 +439,7 @@ int guarded(const std::function<void()>& fn) {
 
 int import_sample(const void* sample, uint64_t sample_len, const uint8_t* ti, size_t ti_len,
                   std::shared_ptr<void> keep, ArrowArray* out_array, ArrowSchema* out_schema,
-                  uint64_t ext_len) {
+                  uint64_t ext_len, bool host) {
   if (ext_len < sample_len) ext_len = sample_len;
   return guarded([&] {
     Cursor c{ti, ti_len};
@@ -435,10 +450,10 @@ int import_sample(const void* sample, uint64_t sample_len, const uint8_t* ti, si
     decode_schema(sc, out_schema);
     try {
       if (sample_len == 0) {
-        build_empty(out_schema, out_array);  // event.rs:65-67
+        build_empty(out_schema, out_array, host);  // event.rs:65-67
       } else {
         build_from_sample(root, out_schema, static_cast<const uint8_t*>(sample), sample_len,
-                          ext_len, keep, out_array);
+                          ext_len, keep, out_array, host);
       }
     } catch (...) {
       release_schema(out_schema);

@@ -37,6 +37,7 @@
 #include "dora_gpu.h"
 #include "plan.h"
 #include "shm.h"
+#include "stdout_capture.h"
 #include "trace.h"
 #include "wire.h"
 
@@ -517,6 +518,7 @@ struct dora_node {
   // RCCL broadcast groups of this node's fan-out outputs (rank 0 of each), DORA_GPU_FANOUT=rccl
   std::map<std::string, dora::BcastComm*> bcast_out;
   uint64_t bcast_seq = 0;
+  dora::StdoutCapture* stdout_capture = nullptr;  // send_stdout_as (DORA_GPU_SEND_STDOUT_AS)
 };
 
 namespace dora {
@@ -1474,6 +1476,20 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     core->ev.wait(100000);
   }
   if (device >= 0 && dora::fanout_rccl() && !n->outputs.empty()) dora::form_bcast_groups(n);
+  // send_stdout_as (spawn.rs:280-437): the descriptor names one of this node's outputs
+  if (const char* so = std::getenv("DORA_GPU_SEND_STDOUT_AS")) {
+    if (!n->outputs.count(so)) {
+      delete n;
+      return dora::fail(DORA_ERR_NOT_FOUND, "send_stdout_as names `%s`, not an output of `%s`",
+                        so, node_id);
+    }
+    std::weak_ptr<dora::NodeCore> wc = core;
+    n->stdout_capture = dora::stdout_capture_start(
+        so, [wc](uint32_t kind, const std::vector<uint8_t>& p) {
+          auto c = wc.lock();
+          return c ? c->request(kind, p) : DORA_ERR_CLOSED;
+        });
+  }
   *out = n;
   return DORA_OK;
   DORA_GUARD_END
@@ -1495,6 +1511,8 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   struct Flush {
     ~Flush() { dora::trace_flush(); }
   } flush_trace_at_end;
+  dora::stdout_capture_stop(n->stdout_capture);  // the last lines go out before the outputs close
+  n->stdout_capture = nullptr;
   std::vector<std::string> outs(n->outputs.begin(), n->outputs.end());
   dora::WBuf w;
   w.u32(static_cast<uint32_t>(outs.size()));
@@ -1709,9 +1727,10 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
   int rc = dora::ensure_local(e->data.get());
   if (rc != DORA_OK) return rc;
   DORA_GUARD_END
-  if (!e->data->has_token && !e->data->local && e->data->len)
-    return dora::fail(DORA_ERR_INVALID, "inline (host Vec) sample: read it with dora_event_data");
   std::shared_ptr<void> keep = e->data;
+  if (!e->data->has_token && !e->data->local)  // inline Vec sample: a host array over its bytes
+    return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
+                               e->meta.type_info.size(), keep, out_array, out_schema, 0, true);
   return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
                              e->meta.type_info.size(), keep, out_array, out_schema,
                              e->data->ext_len);

@@ -5,6 +5,10 @@ The descriptor follows the reference YAML (libraries/core/src/descriptor/mod.rs:
 _unstable_deploy: {gpu: N}}]`.  Input queue_size defaults to 10 (binaries/daemon/src/spawn.rs:56).
 `path: dynamic` nodes are not spawned: the caller attaches them (e.g. the benchmark process).
 GPU placement: `_unstable_deploy.gpu` (new, next to `machine`) sets DORA_GPU_DEVICE.
+Runtime nodes (`operators: [{id, shared-library | python, inputs, outputs}]`, or `operator:` with
+the default id `op`, descriptor/mod.rs:35-100) run every operator in one process —
+`dora-gpu-runtime` for shared libraries, `python -m dora_amd.operator_runtime` for Python
+operators — with inputs and outputs named `<operator>/<id>`.
 
 Processes are spawned either directly (the caller has not touched the GPU yet) or through a
 `dora_amd.launcher.Launcher` started before the caller initialised HIP.
@@ -14,6 +18,7 @@ from __future__ import annotations
 import itertools
 import os
 import shlex
+import sys
 import subprocess
 import tempfile
 import time
@@ -37,18 +42,88 @@ class NodeSpec:
     gpu: int = 0
 
 
+SINGLE_OPERATOR_DEFAULT_ID = "op"  # descriptor/mod.rs:35
+
+
+def shared_library_path(source: str, base: str) -> str:
+    """`adjust_shared_library_path` (libraries/core/src/lib.rs:14-31): `dir/name` ->
+    `dir/libname.so`; the name must carry neither the prefix nor an extension."""
+    name = os.path.basename(source)
+    if name.startswith("lib"):
+        raise ValueError("Shared library file name must not start with `lib`, prefix is added "
+                         "automatically")
+    if os.path.splitext(name)[1]:
+        raise ValueError("Shared library file name must have no extension, it is added "
+                         "automatically")
+    path = os.path.join(os.path.dirname(source), f"lib{name}.so")
+    return path if os.path.isabs(path) else os.path.join(base, path)
+
+
+def _runtime_node(n: dict, base: str) -> dict:
+    """A runtime node (`operators` / `operator`) as a plain node spawning the runtime."""
+    ops = n.get("operators")
+    if ops is None:
+        ops = [dict(n["operator"], id=n["operator"].get("id", SINGLE_OPERATOR_DEFAULT_ID))]
+    inputs, outputs, items, kinds, stdout_as = {}, [], [], set(), None
+    for op in ops:
+        oid = op["id"]
+        for inp, src in (op.get("inputs") or {}).items():
+            inputs[f"{oid}/{inp}"] = src
+        outs = [str(o) for o in op.get("outputs", [])]
+        outputs += [f"{oid}/{o}" for o in outs]
+        if "shared-library" in op:
+            kinds.add("shared-library")
+            target = shared_library_path(op["shared-library"], base)
+        elif "python" in op:
+            kinds.add("python")
+            src = op["python"]
+            target = src if os.path.isabs(src) else os.path.join(base, src)
+        else:
+            raise ValueError(f"operator `{n['id']}/{oid}` needs `shared-library` or `python`")
+        items.append(f"{oid}={target}|{','.join(outs)}")
+        if op.get("send_stdout_as"):
+            stdout_as = f"{oid}/{op['send_stdout_as']}"
+    if len(kinds) > 1:
+        raise ValueError(f"runtime node `{n['id']}` mixes shared-library and Python operators")
+    env = dict(n.get("env") or {}, DORA_GPU_OPERATORS=";".join(items))
+    r = {k: v for k, v in n.items() if k not in ("operators", "operator")}
+    if stdout_as:
+        r["send_stdout_as"] = stdout_as
+    r.update(inputs=inputs, outputs=outputs, env=env)
+    if kinds == {"python"}:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env["PYTHONPATH"] = os.pathsep.join(
+            p for p in (root, os.environ.get("PYTHONPATH", "")) if p)
+        r.update(path=sys.executable, args=["-m", "dora_amd.operator_runtime"])
+    else:
+        r.update(path="dora-gpu-runtime")
+    return r
+
+
 def parse_descriptor(desc) -> List[NodeSpec]:
+    base = os.getcwd()
     if isinstance(desc, str):
         import yaml
+        base = os.path.dirname(os.path.abspath(desc))
         with open(desc) as f:
             desc = yaml.safe_load(f)
+    single_op = {n["id"] for n in desc["nodes"] if "operator" in n}
     nodes = []
     for n in desc["nodes"]:
+        if "operators" in n or "operator" in n:
+            n = _runtime_node(n, base)
         spec = NodeSpec(id=n["id"], path=n.get("path", "dynamic"))
         args = n.get("args", [])
         spec.args = shlex.split(args) if isinstance(args, str) else list(args)
         spec.outputs = list(n.get("outputs", []))
         spec.env = {str(k): str(v) for k, v in (n.get("env") or {}).items()}
+        if n.get("send_stdout_as"):
+            # the node library sends its stdout / stderr lines on this output (spawn.rs:280-437)
+            if n["send_stdout_as"] not in spec.outputs:
+                raise ValueError(f"node `{n['id']}`: send_stdout_as `{n['send_stdout_as']}` is "
+                                 f"not one of its outputs")
+            spec.env["DORA_GPU_SEND_STDOUT_AS"] = str(n["send_stdout_as"])
+            spec.env.setdefault("PYTHONUNBUFFERED", "1")  # lines, not blocks, through the pipe
         spec.gpu = int((n.get("_unstable_deploy") or {}).get("gpu", 0))
         for inp, src in (n.get("inputs") or {}).items():
             q = DEFAULT_QUEUE_SIZE
@@ -56,6 +131,8 @@ def parse_descriptor(desc) -> List[NodeSpec]:
                 q = int(src.get("queue_size", DEFAULT_QUEUE_SIZE))
                 src = src["source"]
             node, out = src.split("/", 1)
+            if node in single_op and "/" not in out:  # `node/out` of a single-operator node
+                out = f"{SINGLE_OPERATOR_DEFAULT_ID}/{out}"
             spec.inputs[inp] = (node, out, q)
         nodes.append(spec)
     ids = [n.id for n in nodes]

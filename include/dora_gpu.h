@@ -281,7 +281,8 @@ int dora_event_type_info(const dora_event* ev, const uint8_t** type_info, size_t
 int dora_event_parameters(const dora_event* ev, const uint8_t** params, size_t* len);
 uint64_t dora_event_timestamp_ns(const dora_event* ev);
 /* RawData::into_arrow_array (event.rs:35-91): zero-copy device ArrowArray over the sample; it
- * keeps the input (and its drop token) alive until released. */
+ * keeps the input (and its drop token) alive until released.  An inline Vec sample (host-only
+ * node, < 4096 B) imports as a host ArrowArray over its bytes instead. */
 int dora_event_array(const dora_event* ev, struct ArrowArray* out_array,
                      struct ArrowSchema* out_schema);
 /* Drop the event; the drop token is reported once no array references the data any more. */
