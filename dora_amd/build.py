@@ -71,9 +71,11 @@ def _aql_blob(verbose):
     src = os.path.join(CSRC, AQL_KERNELS)
     co = os.path.join(OBJ, "aql_kernels.co")
     if _newer(co, [src, *_headers()]):
+        # kernel-argument preload: the single-segment kernels take all 56 B of arguments in
+        # SGPRs (the struct-argument kernels are not affected: their preload length stays 0)
         cmd = [HIPCC, "--genco", f"--offload-arch={ARCH}", "--offload-device-only",
-               "--no-gpu-bundle-output", "-O3", "-std=c++17", f"-I{INCLUDE}", f"-I{CSRC}", src,
-               "-o", co]
+               "--no-gpu-bundle-output", "-O3", "-std=c++17", "-mllvm",
+               "-amdgpu-kernarg-preload-count=14", f"-I{INCLUDE}", f"-I{CSRC}", src, "-o", co]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

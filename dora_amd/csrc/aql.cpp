@@ -1,6 +1,9 @@
 // Direct AQL dispatch of signalling packs (see aql.h): one HSA queue per device per process,
-// kernel arguments in a device-memory ring, the pack kernels from the code object embedded in
-// this library (aql_kernels.hip, aql_blob.S).
+// the pack kernels from the code object embedded in this library (aql_kernels.hip,
+// aql_blob.S).  Multi-segment packs read their 272-byte arguments from a device-memory ring
+// the host writes through the BAR (one HDP flush per dispatch); single-segment packs take their
+// 56 bytes preloaded into SGPRs by the command processor, from a ring in host memory (no BAR
+// write, no flush: profiles/r01_aql_preload_probe.jsonl, 0.15 vs 1.6 us of host time).
 #include "aql.h"
 
 #include <hip/hip_runtime_api.h>
@@ -27,12 +30,16 @@ namespace dora {
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
                    uint8_t* out, size_t cap, uint32_t* grid, int* unroll);
 size_t aql_args_size();
+int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
+                    uint32_t* grid, int* unroll);
 
 namespace {
 
 constexpr uint32_t kQueuePackets = 4096;
 constexpr uint32_t kRingSlots = 512;
 constexpr uint32_t kSlotBytes = 512;
+constexpr uint32_t kArgs1Bytes = 56;    // preloaded arguments of the single-segment kernels
+constexpr uint32_t kHostSlotBytes = 64;
 constexpr uint32_t kProfileSignals = 4096;
 constexpr uint32_t kProfilePrealloc = 2048;  // created when profiling is first enabled
 
@@ -52,9 +59,10 @@ struct AqlQueue {
   // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl)
   hsa_queue_t* qs[kMaxQueues] = {};
   int nq = 0;
-  uint64_t kobj[2] = {0, 0};  // u4, u8
-  uint32_t group[2] = {0, 0}, priv[2] = {0, 0};
+  uint64_t kobj[4] = {0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8
+  uint32_t group[4] = {0, 0, 0, 0}, priv[4] = {0, 0, 0, 0};
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
+  uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
   uint64_t next = 0;
   Use uses[kRingSlots];
@@ -73,6 +81,8 @@ struct Agents {
   int matches = 0;  // GPU agents at this PCI location (> 1: a partitioned GPU)
   hsa_amd_memory_pool_t pool{};
   bool pool_ok = false, pool_fine = false;
+  hsa_amd_memory_pool_t kernarg{};  // host memory the command processor reads arguments from
+  bool kernarg_ok = false;
 };
 
 hsa_status_t on_agent(hsa_agent_t a, void* p) {
@@ -113,6 +123,29 @@ hsa_status_t on_pool(hsa_amd_memory_pool_t pool, void* p) {
     f->pool_fine = fine;
   }
   return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t on_cpu_pool(hsa_amd_memory_pool_t pool, void* p) {
+  Agents* f = static_cast<Agents*>(p);
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) && !f->kernarg_ok) {
+    f->kernarg = pool;
+    f->kernarg_ok = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// DORA_GPU_AQL_PRELOAD=0: single-segment packs use the device argument ring too.
+bool preload_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_PRELOAD");
+    return !(e && *e == '0');
+  }();
+  return v;
 }
 
 void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
@@ -177,8 +210,9 @@ AqlQueue* create(int device) {
     delete a;
     return note("code object");
   }
-  const char* names[2] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd"};
-  for (int k = 0; k < 2; ++k) {
+  const char* names[4] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
+                          "dora_aql_pack1_u8.kd"};
+  for (int k = 0; k < 4; ++k) {
     hsa_executable_symbol_t sym;
     uint32_t ka = 0;
     if (hsa_executable_get_symbol_by_name(exe, names[k], &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
@@ -191,7 +225,7 @@ AqlQueue* create(int device) {
         hsa_executable_symbol_get_info(
             sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &a->priv[k]) !=
             HSA_STATUS_SUCCESS ||
-        ka != aql_args_size() || ka > kSlotBytes) {
+        ka != (k < 2 ? aql_args_size() : size_t(kArgs1Bytes)) || ka > kSlotBytes) {
       delete a;
       return note("kernel symbol / argument size");  // no hidden arguments expected
     }
@@ -224,6 +258,20 @@ AqlQueue* create(int device) {
     hsa_amd_memory_pool_free(ring);
     delete a;
     return note("queue");
+  }
+  // host-memory argument ring of the single-segment kernels (their arguments are preloaded once
+  // per dispatch by the command processor, so no wave reads them over PCIe)
+  hsa_amd_agent_iterate_memory_pools(f.cpu, on_cpu_pool, &f);
+  void* hr = nullptr;
+  if (preload_enabled() && f.kernarg_ok &&
+      hsa_amd_memory_pool_allocate(f.kernarg, size_t(kRingSlots) * kHostSlotBytes, 0, &hr) ==
+          HSA_STATUS_SUCCESS) {
+    if (hsa_amd_agents_allow_access(1, &f.gpu, nullptr, hr) == HSA_STATUS_SUCCESS) {
+      std::memset(hr, 0, size_t(kRingSlots) * kHostSlotBytes);
+      a->hring = static_cast<uint8_t*>(hr);
+    } else {
+      hsa_amd_memory_pool_free(hr);
+    }
   }
   hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &a->ts_freq);
   return a;
@@ -303,7 +351,10 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   uint8_t args[kSlotBytes];
   uint32_t grid = 0;
   int unroll = 4;
-  int rc = build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll);
+  // one segment at sample offset 0: the preloaded kernels, arguments from host memory
+  const bool one = a->hring && n == 1 && segs[0].dst_off == 0;
+  int rc = one ? build_aql_args1(segs[0], dst, sig, args, &grid, &unroll)
+               : build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll);
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};
   static const bool no_prof = [] {
@@ -322,12 +373,19 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
       a->used_sigs.push_back(done);
     }
   }
-  uint8_t* slot = a->ring + r * kSlotBytes;
-  std::memcpy(slot, args, aql_args_size());
-  // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both are
-  // posted writes ordered before the doorbell
-  __builtin_ia32_sfence();
-  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
+  uint8_t* slot;
+  if (one) {
+    // coherent host memory: ordered before the packet header's release store (x86 TSO)
+    slot = a->hring + r * kHostSlotBytes;
+    std::memcpy(slot, args, kArgs1Bytes);
+  } else {
+    slot = a->ring + r * kSlotBytes;
+    std::memcpy(slot, args, aql_args_size());
+    // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both
+    // are posted writes ordered before the doorbell
+    __builtin_ia32_sfence();
+    *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
+  }
   hsa_queue_t* const q = a->qs[a->next % uint64_t(a->nq)];
   const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
   const auto t0 = std::chrono::steady_clock::now();
@@ -337,7 +395,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
       return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
   }
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  const int k = unroll == 8 ? 1 : 0;
+  const int k = (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;

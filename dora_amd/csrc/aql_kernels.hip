@@ -15,3 +15,45 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u4(AqlPackA
 extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u8(AqlPackArgs a) {
   dora::pack::pack_body<8, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
 }
+
+// Single-segment packs (a UInt8 payload at sample offset 0: send_output_raw / _bytes, the C2
+// benchmark) with every argument in SGPRs: the 56 bytes below are preloaded by the command
+// processor once per dispatch (gfx950 kernarg preload, built with
+// -mllvm -amdgpu-kernarg-preload-count=14), so they can sit in host memory — no BAR writes and
+// no HDP flush per send (aql.cpp; profiles/r01_aql_preload_probe.jsonl: 0.15 vs 1.6 us host
+// time per dispatch at the same device time).  The chunk count is derived here as
+// build_aql_args derives it for one segment.
+template <int U>
+__device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t len,
+                                      uint64_t* flag, uint32_t* done, uint64_t epoch,
+                                      uint32_t chunk_bytes, uint32_t grid) {
+  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  const uint64_t A0 = (base + 15) & ~uint64_t(15);
+  const uint64_t A1 = (base + len) & ~uint64_t(15);
+  const uint64_t body = A1 > A0 ? A1 - A0 : 0;
+  const uint64_t nc = body ? (body + chunk_bytes - 1) / chunk_bytes : 1;
+  dora::pack::PackArgsT<1> a;
+  a.dst = dst;
+  a.flag = flag;
+  a.done = done;
+  a.epoch = epoch;
+  a.n_chunks = static_cast<uint32_t>(nc);
+  a.nseg = 1;
+  a.chunk_bytes = chunk_bytes;
+  a.grid = grid;
+  a.chunk_end[0] = static_cast<uint32_t>(nc);
+  a.seg[0] = {src, 0, len};
+  dora::pack::pack_body<U, 2>(a, __builtin_amdgcn_workgroup_id_x(), grid);
+}
+
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u4(
+    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
+    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
+  pack1<4>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
+}
+
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u8(
+    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
+    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
+  pack1<8>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
+}

@@ -418,6 +418,37 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   return DORA_OK;
 }
 
+// Arguments of the preloaded single-segment AQL kernels (aql_kernels.hip dora_aql_pack1_*):
+// dst, src, len, flag, done, epoch, chunk_bytes, grid — 56 bytes, the same chunk shape and grid
+// build_aql_args chooses for one segment at sample offset 0.
+int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
+                    uint32_t* grid_out, int* unroll_out) {
+  if (sg.op != SEG_COPY || sg.dst_off != 0)
+    return fail(DORA_ERR_INVALID, "AQL single-segment pack: segment at offset %llu",
+                (unsigned long long)sg.dst_off);
+  Variant var = pack_variant();
+  if (var.unroll == 0) var.unroll = (sg.len >= (8u << 20) && sg.len < (32u << 20)) ? 8 : 4;
+  const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, var.unroll);
+  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  const uint64_t A0 = (base + 15) & ~uint64_t(15);
+  const uint64_t A1 = (base + sg.len) & ~uint64_t(15);
+  const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
+  const uint64_t chunks = std::max<uint64_t>(1, (bodyb + chunk_bytes - 1) / chunk_bytes);
+  if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
+  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  const uint64_t words[6] = {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(sg.src),
+                             sg.len, reinterpret_cast<uintptr_t>(sig.flag),
+                             reinterpret_cast<uintptr_t>(sig.done), sig.epoch};
+  std::memcpy(out, words, sizeof(words));
+  std::memcpy(out + 48, &chunk_bytes, 4);
+  std::memcpy(out + 52, &grid, 4);
+  *grid_out = grid;
+  *unroll_out = var.unroll == 8 ? 8 : 4;
+  return DORA_OK;
+}
+
 int launch_csum(const void* data, size_t len, uint64_t* out_dev, hipStream_t stream) {
   DORA_HIP(hipMemsetAsync(out_dev, 0, sizeof(uint64_t), stream));
   if (len) {

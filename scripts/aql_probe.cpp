@@ -149,7 +149,8 @@ int main() {
     return 2;
   }
   // code object
-  std::ifstream in("build/aql_kernel.co", std::ios::binary);
+  const char* co_path = std::getenv("CO") ? std::getenv("CO") : "build/aql_kernel.co";
+  std::ifstream in(co_path, std::ios::binary);
   std::vector<char> co((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
   if (co.empty()) {
     std::printf("build/aql_kernel.co missing\n");
@@ -364,9 +365,9 @@ int main() {
     const double us = (now_us() - t0) / N;
     std::printf("{\"path\": \"aql-%s-f%d\", \"size\": %zu, \"dispatch_host_us_p50\": %.3f, "
                 "\"isolated_flag_latency_us_p50\": %.2f, \"b2b_us_per_msg\": %.3f, "
-                "\"b2b_host_us\": %.3f, \"TBps_2S\": %.3f}\n",
+                "\"b2b_host_us\": %.3f, \"TBps_2S\": %.3f, \"queues\": %d, \"code_object\": \"%s\"}\n",
                 hdp ? (nq == 1 ? "devka-hdp" : nq == 2 ? "devka-hdp-q2" : "devka-hdp-q3") : dev_ka ? "devka" : "hostka", acq2 * 10 + rel, S, host_cost[host_cost.size() / 2], lat[lat.size() / 2], us, hc / N,
-                2.0 * S / (us * 1e-6) / 1e12);
+                2.0 * S / (us * 1e-6) / 1e12, nq, co_path);
     std::fflush(stdout);
   }
   HSA(hsa_queue_destroy(q));
