@@ -18,9 +18,11 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <memory_resource>
 #include <set>
 #include <sstream>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -51,16 +53,20 @@ struct DNode {
   std::deque<std::pair<uint32_t, std::vector<uint8_t>>> drop_overflow;
 };
 
+// A sample's drop token: its owner and the receivers still holding it, one bit per node
+// (kMaxNodes = 64), so routing a message allocates nothing for the refcount.
 struct TokenInfo {
-  int owner;
-  std::set<int> pending;
+  int owner = -1;
+  uint64_t pending = 0;
 };
+static_assert(kMaxNodes <= 64, "pending receivers are a 64-bit mask");
 
 }  // namespace
 
 class Daemon {
  public:
   Daemon(const std::string& shm, const std::string& spec, uint64_t ring_cap) {
+    outputs_.resize(kMaxNodes);
     parse(spec);
     std::vector<std::string> ids;
     for (auto& n : nodes_) ids.push_back(n.id);
@@ -187,7 +193,7 @@ class Daemon {
       if (!nodes_[idx[x.src]].outputs.count(x.out))
         throw std::invalid_argument("input " + x.node + "/" + x.input + " maps unknown output " +
                                     x.src + "/" + x.out);
-      mappings_[{idx[x.src], x.out}].push_back({idx[x.node], x.input});
+      outputs_[idx[x.src]][x.out].push_back({idx[x.node], x.input});
     }
   }
 
@@ -198,16 +204,23 @@ class Daemon {
   }
 
   void push_event(int node, uint32_t kind, std::vector<uint8_t> payload) {
-    DNode& n = nodes_[node];
-    if (n.done) return;
-    if (n.ev_overflow.empty() && ev_[node].try_push(kind, payload.data(), payload.size())) return;
-    n.ev_overflow.emplace_back(kind, std::move(payload));
+    push_event_raw(node, kind, payload.data(), payload.size());
+  }
+
+  // Straight into the node's ring; copied only when the ring is full (overflow queue).
+  void push_event_raw(int node, uint32_t kind, const uint8_t* p, size_t n) {
+    DNode& d = nodes_[node];
+    if (d.done) return;
+    if (d.ev_overflow.empty() && ev_[node].try_push(kind, p, n)) return;
+    d.ev_overflow.emplace_back(kind, std::vector<uint8_t>(p, p + n));
   }
 
   void push_drop(int node, const DropToken& t) {
-    WBuf w;
-    w.token(t);
-    push_drop_record(node, DROP_OUTPUT_DROPPED, std::move(w.b));
+    DNode& n = nodes_[node];
+    if (n.done) return;
+    if (n.drop_overflow.empty() && drop_[node].try_push(DROP_OUTPUT_DROPPED, t.b, sizeof(t.b)))
+      return;
+    n.drop_overflow.emplace_back(DROP_OUTPUT_DROPPED, std::vector<uint8_t>(t.b, t.b + sizeof(t.b)));
   }
 
   void push_drop_record(int node, uint32_t kind, std::vector<uint8_t> payload) {
@@ -256,12 +269,16 @@ class Daemon {
         }
         break;
       case REQ_SEND_MESSAGE: {
-        const std::string output = r.str();
-        const size_t meta_start = r.pos();
-        const std::vector<uint8_t> meta = r.bytes();
-        (void)meta_start;
+        // [str output][bytes metadata][data]: the event a receiver gets is [str input] + the
+        // same metadata and data bytes, forwarded verbatim
+        const uint64_t olen = r.u64();
+        r.need(olen);
+        const std::string_view output(reinterpret_cast<const char*>(r.ptr()), olen);
+        r.skip(olen);
+        const size_t tail = r.pos();
+        r.skip(r.u64());  // metadata
         const DataMsg data = r.data();
-        send_out(i, output, meta, data);
+        send_out(i, output, payload.data() + tail, payload.size() - tail, data);
         break;
       }
       case REQ_REPORT_DROP_TOKENS: {
@@ -270,7 +287,11 @@ class Daemon {
           const DropToken t = r.token();
           auto it = tokens_.find(t);
           if (it == tokens_.end()) continue;  // unknown drop token (warned in the reference)
-          if (it->second.pending.erase(i)) check_drop_token(t);
+          const uint64_t bit = uint64_t(1) << i;
+          if (it->second.pending & bit) {
+            it->second.pending &= ~bit;
+            check_drop_token(t);
+          }
         }
         break;
       }
@@ -295,32 +316,31 @@ class Daemon {
   }
 
   // send_output_to_local_receivers (lib.rs:1314-1390), minus the F8 payload copy.
-  void send_out(int i, const std::string& output, const std::vector<uint8_t>& meta,
+  // `tail`: the message's metadata + data bytes as the sender encoded them.
+  void send_out(int i, std::string_view output, const uint8_t* tail, size_t tail_len,
                 const DataMsg& data) {
-    auto it = mappings_.find({i, output});
     ++routed_;
-    if (it != mappings_.end()) {
+    TokenInfo* ti = nullptr;
+    if (data.has_token()) {  // inserted even with no local receivers
+      ti = &tokens_[data.ipc.token];
+      ti->owner = i;
+    }
+    auto it = outputs_[i].find(output);
+    if (it != outputs_[i].end()) {
       for (const Receiver& rc : it->second) {
         DNode& rn = nodes_[rc.node];
         if (!rn.subscribed || rn.done || !rn.open_inputs.count(rc.input)) continue;
-        WBuf w;
-        w.str(rc.input);
-        w.bytes(meta);
-        w.data(data);
-        push_event(rc.node, EV_INPUT, std::move(w.b));
-        if (data.has_token()) trace(TP_ROUTED, data.ipc.token);
-        if (data.has_token()) {
-          auto& ti = tokens_[data.ipc.token];
-          ti.owner = i;
-          ti.pending.insert(rc.node);
+        ev_buf_.b.clear();
+        ev_buf_.str(rc.input);
+        ev_buf_.raw(tail, tail_len);
+        push_event_raw(rc.node, EV_INPUT, ev_buf_.b.data(), ev_buf_.b.size());
+        if (ti) {
+          trace(TP_ROUTED, data.ipc.token);
+          ti->pending |= uint64_t(1) << rc.node;
         }
       }
     }
-    if (data.has_token()) {
-      auto& ti = tokens_[data.ipc.token];  // inserted even with no local receivers
-      ti.owner = i;
-      check_drop_token(data.ipc.token);
-    }
+    if (ti) check_drop_token(data.ipc.token);
   }
 
   // REQ_BCAST_GROUP (bcast.h): admit an RCCL group for output `output` of node `i` when every
@@ -332,8 +352,8 @@ class Daemon {
     std::set<int32_t> devs{root_dev};
     std::vector<Receiver> members;
     bool ok = root_dev >= 0 && nodes_[i].outputs.count(output);
-    auto it = mappings_.find({i, output});
-    if (ok && it != mappings_.end()) {
+    auto it = outputs_[i].find(output);
+    if (ok && it != outputs_[i].end()) {
       for (const Receiver& rc : it->second) {
         const DNode& rn = nodes_[rc.node];
         const int32_t d = h->nodes[rc.node].device.load();
@@ -363,7 +383,7 @@ class Daemon {
 
   void check_drop_token(const DropToken& t) {
     auto it = tokens_.find(t);
-    if (it == tokens_.end() || !it->second.pending.empty()) return;
+    if (it == tokens_.end() || it->second.pending) return;
     const int owner = it->second.owner;
     tokens_.erase(it);
     push_drop(owner, t);
@@ -372,8 +392,8 @@ class Daemon {
 
   void close_output(int i, const std::string& output) {
     if (!nodes_[i].outputs.erase(output)) return;
-    auto it = mappings_.find({i, output});
-    if (it == mappings_.end()) return;
+    auto it = outputs_[i].find(output);
+    if (it == outputs_[i].end()) return;
     for (const Receiver& rc : it->second) {
       DNode& rn = nodes_[rc.node];
       if (!rn.open_inputs.erase(rc.input)) continue;
@@ -396,8 +416,12 @@ class Daemon {
     region_->hdr()->nodes[i].state.store(2);
     // a finished receiver holds nothing any more: release its pending tokens
     std::vector<DropToken> touched;
+    const uint64_t bit = uint64_t(1) << i;
     for (auto& kv : tokens_)
-      if (kv.second.pending.erase(i)) touched.push_back(kv.first);
+      if (kv.second.pending & bit) {
+        kv.second.pending &= ~bit;
+        touched.push_back(kv.first);
+      }
     for (auto& t : touched) check_drop_token(t);
     if (!ready_sent_) {  // a node that exits before subscribing must not stall the others
       bool all = true;
@@ -419,8 +443,12 @@ class Daemon {
 
   std::unique_ptr<Region> region_;
   std::vector<DNode> nodes_;
-  std::map<std::pair<int, std::string>, std::vector<Receiver>> mappings_;
-  std::unordered_map<DropToken, TokenInfo, DropTokenHash> tokens_;
+  // per node: output -> receivers (heterogeneous lookup: no string built per message)
+  std::vector<std::map<std::string, std::vector<Receiver>, std::less<>>> outputs_;
+  // tokens in flight; nodes come from a pool (no malloc per routed message)
+  std::pmr::unsynchronized_pool_resource token_pool_;
+  std::pmr::unordered_map<DropToken, TokenInfo, DropTokenHash> tokens_{&token_pool_};
+  WBuf ev_buf_;  // event encoding scratch, reused
   std::vector<RingReader> req_;
   std::vector<RingWriter> ev_, drop_;
   bool ready_sent_ = false;

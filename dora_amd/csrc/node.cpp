@@ -23,6 +23,7 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <memory_resource>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -489,7 +490,11 @@ struct dora_node {
   std::set<std::string> outputs;
   std::map<std::string, uint32_t> queue_size;
   std::deque<dora::Slot*> cache;
-  std::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out;
+  // samples sent, by drop token (map nodes from a pool: no malloc per send)
+  std::pmr::unsynchronized_pool_resource sent_pool;
+  std::pmr::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out{&sent_pool};
+  dora::WBuf send_buf;                 // request encoding scratch of send_sample, reused
+  std::vector<uint8_t> ti_buf;         // type-info scratch of pack_and_send, reused
   std::deque<std::unique_ptr<dora_event>> queue;
   bool ended = false;
   // profiling of the pack kernel on the node stream
@@ -1018,8 +1023,8 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     }
     delete sample;
   }
-  WBuf w;
-  w.b.reserve(256 + ti.size() + params_len);
+  WBuf& w = n->send_buf;
+  w.b.clear();
   w.str(output_id);
   put_metadata(w, ti, params, params_len, ts);
   w.data(d);
@@ -1352,7 +1357,8 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     }
     t2 = t3 = mono_ns();
   }
-  std::vector<uint8_t> ti;
+  std::vector<uint8_t>& ti = n->ti_buf;
+  ti.clear();
   serialize_type_info(plan->root, ti);
   DropToken tok{};
   const bool traced = trace_enabled() && s->slot;
