@@ -573,6 +573,14 @@ int handle_finished_drop_tokens(dora_node* n) {  // mod.rs:348-362
   return DORA_OK;
 }
 
+// Slots are whole 2 MiB allocations: HIP sub-allocates smaller hipMallocs from shared blocks,
+// and an IPC import of such a slot failed ("invalid device pointer") when the exporting process
+// freed other memory of the block meanwhile (two nodes in one process, r01).
+uint64_t slot_bytes(uint64_t len) {
+  constexpr uint64_t kSlotGrain = 2ull << 20;
+  return (std::max<uint64_t>(len, 1) + kSlotGrain - 1) / kSlotGrain * kSlotGrain;
+}
+
 int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   // best fit among cached slots, iterating newest-first like `.rev()...min_by_key`
   int best = -1;
@@ -589,7 +597,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   auto* s = new Slot();
   s->cap = len;
   s->id = own_slots().next_id.fetch_add(1);
-  hipError_t e = hipMalloc(&s->ptr, (len + 4095) / 4096 * 4096);
+  hipError_t e = hipMalloc(&s->ptr, slot_bytes(len));
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
   if (e == hipSuccess && async_sends()) {
     if (n->core->region_dev && !n->core->free_flags.empty()) {
@@ -726,7 +734,10 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
             hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
             if (e != hipSuccess) {
               ev->type = DORA_EVENT_ERROR;
-              ev->error = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e);
+              ev->error = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e) +
+                          " (slot " + std::to_string(d.ipc.slot_id) + " of pid " +
+                          std::to_string(d.ipc.owner_pid) + " on GPU " +
+                          std::to_string(d.ipc.device) + ", " + std::to_string(d.ipc.len) + " B)";
               base = nullptr;
             } else {
               n->core->ipc_cache[key] = base;

@@ -110,6 +110,7 @@ class DeviceArray:
     def __init__(self, array: ArrowArray, arrow_type, keepalive=None):
         self.array, self.type = array, arrow_type
         self._keepalive = keepalive
+        self._schema = None  # exported once, lent to every send (borrowed by the C ABI)
 
     @classmethod
     def from_pyarrow(cls, arr) -> "DeviceArray":
@@ -123,6 +124,14 @@ class DeviceArray:
         s = ArrowSchema()
         self.type._export_to_c(ctypes.addressof(s))
         return s
+
+    def borrowed_schema(self) -> ArrowSchema:
+        """This array's ArrowSchema, exported once and kept until close(): for calls that only
+        borrow it (dora_node_send_output, plans).  A nested type's export costs ~4 us, more
+        than the rest of a Python send."""
+        if self._schema is None:
+            self._schema = self.export_schema()
+        return self._schema
 
     def to_pyarrow(self):
         """Download to host memory and import into pyarrow (F12: pyarrow cannot import ROCm)."""
@@ -156,6 +165,9 @@ class DeviceArray:
 
     def close(self):
         release_array(self.array)
+        if self._schema is not None:
+            release_schema(self._schema)
+            self._schema = None
         self._keepalive = None
 
     def __del__(self):

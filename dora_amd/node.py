@@ -146,13 +146,8 @@ class Node:
             call("dora_node_send_output_bytes", self.handle, oid, buf, len(data), ARROW_DEVICE_CPU,
                  pb, len(params))
         elif isinstance(data, DeviceArray):
-            s = data.export_schema()
-            try:
-                call("dora_node_send_output", self.handle, oid, byref(data.array), byref(s),
-                     ARROW_DEVICE_ROCM, pb, len(params))
-            finally:
-                from .arrow_c import release_schema
-                release_schema(s)
+            call("dora_node_send_output", self.handle, oid, byref(data.array),
+                 byref(data.borrowed_schema()), ARROW_DEVICE_ROCM, pb, len(params))
         elif isinstance(data, DeviceBuffer):
             call("dora_node_send_output_bytes", self.handle, oid, data.ptr, data.size,
                  ARROW_DEVICE_ROCM, pb, len(params))

@@ -361,11 +361,14 @@ def test_python_forward(launcher, tmp_path):
             ref.free()
             for k in range(3):
                 node.send_output("data", da, {"csum": to_i64(c), "verify": True, "seq": k})
+        # frees in this process (the cloud, the node's slots) race the sink's import of the
+        # relay's newest slot: slots are whole 2 MiB allocations so that import cannot fail
         node.close()
         t.join(60)
         codes = df.wait(60)
+        sink_log = df.log("sink")
     assert not relay_err, relay_err
-    assert codes["sink"] == 0
+    assert codes["sink"] == 0, (codes, sink_log)
     out = json.load(open(res))
     assert sum(x["verified"] for x in out["series"]) == 3
     assert sum(x["mismatches"] for x in out["series"]) == 0
