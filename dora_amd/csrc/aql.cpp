@@ -56,7 +56,11 @@ struct AqlQueue {
   std::mutex mu;
   hsa_agent_t gpu{};
   // Packs rotate over these hardware queues: one queue overlaps consecutive packs only partly
-  // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl)
+  // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl),
+  // and the command processor's per-queue dispatch rate bounds a pipeline of <= 8 messages in
+  // flight (traces: ~12 us from dispatch to fill flag at 2 queues).  4 queues by default
+  // (DORA_GPU_AQL_QUEUES): 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s, the 40.96 MB
+  // headline (HIP fill streams) unchanged (profiles/r01_aql_queues_ab.jsonl).
   hsa_queue_t* qs[kMaxQueues] = {};
   int nq = 0;
   uint64_t kobj[4] = {0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8
@@ -247,7 +251,7 @@ AqlQueue* create(int device) {
   __builtin_ia32_sfence();
   (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
   const char* qe = std::getenv("DORA_GPU_AQL_QUEUES");
-  const int want = std::max(1, std::min(kMaxQueues, qe ? std::atoi(qe) : 2));
+  const int want = std::max(1, std::min(kMaxQueues, qe ? std::atoi(qe) : kMaxQueues));
   for (int i = 0; i < want; ++i) {
     if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
