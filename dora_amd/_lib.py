@@ -137,6 +137,7 @@ _SIGS = {
                                       POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
                                       POINTER(c_char_p)]),
     "dora_node_forward": (c_int, [c_void_p, c_char_p, c_void_p, c_char_p, c_size_t]),
+    "dora_node_forward_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_send_profile": (c_int, [c_void_p, POINTER(c_double), c_size_t, POINTER(c_uint64)]),
     "dora_node_pack_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_double),
                                      POINTER(c_uint64)]),

@@ -524,6 +524,11 @@ struct dora_node {
   std::map<std::string, dora::BcastComm*> bcast_out;
   uint64_t bcast_seq = 0;
   dora::StdoutCapture* stdout_capture = nullptr;  // send_stdout_as (DORA_GPU_SEND_STDOUT_AS)
+  // zero-copy forwards: the input re-sent in place, kept (and its producer's token held) until
+  // the forward's own token returns
+  std::unordered_map<dora::DropToken, std::shared_ptr<dora::InputData>, dora::DropTokenHash>
+      forwarded;
+  uint64_t zero_copy_forwards = 0;
 };
 
 namespace dora {
@@ -555,6 +560,11 @@ void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
 
 void on_token(dora_node* n, const DropToken& t) {
   trace(TP_TOKEN_BACK, t);
+  auto f = n->forwarded.find(t);
+  if (f != n->forwarded.end()) {  // a zero-copy forward: release the input it re-sent
+    n->forwarded.erase(f);
+    return;
+  }
   auto it = n->sent_out.find(t);
   if (it == n->sent_out.end()) return;  // "received unknown finished drop token"
   Slot* s = it->second;
@@ -1228,9 +1238,50 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
 // Re-send a received input on an output with its type info (a relay stage): one copy into a
 // fresh slot of this node — for a cross-GPU input straight from the peer's slot over xGMI, so
 // a pipeline hop moves the payload once.
+// DORA_GPU_FORWARD_COPY=1: relays always copy (no in-place re-send).
+bool forward_copy_forced() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_FORWARD_COPY");
+    return e && *e && *e != '0';
+  }();
+  return v;
+}
+
+// A same-GPU device input re-sent in place: the descriptor points at the producer's slot (its
+// fill is complete: the input was handed out), under a token of this node; the input — and with
+// it the producer's token — is held until that token returns.  No copy, no new slot.
+int forward_in_place(dora_node* n, const char* output_id, const dora_event* ev,
+                     const uint8_t* params, size_t params_len) {
+  handle_finished_drop_tokens(n);
+  if (!n->outputs.count(output_id))
+    return fail(DORA_ERR_NOT_FOUND, "unknown dora node output `%s`", output_id);
+  DataMsg d;
+  d.kind = DATA_DEVICE_IPC;
+  d.ipc = ev->ipc;
+  d.ipc.token = generate_drop_token();
+  d.ipc.fill = FILL_DONE;
+  d.ipc.flag_node = d.ipc.flag_index = 0;
+  d.ipc.epoch = 0;
+  WBuf& w = n->send_buf;
+  w.b.clear();
+  w.str(output_id);
+  put_metadata(w, ev->meta.type_info, params, params_len, now_ns());
+  w.data(d);
+  int rc = n->core->request(REQ_SEND_MESSAGE, w.b);
+  if (rc != DORA_OK) return rc;
+  n->forwarded[d.ipc.token] = ev->data;
+  ++n->zero_copy_forwards;
+  trace(TP_SENT, d.ipc.token);
+  return DORA_OK;
+}
+
 int forward_input(dora_node* n, const char* output_id, const dora_event* ev, const uint8_t* params,
                   size_t params_len) {
   InputData* in = ev->data.get();
+  if (in->has_token && !in->local && in->remote_device < 0 && in->len &&
+      ev->ipc.device == n->core->device && ev->ipc.fill != FILL_BCAST && !edge_copy_forced() &&
+      !forward_copy_forced() && !n->bcast_out.count(output_id))
+    return forward_in_place(n, output_id, ev, params, params_len);
   const uint64_t len = in->len;
   const uint64_t ext = std::max(in->ext_len, len);  // the validity tail travels along
   dora_sample* s = nullptr;
@@ -1537,13 +1588,14 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   (void)n->core->request(dora::REQ_CLOSE_OUTPUTS, w.b);
   n->queue.clear();  // releases undelivered inputs (tokens reported)
   uint64_t t0 = dora::mono_ns();
-  while (!n->sent_out.empty()) {
+  while (!n->sent_out.empty() || !n->forwarded.empty()) {
     dora::handle_finished_drop_tokens(n);
-    if (n->sent_out.empty()) break;
+    if (n->sent_out.empty() && n->forwarded.empty()) break;
     if (dora::mono_ns() - t0 > dora::kDropWaitNs) break;  // "timeout while waiting for drop tokens"
     n->core->drops.wait(10000);
     if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
   }
+  n->forwarded.clear();  // inputs still held by unanswered forwards: their tokens go back
   (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
   // broadcasts read the slots: the groups go (after their streams drain, bounded) first
   for (auto& kv : n->bcast_out) dora::bcast_close(kv.second, n->core->stream, 10000);
@@ -1863,6 +1915,13 @@ int dora_node_pack_intervals(dora_node* n, double* out_ms, size_t cap, size_t* c
   const size_t pairs = n->intervals.size() / 2;
   *count = pairs;
   for (size_t i = 0; i < 2 * std::min(cap, pairs); ++i) out_ms[i] = n->intervals[i];
+  return DORA_OK;
+}
+
+int dora_node_forward_stats(dora_node* n, uint64_t* in_place, uint64_t* held) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (in_place) *in_place = n->zero_copy_forwards;
+  if (held) *held = n->forwarded.size();
   return DORA_OK;
 }
 

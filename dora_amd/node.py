@@ -244,6 +244,8 @@ class Node:
         c, b = c_uint64(), c_uint64()
         call("dora_node_peer_stats", self.handle, byref(c), byref(b))
         out["peer_copies"], out["peer_bytes"] = c.value, b.value
+        call("dora_node_forward_stats", self.handle, byref(c), byref(b))
+        out["zero_copy_forwards"], out["forwards_held"] = c.value, b.value
         return out
 
     def set_profiling(self, enable: bool = True):

@@ -293,6 +293,12 @@ void dora_event_free(dora_event* ev);
  * from the peer's slot straight into this node's new slot.  `ev` stays valid (free it after). */
 int dora_node_forward(dora_node* node, const char* output_id, const dora_event* ev,
                       const uint8_t* params, size_t params_len);
+/* A same-GPU device input is forwarded in place: the new message points at the producer's slot
+ * under a token of this node, and the input (with the producer's token) is held until that token
+ * returns — no copy, no new slot.  Cross-GPU inputs, broadcast-group inputs and
+ * DORA_GPU_FORWARD_COPY=1 copy into a fresh slot instead.  Forwards done in place, and forwards
+ * whose token has not returned yet. */
+int dora_node_forward_stats(dora_node* node, uint64_t* in_place, uint64_t* held);
 
 int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs);

@@ -346,6 +346,9 @@ def test_python_forward(launcher, tmp_path):
                     if ev["type"] == "INPUT":
                         r.forward("data", ev)
                         assert ev["type_info"].to_json()["len"] == len(cloud)
+                st = r.stats()
+                # same GPU: every forward re-sent the producer's slot in place (no new slot)
+                assert st["zero_copy_forwards"] == 3 and st["slots_created"] == 0, st
                 r.close()
             except Exception as e:  # noqa: BLE001
                 relay_err.append(e)
