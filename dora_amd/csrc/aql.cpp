@@ -50,7 +50,7 @@ struct Use {
 
 }  // namespace
 
-constexpr int kMaxQueues = 4;
+constexpr int kMaxQueues = 8;
 
 struct AqlQueue {
   std::mutex mu;
@@ -251,7 +251,7 @@ AqlQueue* create(int device) {
   __builtin_ia32_sfence();
   (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
   const char* qe = std::getenv("DORA_GPU_AQL_QUEUES");
-  const int want = std::max(1, std::min(kMaxQueues, qe ? std::atoi(qe) : kMaxQueues));
+  const int want = std::max(1, std::min(kMaxQueues, qe ? std::atoi(qe) : 4));
   for (int i = 0; i < want; ++i) {
     if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
