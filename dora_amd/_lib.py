@@ -48,6 +48,7 @@ class DoraResult(ctypes.Structure):
 _SIGS = {
     "dora_gpu_last_error": (c_char_p, []),
     "dora_gpu_version": (c_char_p, []),
+    "dora_gpu_busy_stats": (c_int, [POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),

@@ -62,6 +62,7 @@ struct AqlQueue {
   // (DORA_GPU_AQL_QUEUES): 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s, the 40.96 MB
   // headline (HIP fill streams) unchanged (profiles/r01_aql_queues_ab.jsonl).
   hsa_queue_t* qs[kMaxQueues] = {};
+  uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
   int nq = 0;
   uint64_t kobj[4] = {0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8
   uint32_t group[4] = {0, 0, 0, 0}, priv[4] = {0, 0, 0, 0};
@@ -390,13 +391,18 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     __builtin_ia32_sfence();
     *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
   }
-  hsa_queue_t* const q = a->qs[a->next % uint64_t(a->nq)];
+  const size_t qi = size_t(a->next % uint64_t(a->nq));
+  hsa_queue_t* const q = a->qs[qi];
   const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-  const auto t0 = std::chrono::steady_clock::now();
-  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
-    __builtin_ia32_pause();
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
-      return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
+  // the read index lives in host memory the CP writes: reload it (a cache miss) only when the
+  // last value seen does not already prove a free packet slot
+  if (idx - a->rd[qi] >= q->size) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (idx - (a->rd[qi] = hsa_queue_load_read_index_scacquire(q)) >= q->size) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+        return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
+    }
   }
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
   const int k = (one ? 2 : 0) + (unroll == 8 ? 1 : 0);

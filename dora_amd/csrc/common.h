@@ -17,6 +17,12 @@ void clear_error();
 // Return `code` after recording a formatted message.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Process-wide diagnostics (dora_gpu_busy_stats): host time spent blocked on an empty control
+// ring (idle) and spinning on a producer's fill flag, so a pipeline's bottleneck process shows
+// as the one with no idle time.
+void add_idle_ns(uint64_t ns);
+void add_fill_wait_ns(uint64_t ns);
+
 }  // namespace dora
 
 #define DORA_HIP(expr)                                                                  \

@@ -91,6 +91,7 @@ class Daemon {
   int run(int64_t timeout_ms) {
     const uint64_t t0 = mono_ns();
     uint64_t idle_since = mono_ns();
+    uint64_t idle_from = 0;
     uint64_t last_liveness = 0;
     std::vector<uint8_t> payload;
     RegionHdr* h = region_->hdr();
@@ -100,7 +101,7 @@ class Daemon {
         const int32_t numa = h->numa_hint.load(std::memory_order_relaxed);
         if (numa >= 0) {
           placed = true;
-          (void)pin_to_numa(numa);
+          (void)pin_to_numa(numa, -1, &h->l3_cpu, int(h->n_nodes) + 1);
         }
       }
       bool work = false;
@@ -113,18 +114,26 @@ class Daemon {
         }
       }
       work |= flush_overflow();
-      if (all_done()) return DORA_OK;
-      if (h->shutdown.load()) return DORA_ERR_CLOSED;
       const uint64_t now = mono_ns();
-      if (timeout_ms >= 0 && int64_t(now - t0) / 1000000 > timeout_ms) return DORA_ERR_TIMEOUT;
+      auto leave = [&](int rc) {
+        if (idle_from && !work) add_idle_ns(now - idle_from);
+        return rc;
+      };
+      if (all_done()) return leave(DORA_OK);
+      if (h->shutdown.load()) return leave(DORA_ERR_CLOSED);
+      if (timeout_ms >= 0 && int64_t(now - t0) / 1000000 > timeout_ms)
+        return leave(DORA_ERR_TIMEOUT);
       if (now - last_liveness > 200000000ull) {  // 200 ms: reap nodes whose process died
         check_liveness();
         last_liveness = now;
       }
       if (work) {
+        if (idle_from) add_idle_ns(now - idle_from);  // the spin/sleep that preceded this work
+        idle_from = 0;
         idle_since = now;
         continue;
       }
+      if (!idle_from) idle_from = now;
       if (int64_t(now - idle_since) / 1000 < spin_budget_us()) {
         __builtin_ia32_pause();
         continue;

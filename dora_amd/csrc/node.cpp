@@ -310,12 +310,14 @@ struct NodeCore {
   }
 
   int request(uint32_t kind, const std::vector<uint8_t>& payload) {
+    return request(kind, payload.data(), payload.size());
+  }
+  int request(uint32_t kind, const uint8_t* payload, size_t len) {
     {
       std::lock_guard<std::mutex> g(req_mu);
-      if (!req.fits(payload.size()))
-        return fail(DORA_ERR_INVALID, "message of %zu bytes exceeds the control ring",
-                    payload.size());
-      if (!req.push(kind, payload.data(), payload.size(), 30000000))
+      if (!req.fits(len))
+        return fail(DORA_ERR_INVALID, "message of %zu bytes exceeds the control ring", len);
+      if (!req.push(kind, payload, len, 30000000))
         return fail(DORA_ERR_TIMEOUT, "daemon did not drain the request ring for 30 s");
     }
     ring_doorbell();
@@ -323,10 +325,12 @@ struct NodeCore {
   }
 
   void report_drop_token(const DropToken& t) {
-    WBuf w;
-    w.u32(1);
-    w.token(t);
-    (void)request(REQ_REPORT_DROP_TOKENS, w.b);
+    // count (u32) + token, encoded on the stack: released inputs allocate nothing
+    uint8_t b[4 + sizeof(DropToken)];
+    const uint32_t one = 1;
+    std::memcpy(b, &one, 4);
+    std::memcpy(b + 4, &t, sizeof(DropToken));
+    (void)request(REQ_REPORT_DROP_TOKENS, b, sizeof(b));
   }
 
   // The stream the next fill runs on (round robin), ordered after the node stream's queued work.
@@ -517,6 +521,8 @@ struct dora_node {
   double pack_ms = 0;
   uint64_t slots_created = 0, cache_hits = 0, dropped_inputs = 0;
   // host time per send phase: allocate (incl. backpressure), launch, fill sync/record, send
+  std::vector<uint8_t> drop_buf;  // payload buffer of handle_finished_drop_tokens
+  std::vector<uint8_t> ev_buf;    // payload buffer of drain_events
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
   bool compact = false;                     // send_output uses compacting plans
@@ -574,7 +580,7 @@ void on_token(dora_node* n, const DropToken& t) {
 
 int handle_finished_drop_tokens(dora_node* n) {  // mod.rs:348-362
   uint32_t kind;
-  std::vector<uint8_t> p;
+  std::vector<uint8_t>& p = n->drop_buf;  // reused: popping a token allocates nothing
   while (n->core->drops.try_pop(&kind, &p)) {
     if (kind != DROP_OUTPUT_DROPPED) continue;
     RBuf r(p);
@@ -703,9 +709,11 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
     case EV_INPUT: {
       ev->type = DORA_EVENT_INPUT;
       ev->id = r.str();
-      std::vector<uint8_t> meta = r.bytes();
-      RBuf mr(meta);
+      const uint64_t meta_len = r.u64();
+      r.need(meta_len);
+      RBuf mr(r.ptr(), meta_len);  // parsed in place: no copy of the metadata bytes
       ev->meta = mr.metadata();
+      r.skip(meta_len);
       DataMsg d = r.data();
       auto in = std::make_shared<InputData>();
       in->core = n->core;
@@ -842,6 +850,7 @@ void finish_input(dora_node* n, dora_event* ev) {
       }
       if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
     }
+    add_fill_wait_ns(mono_ns() - t0);
   } else if (d.fill == FILL_EVENT) {
     // the producer's fill completes when its interprocess event fires
     hipEvent_t fill = nullptr;
@@ -971,7 +980,7 @@ void drop_oldest_inputs(dora_node* n) {
 
 void drain_events(dora_node* n) {
   uint32_t kind;
-  std::vector<uint8_t> p;
+  std::vector<uint8_t>& p = n->ev_buf;  // reused across events
   bool got = false;
   while (n->core->ev.try_pop(&kind, &p)) {
     encode_event(n, kind, p);
@@ -1478,7 +1487,8 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     if (dora::numa_pinning()) {
       const int numa = dora::gpu_numa_node(device);
       if (numa >= 0) {
-        (void)dora::pin_to_numa(numa);
+        dora::RegionHdr* rh = core->region->hdr();
+        (void)dora::pin_to_numa(numa, device, &rh->l3_cpu, int(rh->n_nodes) + 1);
         int32_t none = -1;
         core->region->hdr()->numa_hint.compare_exchange_strong(none, numa);
       }

@@ -5,6 +5,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +17,10 @@
 namespace dora {
 
 static thread_local char g_last_error[1024] = "no error";
+static std::atomic<uint64_t> g_idle_ns{0}, g_fill_wait_ns{0};
+
+void add_idle_ns(uint64_t ns) { g_idle_ns.fetch_add(ns, std::memory_order_relaxed); }
+void add_fill_wait_ns(uint64_t ns) { g_fill_wait_ns.fetch_add(ns, std::memory_order_relaxed); }
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -73,6 +78,12 @@ extern "C" {
 const char* dora_gpu_last_error(void) { return dora::g_last_error; }
 
 const char* dora_gpu_version(void) { return "dora-gpu 0.3.6-mi355x gfx950"; }
+
+int dora_gpu_busy_stats(uint64_t* idle_ns, uint64_t* fill_wait_ns) {
+  if (idle_ns) *idle_ns = dora::g_idle_ns.load(std::memory_order_relaxed);
+  if (fill_wait_ns) *fill_wait_ns = dora::g_fill_wait_ns.load(std::memory_order_relaxed);
+  return DORA_OK;
+}
 
 int dora_gpu_device_count(int* count) {
   if (!count) return dora::fail(DORA_ERR_INVALID, "count is NULL");

@@ -1,4 +1,5 @@
 // Shared-memory region + SPSC rings + futex waits (see shm.h).
+#include "common.h"
 #include "shm.h"
 
 #include <fcntl.h>
@@ -16,6 +17,7 @@
 #include <cstring>
 #include <new>
 #include <stdexcept>
+#include <vector>
 
 namespace dora {
 
@@ -47,32 +49,83 @@ uint64_t mono_ns() {
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
 }
 
-bool pin_to_numa(int numa) {
-  if (numa < 0) return false;
-  char path[96];
-  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", numa);
+namespace {
+
+// "0-63,128-191" -> set
+void parse_cpulist(const char* path, cpu_set_t* out) {
+  CPU_ZERO(out);
   FILE* f = std::fopen(path, "r");
-  if (!f) return false;
+  if (!f) return;
   char buf[4096];
   const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
   std::fclose(f);
   buf[n] = 0;
-  cpu_set_t want, cur;
-  CPU_ZERO(&want);
-  for (char* p = buf; *p;) {  // "0-63,128-191"
+  for (char* p = buf; *p;) {
     char* end = nullptr;
     const long a = std::strtol(p, &end, 10);
     if (end == p) break;
     long b = a;
     p = end;
     if (*p == '-') b = std::strtol(p + 1, &p, 10);
-    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(int(c), &want);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(int(c), out);
     while (*p == ',' || *p == '\n' || *p == ' ') ++p;
   }
+}
+
+bool l3_placement() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_PIN_L3");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+}  // namespace
+
+bool pin_to_numa(int numa, int device, std::atomic<int32_t>* l3_cpu, int procs) {
+  if (numa < 0) return false;
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", numa);
+  cpu_set_t want, cur, both;
+  parse_cpulist(path, &want);
   if (sched_getaffinity(0, sizeof(cur), &cur) != 0) return false;
-  cpu_set_t both;
   CPU_AND(&both, &want, &cur);
-  if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return false;
+  if (CPU_COUNT(&both) == 0) return false;
+  if (l3_cpu && procs > 0 && l3_placement()) {
+    // One L3 cache domain (a CCD) for the dataflow's processes on this NUMA node: every message
+    // hands control-ring cache lines sender -> daemon -> receiver and back, and a line moved
+    // between CCDs costs several times one moved inside an L3.  The first process picks the
+    // domain (GPU ordinal modulo the domains, so co-located dataflows spread out), the others
+    // follow its choice; a domain without two CPUs per process is not used.
+    std::vector<cpu_set_t> groups;
+    cpu_set_t seen;
+    CPU_ZERO(&seen);
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      if (!CPU_ISSET(c, &both) || CPU_ISSET(c, &seen)) continue;
+      std::snprintf(path, sizeof(path),
+                    "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
+      cpu_set_t g, gb;
+      parse_cpulist(path, &g);
+      if (CPU_COUNT(&g) == 0) CPU_SET(c, &g);
+      CPU_AND(&gb, &g, &both);
+      CPU_OR(&seen, &seen, &gb);
+      if (CPU_COUNT(&gb) > 0) groups.push_back(gb);
+    }
+    int pick = -1;
+    const int hint = l3_cpu->load(std::memory_order_acquire);
+    for (size_t i = 0; i < groups.size() && hint >= 0; ++i)
+      if (hint < CPU_SETSIZE && CPU_ISSET(hint, &groups[i])) pick = int(i);
+    if (pick < 0 && groups.size() > 1) {
+      pick = device >= 0 ? device % int(groups.size()) : 0;
+      int first = 0;
+      while (!CPU_ISSET(first, &groups[size_t(pick)])) ++first;
+      int32_t none = -1;
+      l3_cpu->compare_exchange_strong(none, first);
+    }
+    if (pick >= 0 && groups.size() > 1 && CPU_COUNT(&groups[size_t(pick)]) >= 2 * procs)
+      both = groups[size_t(pick)];
+  }
+  if (CPU_EQUAL(&both, &cur)) return false;
   return sched_setaffinity(0, sizeof(both), &both) == 0;
 }
 
@@ -140,6 +193,7 @@ Region* Region::create(const std::string& name, const std::vector<std::string>& 
   h->version = kRegionVersion;
   h->n_nodes = static_cast<uint32_t>(node_ids.size());
   h->numa_hint.store(-1);
+  new (&h->l3_cpu) std::atomic<int32_t>(-1);
   h->ring_cap = ring_cap;
   h->total_size = total;
   new (&h->doorbell) std::atomic<uint32_t>(0);
@@ -279,6 +333,13 @@ bool RingReader::try_pop(uint32_t* kind, std::vector<uint8_t>* payload) {
 bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag) {
   const uint64_t t0 = mono_ns();
   const int64_t spin = spin_budget_us();
+  struct Idle {
+    uint64_t t0;
+    bool was_empty;
+    ~Idle() {
+      if (was_empty) add_idle_ns(mono_ns() - t0);
+    }
+  } idle{t0, empty()};
   while (empty()) {
     const int64_t el = int64_t(mono_ns() - t0) / 1000;
     if (timeout_us >= 0 && el >= timeout_us) return false;

@@ -67,6 +67,8 @@ struct RegionHdr {
   std::atomic<uint32_t> shutdown;
   // NUMA node of the first GPU node to start (-1: none yet): the daemon moves next to it
   std::atomic<int32_t> numa_hint;
+  // first CPU of the L3 cache domain the dataflow's processes share (-1: none chosen yet)
+  std::atomic<int32_t> l3_cpu;
   char dataflow_id[kIdLen];
   NodeEntry nodes[kMaxNodes];
 };
@@ -135,6 +137,10 @@ uint64_t now_ns();           // CLOCK_REALTIME (timestamps that cross processes)
 uint64_t mono_ns();          // CLOCK_MONOTONIC
 // Restrict the calling thread (and threads it starts later) to the CPUs of NUMA node `numa`
 // within its current affinity; false when that would leave none or changes nothing.
-bool pin_to_numa(int numa);
+// Move the calling thread onto NUMA node `numa`'s CPUs (within its current affinity) and, when
+// `l3_cpu` is given and the node's L3 domains have room for `procs` processes, onto the one L3
+// domain the dataflow shares (DORA_GPU_PIN_L3=0: NUMA node only).
+bool pin_to_numa(int numa, int device = -1, std::atomic<int32_t>* l3_cpu = nullptr,
+                 int procs = 0);
 
 }  // namespace dora

@@ -65,6 +65,11 @@ int main() {
   dora_stream_t st = dora_node_stream(node);
   int errors = 0;
   uint64_t t_next = 0, t_free = 0, n_inputs = 0;
+  Series* last = nullptr;
+  size_t last_len = 0;
+  std::string last_id;
+  // busy = wall - idle between the first and the last input (diagnostics)
+  uint64_t w_first = 0, w_last = 0, idle_first = 0, idle_last = 0, fill_first = 0, fill_last = 0;
   for (;;) {
     dora_event* ev = nullptr;
     const uint64_t tn0 = mono();
@@ -82,11 +87,31 @@ int main() {
         ++errors;
       }
       const uint64_t t = now_ns();
+      {
+        uint64_t idle = 0, fw = 0;
+        dora_gpu_busy_stats(&idle, &fw);
+        if (!n_inputs) {
+          w_first = mono();
+          idle_first = idle;
+          fill_first = fw;
+        }
+        w_last = mono();
+        idle_last = idle;
+        fill_last = fw;
+      }
       const uint8_t* pp = nullptr;
       size_t pl = 0;
       dora_event_parameters(ev, &pp, &pl);
-      auto params = decode_params(pp, pl);
-      Series& s = stats[{dora_event_id(ev), len}];
+      std::map<std::string, Param> params;
+      if (pl) params = decode_params(pp, pl);
+      // consecutive inputs mostly share (input, size): skip the keyed lookup then
+      const char* id = dora_event_id(ev);
+      if (!last || len != last_len || last_id != id) {
+        last = &stats[{id, len}];
+        last_len = len;
+        last_id = id;
+      }
+      Series& s = *last;
       const uint64_t ts = dora_event_timestamp_ns(ev);
       s.lat_us.push_back((double(t) - double(ts)) / 1000.0);
       if (params.count("t_start"))
@@ -140,11 +165,17 @@ int main() {
   FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
   std::fprintf(f,
                "{\"errors\": %d, \"dropped_inputs\": %llu, \"next_event_us\": %.3f, "
-               "\"free_us\": %.3f, \"pulls\": %llu, \"bcast_groups\": %llu, "
+               "\"free_us\": %.3f, \"busy_us_per_input\": %.3f, "
+               "\"fill_wait_us_per_input\": %.3f, \"pulls\": %llu, \"bcast_groups\": %llu, "
                "\"bcast_received\": %llu, \"bcast_error\": \"%s\", \"series\": [",
                errors, (unsigned long long)dropped,
                n_inputs ? double(t_next) / n_inputs / 1000.0 : 0.0,
-               n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0, (unsigned long long)pulls,
+               n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0,
+               n_inputs > 1 ? (double(w_last - w_first) - double(idle_last - idle_first)) / 1e3 /
+                                  double(n_inputs - 1)
+                            : 0.0,
+               n_inputs > 1 ? double(fill_last - fill_first) / 1e3 / double(n_inputs - 1) : 0.0,
+               (unsigned long long)pulls,
                (unsigned long long)bgroups, (unsigned long long)brecv, json_safe(berr).c_str());
   bool first = true;
   for (auto& kv : stats) {

@@ -100,6 +100,16 @@ int main() {
   }
 
   int64_t seq = 0;
+  // throughput-mode messages carry default parameters, like the reference node's
+  // send_output_raw(.., Default::default(), ..): latency comes from the metadata timestamp
+  auto send_plain = [&](const char* output, uint64_t size) {
+    ++seq;
+    if (dora_node_send_output_bytes(node, output, src[size].ptr, size, ARROW_DEVICE_ROCM, nullptr,
+                                    0) != 0) {
+      std::fprintf(stderr, "source: send failed: %s\n", dora_gpu_last_error());
+      ++errors;
+    }
+  };
   auto send = [&](const char* output, uint64_t size, bool verify) {
     std::map<std::string, Param> p;
     p["seq"].i = seq++;
@@ -169,12 +179,15 @@ int main() {
 
   // throughput mode
   double tp_s = 0;
+  uint64_t idle0 = 0, idle1 = 0;
   if (ok && tp_size) {
     dora_node_set_profiling(node, 0);  // resets the send-phase counters, no kernel stamps
+    dora_gpu_busy_stats(&idle0, nullptr);
     const uint64_t t0 = mono();
-    for (long k = 0; k < tp_n; ++k) send("throughput", tp_size, false);
+    for (long k = 0; k < tp_n; ++k) send_plain("throughput", tp_size);
     ok = barrier();
     tp_s = double(mono() - t0) / 1e9;
+    dora_gpu_busy_stats(&idle1, nullptr);
   }
   double phase[4] = {0, 0, 0, 0};
   uint64_t cnt = 0;
@@ -192,12 +205,14 @@ int main() {
                "\"tp_seconds\": %.6f, \"tp_delivered_GBps\": %.3f, \"tp_per_receiver_GBps\": %.3f, "
                "\"send_phase_us\": {\"alloc_us\": %.2f, \"launch_us\": %.2f, \"fill_us\": %.2f, "
                "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu, "
-               "\"bcast_groups\": %llu, \"bcast_sent\": %llu, \"bcast_error\": \"%s\"}\n",
+               "\"bcast_groups\": %llu, \"bcast_sent\": %llu, \"bcast_error\": \"%s\", "
+               "\"tp_busy_us_per_msg\": %.3f}\n",
                errors, ok ? "true" : "false", acks, (unsigned long long)tp_size, tp_n, tp_s,
                tp_s > 0 ? delivered / tp_s / 1e9 : 0.0,
                tp_s > 0 ? double(tp_size) * double(tp_n) / tp_s / 1e9 : 0.0, phase[0], phase[1],
                phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits,
-               (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str());
+               (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str(),
+               tp_n > 0 ? (tp_s * 1e9 - double(idle1 - idle0)) / 1e3 / double(tp_n) : 0.0);
   if (f != stdout) std::fclose(f);
   for (auto& kv : src) dora_gpu_free(kv.second.ptr);
   dora_node_free(node);

@@ -1,6 +1,8 @@
 // dora-gpu-daemon: runs the data-plane daemon of one local dataflow (the `dora daemon
 // --run-dataflow` role of binaries/cli/src/main.rs:468-499, data plane only).
 //   dora-gpu-daemon --shm /name --spec FILE [--ring-bytes N] [--timeout-ms T]
+#include <time.h>
+
 #include <csignal>
 #include <cstdio>
 #include <cstdlib>
@@ -12,6 +14,11 @@
 #include "dora_gpu.h"
 
 static volatile sig_atomic_t g_stop = 0;
+static uint64_t mono_ns_main() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
 static void on_signal(int) { g_stop = 1; }
 
 int main(int argc, char** argv) {
@@ -42,6 +49,7 @@ int main(int argc, char** argv) {
   std::signal(SIGINT, on_signal);
   std::printf("{\"daemon\": \"ready\", \"shm\": \"%s\"}\n", shm.c_str());
   std::fflush(stdout);
+  const uint64_t t_start = mono_ns_main();
   int rc;
   long long waited = 0;
   bool stop_sent = false;
@@ -57,8 +65,13 @@ int main(int argc, char** argv) {
   }
   uint64_t routed = 0, pending = 0;
   dora_daemon_stats(d, &routed, &pending);
-  std::printf("{\"daemon\": \"done\", \"rc\": %d, \"routed\": %llu, \"pending_tokens\": %llu}\n", rc,
-              (unsigned long long)routed, (unsigned long long)pending);
+  uint64_t idle = 0;
+  dora_gpu_busy_stats(&idle, nullptr);
+  const double busy_us = (double(mono_ns_main() - t_start) - double(idle)) / 1e3;
+  std::printf("{\"daemon\": \"done\", \"rc\": %d, \"routed\": %llu, \"pending_tokens\": %llu, "
+              "\"busy_us\": %.1f, \"busy_us_per_routed\": %.3f}\n",
+              rc, (unsigned long long)routed, (unsigned long long)pending, busy_us,
+              routed ? busy_us / double(routed) : 0.0);
   dora_daemon_free(d);
   return rc == 0 ? 0 : 1;
 }

@@ -85,6 +85,10 @@ typedef void* dora_stream_t; /* a hipStream_t; NULL = the device's null stream *
 const char* dora_gpu_last_error(void);
 /* Library version string "dora-gpu <semver> gfx950". */
 const char* dora_gpu_version(void);
+/* Diagnostics (no reference counterpart): this process's host time blocked on empty control
+ * rings (node event/drop rings, the daemon's request rings) and spent spinning on producers'
+ * fill flags, in ns since start.  Busy time = wall - idle locates a pipeline's bottleneck. */
+int dora_gpu_busy_stats(uint64_t* idle_ns, uint64_t* fill_wait_ns);
 
 int dora_gpu_device_count(int* count);
 int dora_gpu_set_device(int ordinal);

@@ -35,10 +35,26 @@ def main():
         finally:
             df.stop()
         r = bench._load(os.path.join(tmp, "source.json")) or {}
+        sink = bench._load(os.path.join(tmp, "sink1.json")) or {}
+        dlog = df.log("_daemon")
+        dstat = {}
+        for line in dlog.splitlines():
+            if '"done"' in line:
+                try:
+                    dstat = json.loads(line)
+                except ValueError:
+                    pass
         print(json.dumps({"size": size, "n": a.n, "GBps": r.get("tp_delivered_GBps"),
                           "us_per_msg": round(size / (r["tp_delivered_GBps"] * 1e3), 3)
                           if r.get("tp_delivered_GBps") else None,
                           "send_phase_us": r.get("send_phase_us"), "ok": r.get("ok"),
+                          "busy_us_per_msg": {
+                              "source": r.get("tp_busy_us_per_msg"),
+                              "sink": sink.get("busy_us_per_input"),
+                              "sink_fill_wait": sink.get("fill_wait_us_per_input"),
+                              "sink_next_event": sink.get("next_event_us"),
+                              "sink_free": sink.get("free_us"),
+                              "daemon_per_routed": dstat.get("busy_us_per_routed")},
                           "exit_codes": codes, "env": env}), flush=True)
 
 
