@@ -44,6 +44,23 @@
 
 namespace dora {
 
+// A hipIpcMemHandle_t as a hash key without a heap allocation per lookup.
+struct IpcKey {
+  uint8_t b[64];
+  bool operator==(const IpcKey& o) const { return std::memcmp(b, o.b, 64) == 0; }
+};
+struct IpcKeyHash {
+  size_t operator()(const IpcKey& k) const {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < 64; i += 8) {
+      uint64_t w;
+      std::memcpy(&w, k.b + i, 8);
+      h = (h ^ w) * 0x100000001b3ull;
+    }
+    return static_cast<size_t>(h ^ (h >> 29));
+  }
+};
+
 namespace {
 
 constexpr size_t kMaxCacheSize = 20;          // mod.rs:365
@@ -242,7 +259,8 @@ struct NodeCore {
   RingReader drops;
   std::mutex req_mu;
   std::mutex ipc_mu;
-  std::unordered_map<std::string, void*> ipc_cache;  // handle bytes -> mapped base
+  // handle bytes -> mapped base (keyed by the whole 64-byte handle: slot ids and pids recur)
+  std::unordered_map<IpcKey, void*, IpcKeyHash> ipc_cache;
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
@@ -741,7 +759,8 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           auto it = own_slots().ptrs.find(d.ipc.slot_id);
           if (it != own_slots().ptrs.end()) base = it->second;
         } else {
-          std::string key(reinterpret_cast<const char*>(d.ipc.handle), 64);
+          IpcKey key;
+          std::memcpy(key.b, d.ipc.handle, 64);
           std::lock_guard<std::mutex> g(n->core->ipc_mu);
           auto it = n->core->ipc_cache.find(key);
           if (it != n->core->ipc_cache.end()) {
