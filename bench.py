@@ -338,6 +338,14 @@ def main():
         # spawns the cross-GPU stages / native ladder nodes after this process touched HIP
         launcher = Launcher()
 
+    # The native ladder runs before this process opens the GPU: afterwards this process keeps
+    # its HIP and AQL hardware queues, and the ladder's nodes then ran >= 16 MB ~1.4x slower
+    # (DORA_BENCH_LADDER_LATE=1 keeps the old order for A/B).
+    native = None
+    ladder_late = os.environ.get("DORA_BENCH_LADDER_LATE") == "1"
+    if native_ladder and not ladder_late:
+        native = run_native_ladder(launcher, local_rank)
+
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
     desc = {"nodes": [
@@ -507,11 +515,10 @@ def main():
     t_max = max_over_ranks(elapsed)
     total_bytes = sum_over_ranks(float(args.steps * S))
     cross = None
-    native = None
     if launcher is not None:
         if world > 1:
             cross = run_cross_gpu(world, launcher, gpu=gpu_of)
-        if native_ladder:
+        if native_ladder and ladder_late:
             native = run_native_ladder(launcher, local_rank)
         launcher.close()
     barrier()
