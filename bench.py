@@ -246,6 +246,11 @@ def run_cross_gpu(n_gpus, launcher, timeout=240.0, runs=None, **desc_kw):
 NATIVE_SIZES = [4096, 65536, 1 << 20, 4096000, 16 << 20, 40960000]
 
 
+# extra environment of the bench sink (A/B of sink-side settings, e.g. its fill streams)
+SINK_ENV = {k[len("DORA_BENCH_SINK_"):]: v for k, v in os.environ.items()
+            if k.startswith("DORA_BENCH_SINK_DORA_")}
+
+
 def run_native_ladder(launcher, gpu, n=1000, timeout=120.0):
     """Throughput mode of the native benchmark node (dora-gpu-bench-source -> -sink, one GPU,
     zero-copy edge) per size: the data plane through its C ABI, as a Rust node would bind it,
@@ -354,7 +359,8 @@ def main():
         {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
          "inputs": {"latency": {"source": "node/latency", "queue_size": 10},
                     "throughput": {"source": "node/throughput", "queue_size": 10}},
-         "env": {"DORA_BENCH_RESULT": result_path}, "_unstable_deploy": {"gpu": local_rank}},
+         "env": dict({"DORA_BENCH_RESULT": result_path}, **SINK_ENV),
+         "_unstable_deploy": {"gpu": local_rank}},
     ]}
     df = Dataflow(desc).start()
 
