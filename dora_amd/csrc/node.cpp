@@ -88,13 +88,20 @@ bool async_sends() {
 }
 
 // Samples a node may have in flight (sent, token not yet back) before an allocation waits.
-size_t max_in_flight() {
-  static const size_t v = [] {
+constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
+
+// Samples a sender may have in flight (sent, token not back) before it waits for a returned
+// slot.  Below 8 MiB a message's life is dominated by the dispatch-to-fill-flag latency
+// (~5-8 us for a 4 KB-4 MB pack over the AQL queues, scripts/trace_report.py), so the pipeline
+// depth sets the rate: 12 there, 8 for larger samples, which are HBM-bound and lose to more
+// concurrent packs (C3, 13 MB: -20 % at 12).  DORA_GPU_MAX_IN_FLIGHT sets both.
+size_t max_in_flight(uint64_t len) {
+  static const long env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
-    long x = e ? std::atol(e) : 8;
-    return static_cast<size_t>(x > 0 ? x : 8);
+    return e ? std::atol(e) : 0L;
   }();
-  return v;
+  if (env > 0) return static_cast<size_t>(env);
+  return len < kSmallInFlightBytes ? 12 : 8;
 }
 
 // Streams the sends of a node spread their fills over (DORA_GPU_FILL_STREAMS, default 3).  A
@@ -1118,7 +1125,7 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
     // After `slot_wait_ns` without a returned token the slot is allocated anyway, as the
     // reference would (a receiver may legitimately hold many inputs).
     const uint64_t t0 = mono_ns();
-    while (async_sends() && n->sent_out.size() >= max_in_flight() &&
+    while (async_sends() && n->sent_out.size() >= max_in_flight(len) &&
            mono_ns() - t0 < slot_wait_ns()) {
       n->core->drops.wait(1000);
       handle_finished_drop_tokens(n);
