@@ -594,6 +594,9 @@ def main():
                      "algorithmic_bytes_per_launch": 2 * S},
         "parity": {"verified_msgs": verified, "mismatches": mismatches},
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
+        # inputs the sink's queue (queue_size 10, the reference default) dropped, all phases:
+        # non-zero would mean the throughput ladders counted undelivered messages
+        "sink_dropped_inputs": sink.get("dropped_inputs"),
         "node_stats": stats, "exit_codes": codes,
     }
     if cross is not None:
