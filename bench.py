@@ -408,16 +408,22 @@ def main():
             node.send_output("throughput", srcs[k % nsrc], meta)
 
     def wait_ack(seq, timeout=60.0):
-        deadline = time.time() + timeout
-        while time.time() < deadline:
-            ev = node.next(timeout=1.0)
-            if ev and ev["type"] == "INPUT" and ev["id"] == "ack" and \
-                    ev["metadata"].get("seq") == seq:
-                return True
-        raise RuntimeError(f"no ack for seq {seq}")
+        node.wait_input("ack", "seq", seq, timeout)
+
+    # ---- cold start: the very first message (device queues, code object, the sink's first IPC
+    # mapping), reported on its own so the ladders below measure a warm data plane ----
+    seq = 0
+    cold_buf = device.DeviceBuffer(4096)
+    device.fill_splitmix(cold_buf.ptr, 4096, payload_seed(4096), stream)
+    stream.sync()
+    t_c = time.perf_counter()
+    node.send_output_device_bytes("throughput", cold_buf.ptr, 4096, {"seq": seq, "ack": True})
+    cold_send_us = (time.perf_counter() - t_c) * 1e6  # sender side: slot, queues, dispatch
+    wait_ack(seq)
+    cold_start_us = (time.perf_counter() - t_c) * 1e6
+    seq += 1
 
     # ---- warmup (the first messages are verified bit-exact by the sink's csum kernel) ----
-    seq = 0
     for k in range(args.warmup):
         meta = {"seq": seq, "t_start": time.time_ns()}
         if k < 3:
@@ -436,6 +442,15 @@ def main():
             device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
             ladder_bufs[size] = b
         stream.sync()
+        # every size once through the path untimed first (its slot, the sink's mapping of it)
+        for size in LADDER:
+            for _ in range(2):
+                node.send_output_device_bytes("throughput", ladder_bufs[size].ptr, size,
+                                              {"seq": seq})
+                seq += 1
+        node.send_output("throughput", b"", {"seq": seq, "ack": True})
+        wait_ack(seq)
+        seq += 1
         for size in LADDER:
             for _ in range(args.lat_n):
                 node.send_output_device_bytes("latency", ladder_bufs[size].ptr, size,
@@ -463,6 +478,7 @@ def main():
             node.send_output("throughput", b"", {"seq": seq, "ack": True})
             wait_ack(seq)
             seq += 1
+            d0 = node.dataflow_counters("sink")["dropped_inputs"]
             t_a = time.perf_counter()
             for k in range(args.tp_n):
                 node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, {"seq": seq})
@@ -471,16 +487,38 @@ def main():
             wait_ack(seq)
             seq += 1
             dt = time.perf_counter() - t_a
-            tp_ladder[str(size)] = {"GBps": round(args.tp_n * size / dt / 1e9, 2),
-                                    "msgs_per_s": round(args.tp_n / dt, 1),
-                                    "us_per_msg": round(dt / args.tp_n * 1e6, 2),
-                                    "hbm_frac_2S": round(2 * args.tp_n * size / dt / 1e9 /
-                                                         HBM_PEAK_GBPS, 4)}
+            # the sink's queue (queue_size 10, the reference default) may drop inputs when it
+            # falls behind: only delivered messages count
+            dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
+            got = args.tp_n - dropped
+            tp_ladder[str(size)] = {"GBps": round(got * size / dt / 1e9, 2),
+                                    "msgs_per_s": round(got / dt, 1),
+                                    "us_per_msg": round(dt / got * 1e6, 2),
+                                    "hbm_frac_2S": round(2 * got * size / dt / 1e9 /
+                                                         HBM_PEAK_GBPS, 4),
+                                    "dropped": dropped}
             for b in bufs:
                 b.free()
 
+    cold_buf.free()
+
+    # ---- refill: the ladders evicted the headline size's slots from the sender's 20-entry cache
+    # (and the sink's mappings of them); send the in-flight cap's worth and more untimed, so the
+    # timed region allocates and maps nothing ----
+    for k in range(2 * 12):
+        send(k, {"seq": seq})
+        seq += 1
+    node.send_output("throughput", b"", {"seq": seq, "ack": True})
+    wait_ack(seq)
+    seq += 1
+
     # ---- timed region: K back-to-back steps, closed by the sink's ack ----
+    # The last `late` messages are checksummed by the sink right after it acks the region (it
+    # holds them until then), so parity covers timed traffic without a kernel inside the region.
+    late = min(4, args.steps)
     node.set_profiling(False)  # resets the per-phase send timers: they cover the timed steps
+    sink_before = node.dataflow_counters("sink")
+    node_before = node.stats()
     barrier()
     device.set_device(local_rank)
     from dora_amd._lib import call
@@ -489,14 +527,34 @@ def main():
         node.region_begin()  # setup (profiling signals) before the clock starts
     t0 = time.perf_counter()
     for k in range(args.steps):
-        send(k, {"seq": seq, "t_start": time.time_ns()})
+        meta = {"seq": seq, "t_start": time.time_ns()}
+        if k >= args.steps - late:
+            meta.update({"csum": to_i64(csum), "verify_late": True})
+        if k == args.steps - 1:
+            meta["ack"] = True  # the sink acks the region's last message on receipt
+        send(k, meta)
         seq += 1
-    region = node.region_end() if not args.no_kernel_timing else None
-    node.send_output("throughput", b"", {"seq": seq, "ack": True})
-    wait_ack(seq)
-    call("dora_gpu_device_sync")
+    t_sent = time.perf_counter()
+    if not args.no_kernel_timing:
+        node.region_mark()  # stop events after the last pack, while it is delivered
+    wait_ack(seq - 1)
+    t_acked = time.perf_counter()
+    node.sync()  # every stream and AQL fill of this node complete (the ack implies it)
     elapsed = time.perf_counter() - t0
     barrier()
+    region = node.region_end() if not args.no_kernel_timing else None
+    sink_after = node.dataflow_counters("sink")
+    node_after = node.stats()
+    region_setup = {
+        "slots_created_in_region": node_after["slots_created"] - node_before["slots_created"],
+        "ipc_opens_in_region": sink_after["ipc_opens"] - sink_before["ipc_opens"],
+        "sink_slots_created_in_region": sink_after["slots_created"] - sink_before["slots_created"],
+        # every message counted in `value` was delivered: the sink's queue dropped none
+        "sink_dropped_in_region": sink_after["dropped_inputs"] - sink_before["dropped_inputs"],
+        "host_send_loop_us": round((t_sent - t0) * 1e6, 1),
+        "close_us": round((t_acked - t_sent) * 1e6, 1),
+        "sync_us": round((t0 + elapsed - t_acked) * 1e6, 1),
+        "late_verified_msgs": late}
     stats = node.stats()
     stats["send_phase_us"] = {k: round(v, 2) for k, v in node.send_profile().items()}
     stats["fill_paths"] = node.fill_paths()
@@ -592,7 +650,11 @@ def main():
                                                 "streams; busy = union of the intervals"},
                      "fill_streams": int(os.environ.get("DORA_GPU_FILL_STREAMS", "3")),
                      "algorithmic_bytes_per_launch": 2 * S},
-        "parity": {"verified_msgs": verified, "mismatches": mismatches},
+        "parity": {"verified_msgs": verified, "mismatches": mismatches,
+                   "timed_region_verified": verified - min(3, args.warmup)},
+        "cold_start_us": round(cold_start_us, 1),
+        "cold_start_send_us": round(cold_send_us, 1),
+        "timed_region": region_setup,
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
         # inputs the sink's queue (queue_size 10, the reference default) dropped, all phases:
         # non-zero would mean the throughput ladders counted undelivered messages

@@ -349,8 +349,10 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     const auto t0 = std::chrono::steady_clock::now();
     while (u.flag->load(std::memory_order_acquire) < u.epoch) {
       __builtin_ia32_pause();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        a->failed.store(true);  // a pack that never completes: stop dispatching here
         return fail(DORA_ERR_TIMEOUT, "AQL argument slot still in use after 5 s");
+      }
     }
   }
   uint8_t args[kSlotBytes];
@@ -393,17 +395,23 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   }
   const size_t qi = size_t(a->next % uint64_t(a->nq));
   hsa_queue_t* const q = a->qs[qi];
-  const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-  // the read index lives in host memory the CP writes: reload it (a cache miss) only when the
-  // last value seen does not already prove a free packet slot
+  // Wait for a free packet slot before reserving one: a reserved packet must be written, or the
+  // command processor stalls at its INVALID header for good.  This process is the queue's only
+  // producer (HSA_QUEUE_TYPE_SINGLE, under a->mu), so the write index cannot move meanwhile.  The
+  // read index lives in host memory the CP writes: reload it (a cache miss) only when the last
+  // value seen does not already prove a free slot.
+  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
   if (idx - a->rd[qi] >= q->size) {
     const auto t0 = std::chrono::steady_clock::now();
     while (idx - (a->rd[qi] = hsa_queue_load_read_index_scacquire(q)) >= q->size) {
       __builtin_ia32_pause();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        a->failed.store(true);  // a stuck queue: later sends take the HIP fill streams
         return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
+      }
     }
   }
+  hsa_queue_store_write_index_relaxed(q, idx + 1);
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
   const int k = (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;

@@ -53,20 +53,72 @@ struct DNode {
   std::deque<std::pair<uint32_t, std::vector<uint8_t>>> drop_overflow;
 };
 
-// A sample's drop token: its owner and the receivers still holding it, one bit per node
-// (kMaxNodes = 64), so routing a message allocates nothing for the refcount.
+// A sample's drop token: its owner and the receivers still holding it, with the number of
+// inputs each was delivered (a node may map one output under several input ids: each delivery
+// is released on its own, so the token returns only after the last one).  Up to kInline
+// receivers live in the entry itself (C4's 1 -> 7 fan-out included), so routing a message
+// allocates nothing for the refcount; wider fan-outs spill into `more`.
 struct TokenInfo {
+  static constexpr int kInline = 8;
+  struct Hold {
+    int32_t node;
+    uint32_t count;
+  };
   int owner = -1;
-  uint64_t pending = 0;
+  uint32_t n = 0;  // entries of `inl` in use
+  Hold inl[kInline];
+  std::vector<Hold> more;
+
+  Hold* find(int node) {
+    for (uint32_t k = 0; k < n; ++k)
+      if (inl[k].node == node) return &inl[k];
+    for (Hold& h : more)
+      if (h.node == node) return &h;
+    return nullptr;
+  }
+  void add(int node) {
+    if (Hold* h = find(node)) {
+      ++h->count;
+    } else if (n < kInline) {
+      inl[n++] = {node, 1};
+    } else {
+      more.push_back({node, 1});
+    }
+  }
+  void erase(Hold* h) {
+    if (h >= inl && h < inl + n) {
+      *h = inl[--n];
+      if (!more.empty()) {  // keep the inline entries dense
+        inl[n++] = more.back();
+        more.pop_back();
+      }
+    } else {
+      *h = more.back();
+      more.pop_back();
+    }
+  }
+  // One delivery to `node` released; false when `node` held none.
+  bool release(int node) {
+    Hold* h = find(node);
+    if (!h) return false;
+    if (--h->count == 0) erase(h);
+    return true;
+  }
+  // Every delivery to `node` released (the node finished); false when it held none.
+  bool release_all(int node) {
+    Hold* h = find(node);
+    if (!h) return false;
+    erase(h);
+    return true;
+  }
+  bool pending() const { return n != 0 || !more.empty(); }
 };
-static_assert(kMaxNodes <= 64, "pending receivers are a 64-bit mask");
 
 }  // namespace
 
 class Daemon {
  public:
   Daemon(const std::string& shm, const std::string& spec, uint64_t ring_cap) {
-    outputs_.resize(kMaxNodes);
     parse(spec);
     std::vector<std::string> ids;
     for (auto& n : nodes_) ids.push_back(n.id);
@@ -177,8 +229,11 @@ class Daemon {
         DNode n;
         ls >> n.id;
         if (n.id.empty() || idx.count(n.id)) throw std::invalid_argument("bad node line: " + line);
+        if (nodes_.size() >= kMaxNodes)
+          throw std::invalid_argument("more than " + std::to_string(kMaxNodes) + " nodes");
         idx[n.id] = static_cast<int>(nodes_.size());
         nodes_.push_back(n);
+        outputs_.emplace_back();
       } else if (kw == "output") {
         std::string node, out;
         ls >> node >> out;
@@ -296,11 +351,7 @@ class Daemon {
           const DropToken t = r.token();
           auto it = tokens_.find(t);
           if (it == tokens_.end()) continue;  // unknown drop token (warned in the reference)
-          const uint64_t bit = uint64_t(1) << i;
-          if (it->second.pending & bit) {
-            it->second.pending &= ~bit;
-            check_drop_token(t);
-          }
+          if (it->second.release(i)) check_drop_token(t);
         }
         break;
       }
@@ -345,7 +396,7 @@ class Daemon {
         push_event_raw(rc.node, EV_INPUT, ev_buf_.b.data(), ev_buf_.b.size());
         if (ti) {
           trace(TP_ROUTED, data.ipc.token);
-          ti->pending |= uint64_t(1) << rc.node;
+          ti->add(rc.node);
         }
       }
     }
@@ -392,7 +443,7 @@ class Daemon {
 
   void check_drop_token(const DropToken& t) {
     auto it = tokens_.find(t);
-    if (it == tokens_.end() || it->second.pending) return;
+    if (it == tokens_.end() || it->second.pending()) return;
     const int owner = it->second.owner;
     tokens_.erase(it);
     push_drop(owner, t);
@@ -425,12 +476,8 @@ class Daemon {
     region_->hdr()->nodes[i].state.store(2);
     // a finished receiver holds nothing any more: release its pending tokens
     std::vector<DropToken> touched;
-    const uint64_t bit = uint64_t(1) << i;
     for (auto& kv : tokens_)
-      if (kv.second.pending & bit) {
-        kv.second.pending &= ~bit;
-        touched.push_back(kv.first);
-      }
+      if (kv.second.release_all(i)) touched.push_back(kv.first);
     for (auto& t : touched) check_drop_token(t);
     if (!ready_sent_) {  // a node that exits before subscribing must not stall the others
       bool all = true;

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -44,14 +45,20 @@
 
 namespace dora {
 
-// A hipIpcMemHandle_t as a hash key without a heap allocation per lookup.
+// A received slot's identity as a hash key without a heap allocation per lookup: the
+// hipIpcMemHandle_t bytes plus the owner's pid and its process-unique slot id.  The handle alone
+// is not enough: a freed slot's handle encoding can recur for a new allocation of the same size.
 struct IpcKey {
   uint8_t b[64];
-  bool operator==(const IpcKey& o) const { return std::memcmp(b, o.b, 64) == 0; }
+  int32_t pid;
+  uint64_t slot;
+  bool operator==(const IpcKey& o) const {
+    return pid == o.pid && slot == o.slot && std::memcmp(b, o.b, 64) == 0;
+  }
 };
 struct IpcKeyHash {
   size_t operator()(const IpcKey& k) const {
-    uint64_t h = 0xcbf29ce484222325ull;
+    uint64_t h = 0xcbf29ce484222325ull ^ k.slot ^ (uint64_t(uint32_t(k.pid)) << 40);
     for (size_t i = 0; i < 64; i += 8) {
       uint64_t w;
       std::memcpy(&w, k.b + i, 8);
@@ -60,6 +67,22 @@ struct IpcKeyHash {
     return static_cast<size_t>(h ^ (h >> 29));
   }
 };
+
+// One hipIpcOpenMemHandle mapping of a producer's slot.  Shared by the receiver's mapping cache
+// and every input that points into it; closed when the last of them lets go, so evicting a
+// mapping from the cache never unmaps memory an input still reads.
+struct IpcMapping {
+  void* base = nullptr;
+  uint64_t last_use = 0;
+  ~IpcMapping() {
+    if (base) (void)hipIpcCloseMemHandle(base);
+  }
+};
+
+// Mappings a receiver keeps open for reuse (LRU beyond this).  Producers recycle at most
+// kMaxCacheSize (20) slots plus those in flight, so a steady edge stays within it; slots a
+// producer has freed (size changes) age out instead of pinning the producer's memory for good.
+constexpr size_t kMaxIpcMappings = 64;
 
 namespace {
 
@@ -72,8 +95,13 @@ struct Slot {
   uint64_t id = 0;
   hipIpcMemHandle_t handle;
   int flag = -1;              // FillFlag index in the node's region entry (async sends)
+  uint64_t fill_epoch = 0;    // epoch the last fill into this slot stores into `flag`
   hipEvent_t done = nullptr;  // fallback: interprocess completion event of the last fill
   hipIpcEventHandle_t done_handle;
+  // node-stream work on the slot with no fill flag (a broadcast group's pack + broadcast):
+  // recorded after it, waited on before the slot is reused or freed
+  hipEvent_t use_ev = nullptr;
+  bool use_pending = false;
 };
 
 // Async sends (default): the sender records the slot's interprocess event after the pack and
@@ -266,8 +294,24 @@ struct NodeCore {
   RingReader drops;
   std::mutex req_mu;
   std::mutex ipc_mu;
-  // handle bytes -> mapped base (keyed by the whole 64-byte handle: slot ids and pids recur)
-  std::unordered_map<IpcKey, void*, IpcKeyHash> ipc_cache;
+  // (handle, owner pid, slot id) -> open mapping; bounded LRU (kMaxIpcMappings)
+  std::unordered_map<IpcKey, std::shared_ptr<IpcMapping>, IpcKeyHash> ipc_cache;
+  uint64_t ipc_clock = 0;
+  std::atomic<uint64_t> ipc_opens{0}, ipc_closes{0};
+
+  // Drop the least recently used mappings that no input holds until the cache is within bound.
+  void trim_ipc_cache() {
+    while (ipc_cache.size() > kMaxIpcMappings) {
+      auto victim = ipc_cache.end();
+      for (auto it = ipc_cache.begin(); it != ipc_cache.end(); ++it)
+        if (it->second.use_count() == 1 &&
+            (victim == ipc_cache.end() || it->second->last_use < victim->second->last_use))
+          victim = it;
+      if (victim == ipc_cache.end()) return;  // every mapping is held by an input
+      ipc_cache.erase(victim);
+      ipc_closes.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
@@ -432,7 +476,7 @@ struct NodeCore {
     // AQL argument slots must not keep pointing at this region's fill flags once it is unmapped
     if (device >= 0 && region) aql_forget_flags(device, region->base(), region->size());
     for (auto& kv : ipc_events) (void)hipEventDestroy(kv.second);
-    for (auto& kv : ipc_cache) (void)hipIpcCloseMemHandle(kv.second);
+    ipc_cache.clear();
     for (hipStream_t s : fill_streams) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
@@ -456,6 +500,7 @@ struct InputData {
   bool has_token = false;
   DropToken token{};
   std::vector<uint8_t> vec;   // inline (Vec) samples stay on the host
+  std::shared_ptr<IpcMapping> mapping;  // the producer's slot as mapped here (IPC edges)
   void* local = nullptr;      // cross-GPU edge: local copy in this node's receive pool
   uint64_t local_cap = 0;
   int remote_device = -1;     // >= 0: `ptr` is a peer GPU's slot not yet pulled (ensure_local)
@@ -536,9 +581,10 @@ struct dora_node {
   std::vector<double> intervals;         // (start, stop) ms after timing_ref per stamped pack
   // Timed region (dora_node_region_begin/end): the first pack after begin stamps its start;
   // end records a stop event on every fill stream once the packs queued there have finished.
-  bool region_armed = false, region_started = false;
+  bool region_armed = false, region_started = false, region_marked = false;
   uint64_t region_aql = 0;  // packs of the region dispatched on the AQL queue
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
+  bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
   uint64_t region_packs = 0, region_bytes = 0;
@@ -565,17 +611,52 @@ struct dora_node {
 namespace dora {
 namespace {
 
+// A returned drop token does not prove that the slot's last fill has completed: the daemon
+// returns the token at once for an output without receivers, a receiver's drop-oldest queue
+// releases inputs it never waited on, and a finished receiver's tokens are released for it.
+// Before a slot is refilled or freed, wait for its last fill (normally long complete: one load).
+// False when the fill did not complete within `timeout_ns` — the slot must then be neither
+// reused nor freed (a kernel may still write it).
+bool wait_slot_idle(dora_node* n, Slot* s, uint64_t timeout_ns = 10000000000ull) {
+  const uint64_t t0 = mono_ns();
+  if (s->flag >= 0 && s->fill_epoch) {
+    const std::atomic<uint64_t>* f = n->core->flag_host(s->flag);
+    while (f->load(std::memory_order_acquire) < s->fill_epoch) {
+      if (mono_ns() - t0 > timeout_ns) return false;
+      __builtin_ia32_pause();
+    }
+  }
+  if (s->done && hipEventQuery(s->done) == hipErrorNotReady &&
+      hipEventSynchronize(s->done) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (s->use_pending) {
+    if (hipEventSynchronize(s->use_ev) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    s->use_pending = false;
+  }
+  return true;
+}
+
 void free_slot(dora_node* n, Slot* s) {
   if (!s) return;
   {
     std::lock_guard<std::mutex> g(own_slots().mu);
     own_slots().ptrs.erase(s->id);
   }
-  if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
-  if (s->done) {
-    (void)hipEventSynchronize(s->done);
-    (void)hipEventDestroy(s->done);
+  if (!wait_slot_idle(n, s)) {
+    // a fill that never completed may still write the slot (and its flag's done words): leak
+    // both rather than hand them to another allocation
+    std::fprintf(stderr, "dora-gpu: slot %llu: last fill did not complete; not freed\n",
+                 (unsigned long long)s->id);
+    return;
   }
+  if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
+  if (s->done) (void)hipEventDestroy(s->done);
+  if (s->use_ev) (void)hipEventDestroy(s->use_ev);
   (void)hipFree(s->ptr);
   delete s;
 }
@@ -630,10 +711,18 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
     if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) best = i;
   }
   if (best >= 0) {
-    *out = n->cache[static_cast<size_t>(best)];
+    Slot* s = n->cache[static_cast<size_t>(best)];
     n->cache.erase(n->cache.begin() + best);
-    ++n->cache_hits;
-    return DORA_OK;
+    if (wait_slot_idle(n, s)) {
+      *out = s;
+      ++n->cache_hits;
+      return DORA_OK;
+    }
+    // its last fill never completed: leak the slot (a kernel may still write it), take a new one
+    std::fprintf(stderr, "dora-gpu: slot %llu: last fill did not complete; not reused\n",
+                 (unsigned long long)s->id);
+    std::lock_guard<std::mutex> g(own_slots().mu);
+    own_slots().ptrs.erase(s->id);
   }
   auto* s = new Slot();
   s->cap = len;
@@ -662,6 +751,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
     own_slots().ptrs[s->id] = s->ptr;
   }
   ++n->slots_created;
+  n->core->region->hdr()->nodes[n->core->idx].slots_created.fetch_add(1, std::memory_order_relaxed);
   *out = s;
   return DORA_OK;
 }
@@ -768,10 +858,13 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         } else {
           IpcKey key;
           std::memcpy(key.b, d.ipc.handle, 64);
-          std::lock_guard<std::mutex> g(n->core->ipc_mu);
-          auto it = n->core->ipc_cache.find(key);
-          if (it != n->core->ipc_cache.end()) {
-            base = it->second;
+          key.pid = d.ipc.owner_pid;
+          key.slot = d.ipc.slot_id;
+          NodeCore* c = n->core.get();
+          std::lock_guard<std::mutex> g(c->ipc_mu);
+          auto it = c->ipc_cache.find(key);
+          if (it != c->ipc_cache.end()) {
+            in->mapping = it->second;
           } else {
             hipIpcMemHandle_t h;
             std::memcpy(&h, d.ipc.handle, sizeof(h));
@@ -784,8 +877,17 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
                           std::to_string(d.ipc.device) + ", " + std::to_string(d.ipc.len) + " B)";
               base = nullptr;
             } else {
-              n->core->ipc_cache[key] = base;
+              in->mapping = std::make_shared<IpcMapping>();
+              in->mapping->base = base;
+              c->ipc_cache.emplace(key, in->mapping);
+              c->ipc_opens.fetch_add(1, std::memory_order_relaxed);
+              n->core->region->hdr()->nodes[c->idx].ipc_opens.fetch_add(1, std::memory_order_relaxed);
+              c->trim_ipc_cache();
             }
+          }
+          if (in->mapping) {
+            in->mapping->last_use = ++c->ipc_clock;
+            base = in->mapping->base;
           }
         }
         if (base) in->ptr = static_cast<uint8_t*>(base) + d.ipc.offset;
@@ -995,6 +1097,8 @@ void drop_oldest_inputs(dora_node* n) {
     if (q->second == 0) {
       it->reset();  // releases the InputData -> drop token reported
       ++n->dropped_inputs;
+      n->core->region->hdr()->nodes[n->core->idx].dropped_inputs.fetch_add(
+          1, std::memory_order_relaxed);
     } else {
       --q->second;
     }
@@ -1060,6 +1164,14 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
         // every fill so far (fills of other streams / the AQL queues are fenced first)
         if (sample->fill != FILL_DONE) n->core->fence_fills();
         int rc = bcast_enqueue(g->second, slot->ptr, d.ipc.ext_len, n->core->stream);
+        // the broadcast reads the slot on the node stream: the slot is idle after it
+        if (!slot->use_ev && hipEventCreateWithFlags(&slot->use_ev, hipEventDisableTiming) != hipSuccess)
+          slot->use_ev = nullptr;
+        if (slot->use_ev && hipEventRecord(slot->use_ev, n->core->stream) == hipSuccess)
+          slot->use_pending = true;
+        else
+          (void)hipStreamSynchronize(n->core->stream);
+        (void)hipGetLastError();
         if (rc != DORA_OK) {
           add_to_cache(n, slot);
           delete sample;
@@ -1118,6 +1230,13 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
   auto* s = new dora_sample();
   s->len = len;
   if (len > 0) {
+    if (!n->aql_ready) {
+      // the first non-empty sample of this node sets up the process's AQL queues and loads the
+      // pack code object (~20 ms), whatever its size: a later small send then finds them ready
+      // instead of paying that inside its latency (nodes that never send data create none)
+      n->aql_ready = true;
+      (void)aql_queue(n->core->device);
+    }
     handle_finished_drop_tokens(n);
     // Async sends run ahead of the GPU; bound the samples in flight so the sender waits for a
     // returned slot instead of hipMalloc-ing new ones (a device slot costs far more to create
@@ -1196,6 +1315,7 @@ hipError_t order_fill(dora_node* n, dora_sample* s, hipStream_t st) {
     // completed; the receiver polls it, the sender moves on
     s->epoch = ++n->core->epoch;
     s->fill = FILL_FLAG;
+    s->slot->fill_epoch = s->epoch;
     return hipStreamWriteValue64(st, n->core->flag_dev(s->slot->flag), s->epoch, 0);
   }
   if (s->slot->done) {
@@ -1250,6 +1370,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
         ++n->aql_packs;
         s->epoch = sig.epoch;
         s->fill = FILL_FLAG;
+        s->slot->fill_epoch = sig.epoch;
         return DORA_OK;
       }
     }
@@ -1263,6 +1384,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   if (signalled) {
     s->epoch = sig.epoch;
     s->fill = FILL_FLAG;
+    s->slot->fill_epoch = sig.epoch;
     return DORA_OK;
   }
   hipError_t e = order_fill(n, s, st);
@@ -1649,6 +1771,27 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   delete n;
 }
 
+int dora_node_sync(dora_node* n) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (n->core->device < 0) return DORA_OK;
+  dora::NodeCore* c = n->core.get();
+  // AQL fills: their flags; HIP fills and the node stream: query first (an idle stream costs
+  // no blocking wait), then synchronise what is still running
+  const uint64_t t0 = dora::mono_ns();
+  for (auto& x : c->aql_pending)
+    while (x.first->load(std::memory_order_acquire) < x.second) {
+      if (dora::mono_ns() - t0 > 10000000000ull)
+        return dora::fail(DORA_ERR_TIMEOUT, "a fill did not complete within 10 s");
+      __builtin_ia32_pause();
+    }
+  c->aql_pending.clear();
+  std::vector<hipStream_t> ss = c->fill_streams;
+  ss.push_back(c->stream);
+  for (hipStream_t s : ss)
+    if (hipStreamQuery(s) != hipSuccess) DORA_HIP(hipStreamSynchronize(s));
+  return DORA_OK;
+}
+
 dora_stream_t dora_node_stream(dora_node* n) {
   if (!n) return nullptr;
   n->core->fence_fills();  // work the caller queues next runs after every fill so far
@@ -1874,6 +2017,18 @@ int dora_node_pack_stats(dora_node* n, uint64_t* count, double* total_ms, uint64
   return DORA_OK;
 }
 
+int dora_node_dataflow_counters(dora_node* n, const char* node_id, uint64_t* slots_created,
+                                uint64_t* ipc_opens, uint64_t* dropped_inputs) {
+  if (!n || !node_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  const int i = n->core->region->node_index(node_id);
+  if (i < 0) return dora::fail(DORA_ERR_NOT_FOUND, "node `%s` is not part of the dataflow", node_id);
+  const dora::NodeEntry& e = n->core->region->hdr()->nodes[i];
+  if (slots_created) *slots_created = e.slots_created.load(std::memory_order_relaxed);
+  if (ipc_opens) *ipc_opens = e.ipc_opens.load(std::memory_order_relaxed);
+  if (dropped_inputs) *dropped_inputs = e.dropped_inputs.load(std::memory_order_relaxed);
+  return DORA_OK;
+}
+
 int dora_node_fill_paths(dora_node* n, uint64_t* aql_packs, uint64_t* hip_packs) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (aql_packs) *aql_packs = n->aql_packs;
@@ -1904,10 +2059,38 @@ int dora_node_region_begin(dora_node* n) {
   return DORA_OK;
 }
 
+namespace dora {
+namespace {
+// Record the region's stop events: one after the last pack queued on each fill stream and on
+// the node stream.  No wait.
+int region_record_stops(dora_node* n) {
+  std::vector<hipStream_t> ss = n->core->fill_streams;
+  ss.push_back(n->core->stream);
+  while (n->region_stop.size() < ss.size()) {  // fill streams are created lazily
+    hipEvent_t e = nullptr;
+    DORA_HIP(hipEventCreate(&e));
+    n->region_stop.push_back(e);
+  }
+  for (size_t i = 0; i < ss.size(); ++i) DORA_HIP(hipEventRecord(n->region_stop[i], ss[i]));
+  n->region_marked = true;
+  return DORA_OK;
+}
+}  // namespace
+}  // namespace dora
+
+int dora_node_region_mark(dora_node* n) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (!n->region_armed) return dora::fail(DORA_ERR_INVALID, "no region begun");
+  if (!n->region_started || n->region_aql) return DORA_OK;  // AQL packs carry their own stamps
+  return dora::region_record_stops(n);
+}
+
 int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_t* bytes) {
   if (!n || !span_ms) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!n->region_armed) return dora::fail(DORA_ERR_INVALID, "no region begun");
   n->region_armed = false;
+  const bool marked = n->region_marked;
+  n->region_marked = false;
   *span_ms = 0;
   if (packs) *packs = n->region_packs;
   if (bytes) *bytes = n->region_bytes;
@@ -1926,17 +2109,15 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
     }
   }
   if (!n->region_started) return DORA_OK;
-  // stop = the end of the last pack on each fill stream (and the node stream)
-  std::vector<hipStream_t> ss = n->core->fill_streams;
-  ss.push_back(n->core->stream);
-  while (n->region_stop.size() < ss.size()) {  // fill streams are created lazily
-    hipEvent_t e = nullptr;
-    DORA_HIP(hipEventCreate(&e));
-    n->region_stop.push_back(e);
+  // stop = the end of the last pack on each fill stream (and the node stream), recorded by
+  // dora_node_region_mark right after the last send, or now
+  if (!marked) {
+    int rc = dora::region_record_stops(n);
+    if (rc != DORA_OK) return rc;
+    n->region_marked = false;
   }
-  for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i)
-    DORA_HIP(hipEventRecord(n->region_stop[i], ss[i]));
-  for (size_t i = 0; i < ss.size() && i < n->region_stop.size(); ++i) {
+  const size_t ns = n->core->fill_streams.size() + 1;
+  for (size_t i = 0; i < ns && i < n->region_stop.size(); ++i) {
     DORA_HIP(hipEventSynchronize(n->region_stop[i]));
     float ms = 0;
     DORA_HIP(hipEventElapsedTime(&ms, n->region_start, n->region_stop[i]));

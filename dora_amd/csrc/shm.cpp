@@ -2,6 +2,8 @@
 #include "common.h"
 #include "shm.h"
 
+#include <cstddef>
+
 #include <fcntl.h>
 #include <linux/futex.h>
 #include <sched.h>
@@ -163,12 +165,16 @@ void Region::unlink() {
   }
 }
 
+size_t region_header_bytes(size_t n) {
+  return offsetof(RegionHdr, nodes) + n * sizeof(NodeEntry);
+}
+
 Region* Region::create(const std::string& name, const std::vector<std::string>& node_ids,
                        uint64_t ring_cap, const std::string& dataflow_id) {
   if (node_ids.size() > kMaxNodes) throw std::invalid_argument("too many nodes");
   if (ring_cap < 4096 || (ring_cap & (ring_cap - 1)))
     throw std::invalid_argument("ring capacity must be a power of two >= 4096");
-  const uint64_t hdr = round_up(sizeof(RegionHdr), kPage);
+  const uint64_t hdr = round_up(region_header_bytes(node_ids.size()), kPage);
   const uint64_t total = hdr + 3 * ring_cap * node_ids.size();
   int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
   if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
@@ -189,7 +195,7 @@ Region* Region::create(const std::string& name, const std::vector<std::string>& 
   r->name_ = name;
   r->owner_ = true;
   RegionHdr* h = r->hdr_;
-  std::memset(static_cast<void*>(h), 0, sizeof(RegionHdr));
+  std::memset(static_cast<void*>(h), 0, region_header_bytes(node_ids.size()));
   h->version = kRegionVersion;
   h->n_nodes = static_cast<uint32_t>(node_ids.size());
   h->numa_hint.store(-1);
@@ -207,6 +213,9 @@ Region* Region::create(const std::string& name, const std::vector<std::string>& 
     new (&n.pid) std::atomic<int32_t>(0);
     new (&n.state) std::atomic<uint32_t>(0);
     new (&n.device) std::atomic<int32_t>(-2);
+    new (&n.slots_created) std::atomic<uint64_t>(0);
+    new (&n.ipc_opens) std::atomic<uint64_t>(0);
+    new (&n.dropped_inputs) std::atomic<uint64_t>(0);
     for (auto& f : n.fill) new (&f.epoch) std::atomic<uint64_t>(0);
     init_ring(n.requests, off, ring_cap);
     off += ring_cap;
@@ -236,7 +245,9 @@ Region* Region::attach(const std::string& name) {
   r->hdr_ = static_cast<RegionHdr*>(p);
   r->size_ = static_cast<size_t>(st.st_size);
   r->name_ = name;
-  if (r->hdr_->magic != kRegionMagic || r->hdr_->version != kRegionVersion) {
+  if (r->size_ < offsetof(RegionHdr, nodes) || r->hdr_->magic != kRegionMagic ||
+      r->hdr_->version != kRegionVersion || r->hdr_->n_nodes > kMaxNodes ||
+      region_header_bytes(r->hdr_->n_nodes) > r->size_) {
     delete r;
     throw std::runtime_error("shm region " + name + " is not a dora-gpu dataflow region");
   }

@@ -20,8 +20,10 @@
 namespace dora {
 
 constexpr uint64_t kRegionMagic = 0x444f5241474d5358ull;  // "DORAGMSX"
-constexpr uint32_t kRegionVersion = 3;
-constexpr uint32_t kMaxNodes = 64;
+constexpr uint32_t kRegionVersion = 4;
+// Upper bound on the nodes of one dataflow.  The region holds only the `n_nodes` entries in use
+// (region_header_bytes), so the bound costs nothing.
+constexpr uint32_t kMaxNodes = 4096;
 constexpr size_t kIdLen = 64;
 
 struct RingHdr {
@@ -51,6 +53,10 @@ struct NodeEntry {
   std::atomic<int32_t> pid;
   std::atomic<uint32_t> state;  // 0 idle, 1 subscribed, 2 done
   std::atomic<int32_t> device;  // GPU ordinal of the running node (-1 host-only, -2 not started)
+  // diagnostics any process of the dataflow may read (bench: set-up work inside a timed region)
+  std::atomic<uint64_t> slots_created;  // device slots this node allocated (hipMalloc + export)
+  std::atomic<uint64_t> ipc_opens;      // producers' slots this node mapped (hipIpcOpenMemHandle)
+  std::atomic<uint64_t> dropped_inputs; // inputs its queue_size policy dropped (drop_oldest)
   RingHdr requests;
   RingHdr events;
   RingHdr drops;
@@ -70,8 +76,11 @@ struct RegionHdr {
   // first CPU of the L3 cache domain the dataflow's processes share (-1: none chosen yet)
   std::atomic<int32_t> l3_cpu;
   char dataflow_id[kIdLen];
-  NodeEntry nodes[kMaxNodes];
+  NodeEntry nodes[kMaxNodes];  // only the first n_nodes exist in the mapping
 };
+
+// Bytes of the header of a region with `n` nodes (the node entries in use, nothing more).
+size_t region_header_bytes(size_t n);
 
 // A mapped region (creator or attacher).
 class Region {

@@ -4,6 +4,9 @@
 // `t_start` parameter, the latency including allocation + pack.  With `verify` it checksums the
 // received device sample (csum64 kernel) against the sender's `csum` parameter.  Inputs with an
 // `ack` parameter are acknowledged on the `ack` output (used by the bench to close a timed burst).
+// With `verify_late` the input is held (its token not returned) and checksummed right after the
+// next ack has gone out: the bench marks the last messages of its timed region so, and their
+// bytes are verified without putting a checksum kernel inside the timed region.
 // At the end of the stream it writes one JSON document with per-(input, size) statistics.
 //   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE, DORA_BENCH_RESULT (path)
 #include <algorithm>
@@ -68,6 +71,24 @@ int main() {
   Series* last = nullptr;
   size_t last_len = 0;
   std::string last_id;
+  struct Held {
+    dora_event* ev;
+    const void* p;
+    size_t len;
+    uint64_t csum;
+    Series* s;
+  };
+  std::vector<Held> held;  // verify_late inputs, checksummed after the next ack
+  auto verify = [&](const void* p, size_t len, uint64_t want, Series& s) {
+    uint64_t c = 0;
+    if (dora_gpu_csum64(p, len, csum_dev, st) == 0 &&
+        dora_gpu_memcpy_async(&c, csum_dev, 8, st) == 0 && dora_gpu_stream_sync(st) == 0) {
+      ++s.verified;
+      if (c != want) ++s.mismatches;
+    } else {
+      ++errors;
+    }
+  };
   // busy = wall - idle between the first and the last input (diagnostics)
   uint64_t w_first = 0, w_last = 0, idle_first = 0, idle_last = 0, fill_first = 0, fill_last = 0;
   for (;;) {
@@ -120,21 +141,18 @@ int main() {
       s.last_ns = t;
       ++s.n;
       s.bytes += len;
-      if (params.count("csum") && params.count("verify") && dora_event_is_device(ev)) {
-        uint64_t c = 0;
-        if (dora_gpu_csum64(p, len, csum_dev, st) == 0 &&
-            dora_gpu_memcpy_async(&c, csum_dev, 8, st) == 0 && dora_gpu_stream_sync(st) == 0) {
-          ++s.verified;
-          if (c != static_cast<uint64_t>(params["csum"].i)) ++s.mismatches;
-        } else {
-          ++errors;
-        }
-      }
+      const bool dev = dora_event_is_device(ev);
+      if (params.count("csum") && params.count("verify") && dev)
+        verify(p, len, static_cast<uint64_t>(params["csum"].i), s);
       const bool ack = params.count("ack") != 0;
       const int64_t seq = params.count("seq") ? params["seq"].i : -1;
-      const uint64_t tf0 = mono();
-      dora_event_free(ev);  // zero-copy consumer done: token goes back to the sender
-      t_free += mono() - tf0;
+      if (params.count("csum") && params.count("verify_late") && dev) {
+        held.push_back({ev, p, len, static_cast<uint64_t>(params["csum"].i), &s});
+      } else {
+        const uint64_t tf0 = mono();
+        dora_event_free(ev);  // zero-copy consumer done: token goes back to the sender
+        t_free += mono() - tf0;
+      }
       ++n_inputs;
       if (ack) {
         std::map<std::string, Param> ap;
@@ -145,6 +163,11 @@ int main() {
           std::fprintf(stderr, "sink: ack failed: %s\n", dora_gpu_last_error());
           ++errors;
         }
+        for (Held& h : held) {
+          verify(h.p, h.len, h.csum, *h.s);
+          dora_event_free(h.ev);
+        }
+        held.clear();
       }
       continue;
     }
@@ -156,6 +179,11 @@ int main() {
     dora_event_free(ev);
     if (end) break;
   }
+  for (Held& h : held) {  // no ack followed them
+    verify(h.p, h.len, h.csum, *h.s);
+    dora_event_free(h.ev);
+  }
+  held.clear();
   uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
   dora_node_stats(node, &slots, &hits, &inflight, &dropped);
   uint64_t pulls = 0, pull_bytes = 0, bgroups = 0, brecv = 0, brecv_bytes = 0;

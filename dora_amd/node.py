@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes
 import os
 import struct
+import time
 from ctypes import byref, c_double, c_size_t, c_uint8, c_uint64, c_void_p
 from typing import Optional
 
@@ -224,6 +225,32 @@ class Node:
         out["_event"] = ev
         return out
 
+    def wait_input(self, input_id: str, key: str, value, timeout: float = 60.0) -> dict:
+        """Wait for an input event on `input_id` whose parameters have `key == value` and return
+        its parameters; other events are skipped.  A control-message fast path: only the id and
+        the parameters are decoded (no data mapping, no Arrow value), so the wait costs about one
+        ring hop, not a Python event construction."""
+        lib, h = self._lib, c_void_p()
+        p, n = ctypes.POINTER(c_uint8)(), c_size_t()
+        want = input_id.encode()
+        deadline = time.monotonic() + timeout
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise TimeoutError(f"no `{input_id}` input with {key}={value!r}")
+            rc = lib.dora_node_next_event(self.handle, int(left * 1e6), byref(h))
+            if rc == -6:
+                continue
+            _lib.check(rc)
+            try:
+                if lib.dora_event_type(h) == 1 and lib.dora_event_id(h) == want:
+                    call("dora_event_parameters", h, byref(p), byref(n))
+                    meta = decode_parameters(ctypes.string_at(p, n.value) if n.value else b"")
+                    if meta.get(key) == value:
+                        return meta
+            finally:
+                lib.dora_event_free(h)
+
     def __iter__(self):
         while True:
             ev = self.next()
@@ -251,6 +278,14 @@ class Node:
     def set_profiling(self, enable: bool = True):
         call("dora_node_set_profiling", self.handle, int(enable))
 
+    def dataflow_counters(self, node_id: str) -> dict:
+        """Slots created and IPC mappings opened by any node of the dataflow
+        (dora_node_dataflow_counters)."""
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        call("dora_node_dataflow_counters", self.handle, node_id.encode(), byref(a), byref(b),
+             byref(c))
+        return {"slots_created": a.value, "ipc_opens": b.value, "dropped_inputs": c.value}
+
     def fill_paths(self) -> dict:
         """Fills by dispatch path: raw AQL packets vs hipLaunchKernel (dora_node_fill_paths)."""
         a, h = c_uint64(), c_uint64()
@@ -271,6 +306,14 @@ class Node:
     def region_begin(self):
         """Start a device-timed run of sends (dora_node_region_begin)."""
         call("dora_node_region_begin", self.handle)
+
+    def sync(self):
+        """Wait for every fill of this node and its node stream (dora_node_sync)."""
+        call("dora_node_sync", self.handle)
+
+    def region_mark(self):
+        """Record the region's stop events after the last send, without waiting on them."""
+        call("dora_node_region_mark", self.handle)
 
     def region_end(self) -> dict:
         """Device span of the sends since region_begin: first pack start -> last pack end."""

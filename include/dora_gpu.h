@@ -306,6 +306,13 @@ int dora_node_forward_stats(dora_node* node, uint64_t* in_place, uint64_t* held)
 
 int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs);
+/* Counters of any node of this node's dataflow (new; diagnostics, read through the shared
+ * control region): device slots it created, producers' slots it mapped with
+ * hipIpcOpenMemHandle, and inputs its queue_size policy dropped.  A steady edge creates and maps
+ * nothing: a benchmark reads them around a timed region to show it paid no set-up cost inside
+ * and that every message it counts was delivered. */
+int dora_node_dataflow_counters(dora_node* node, const char* node_id, uint64_t* slots_created,
+                                uint64_t* ipc_opens, uint64_t* dropped_inputs);
 /* Fills (packs of sends) by dispatch path: raw AQL packets on the process's HSA queue (device
  * sources below DORA_GPU_AQL_MAX_BYTES, default 32 MiB, <= 8 segments) or hipLaunchKernel on
  * the node's fill streams (larger, host sources, compacting transforms, relays). */
@@ -342,6 +349,12 @@ int dora_node_pack_intervals(dora_node* node, double* out_ms, size_t cap, size_t
  * stream (HIP events recorded by region_end, which waits for them); packs and sample bytes
  * launched in between. */
 int dora_node_region_begin(dora_node* node);
+/* Wait until every fill this node launched (AQL packets, fill streams) and the work on its node
+ * stream have completed (new; the node-scoped counterpart of a device synchronise). */
+int dora_node_sync(dora_node* node);
+/* Record the region's stop events now (after the last send), without waiting; region_end then
+ * waits for them.  Lets a caller close its clock before it waits on the device. */
+int dora_node_region_mark(dora_node* node);
 int dora_node_region_end(dora_node* node, double* span_ms, uint64_t* packs, uint64_t* bytes);
 /* Mean host time (µs) per send phase since profiling was (re)enabled: [0] allocate incl.
  * backpressure, [1] pack launch, [2] fill event record / stream sync, [3] descriptor send. */

@@ -403,23 +403,153 @@ def test_cross_gpu_bench_runs_on_one_gpu(launcher):
     assert rc["pulls"] > 0
 
 
+def _distinct_sources(n, size):
+    """n device buffers with distinct splitmix64 payloads and their checksums."""
+    from dora_amd import device
+    from dora_amd.verify import to_i64
+    s = device.Stream()
+    bufs, sums = [], []
+    for k in range(n):
+        b = device.DeviceBuffer(size)
+        device.fill_splitmix(b.ptr, size, 0x5EED0000 + k, s)
+        bufs.append(b)
+    s.sync()
+    for b in bufs:
+        sums.append(to_i64(device.csum64(b.ptr, size, s)))
+    s.close()
+    return bufs, sums
+
+
 def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
-    """queue_size 2 and a burst: dropped inputs still return their drop tokens."""
+    """queue_size 2 (node_communication/mod.rs:320-359): a receiver that drains a burst of 60
+    inputs at once keeps exactly the newest 2, every dropped input's token goes back at once,
+    and the sender's close finds every token returned (no 10-s drop-token wait)."""
+    import threading
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.node import Node
-    res = str(tmp_path / "sink.json")
-    with Dataflow(_bench_desc(res, queue_size=2), launcher=launcher) as df:
+    n_msgs, size = 60, 1 << 20
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["data"]},
+        {"id": "recv", "path": "dynamic", "inputs": {"data": {"source": "node/data",
+                                                               "queue_size": 2}}},
+    ]}
+    bufs, sums = _distinct_sources(n_msgs, size)
+    with Dataflow(desc, launcher=launcher) as df:
+        sent = threading.Event()
+        got, err = [], []
+
+        def receiver():
+            try:
+                r = Node("recv", dataflow=df.shm, device=0)
+                sent.wait(60)
+                s = device.Stream()
+                for ev in r:
+                    if ev["type"] != "INPUT":
+                        continue
+                    c = device.csum64(ev["data_ptr"], ev["data_len"], s)
+                    got.append((ev["metadata"]["seq"], c, r.stats()["dropped_inputs"]))
+                    del ev
+                s.close()
+                r.close()
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        t = threading.Thread(target=receiver)
+        t.start()
         node = Node("node", dataflow=df.shm, device=0)
-        buf = device.DeviceBuffer(1 << 20)
-        for k in range(200):
-            node.send_output_device_bytes("data", buf.ptr, buf.size, {"seq": k})
-        node.close()   # waits for every drop token (<= 10 s each)
+        for k in range(n_msgs):
+            node.send_output_device_bytes("data", bufs[k].ptr, size, {"seq": k})
+        sent.set()
+        t_close = time.time()
+        node_stats = node.stats()
+        node.close()  # returns once every drop token is back
+        close_s = time.time() - t_close
+        t.join(60)
         df.wait(60)
-        buf.free()
+    for b in bufs:
+        b.free()
+    assert not err, err
+    # exactly the newest queue_size inputs survived, bit-exact; the other 58 were dropped
+    assert [g[0] for g in got] == [n_msgs - 2, n_msgs - 1], got
+    from dora_amd.verify import to_i64
+    assert [to_i64(g[1]) for g in got] == sums[-2:]
+    assert got[0][2] == n_msgs - 2
+    assert node_stats["slots_created"] + node_stats["cache_hits"] == n_msgs
+    assert close_s < 5.0, close_s
+
+
+def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
+    """A queue_size 1 receiver that checksums every input it keeps drops most of a fast
+    sender's burst.  Dropped inputs return their tokens before their fills were waited on, so
+    the sender refills recycled slots while earlier packs may still run: every payload is
+    distinct and every delivered one must match its own checksum."""
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    res = str(tmp_path / "sink.json")
+    n_msgs, size, nsrc = 300, 4 << 20, 24
+    bufs, sums = _distinct_sources(nsrc, size)
+    with Dataflow(_bench_desc(res, queue_size=1), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        for k in range(n_msgs):
+            node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size,
+                                          {"seq": k, "csum": sums[k % nsrc], "verify": True})
+        stats = node.stats()
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    for b in bufs:
+        b.free()
+    assert codes["sink"] == 0, log
     out = json.load(open(res))
     assert out["errors"] == 0
-    assert sum(s["n"] for s in out["series"]) <= 200
+    verified = sum(s["verified"] for s in out["series"])
+    assert verified == sum(s["n"] for s in out["series"]) and verified > 0
+    assert sum(s["mismatches"] for s in out["series"]) == 0
+    assert verified + out["dropped_inputs"] == n_msgs, out
+    assert stats["slots_created"] + stats["cache_hits"] == n_msgs
+
+
+def test_output_without_receivers_recycles_safely(launcher, tmp_path):
+    """Sends on an output nobody subscribes to get their drop token back at once (the daemon's
+    check_drop_token with no pending receiver), long before their packs finish.  The recycled
+    slots then carry the next sends, here interleaved with verified sends on a connected
+    output: every verified payload is bit-exact and no slot is created per send."""
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    res = str(tmp_path / "sink.json")
+    size, nsrc = 4 << 20, 16
+    bufs, sums = _distinct_sources(nsrc, size)
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["void", "data"]},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"data": {"source": "node/data", "queue_size": 1000}},
+         "env": {"DORA_BENCH_RESULT": res}},
+    ]}
+    with Dataflow(desc, launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        n_data = 0
+        for k in range(400):
+            if k % 8 == 7:
+                node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size,
+                                              {"seq": k, "csum": sums[k % nsrc], "verify": True})
+                n_data += 1
+            else:
+                node.send_output_device_bytes("void", bufs[k % nsrc].ptr, size, {"seq": k})
+        stats = node.stats()
+        t_close = time.time()
+        node.close()
+        close_s = time.time() - t_close
+        codes = df.wait(60)
+        log = df.log("sink")
+    for b in bufs:
+        b.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(s["verified"] for s in out["series"]) == n_data
+    assert sum(s["mismatches"] for s in out["series"]) == 0
+    assert stats["slots_created"] <= 40, stats
+    assert close_s < 5.0, close_s
 
 
 def _roundtrip_through_node(launcher, names, env=None):
