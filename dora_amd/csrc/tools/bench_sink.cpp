@@ -125,6 +125,18 @@ int main() {
       dora_event_parameters(ev, &pp, &pl);
       std::map<std::string, Param> params;
       if (pl) params = decode_params(pp, pl);
+      if (params.count("ack")) {
+        // acknowledge first: the sender's clock waits on this (the data is complete and
+        // readable here; the bookkeeping below does not delay the ack)
+        std::map<std::string, Param> ap;
+        ap["seq"].i = params.count("seq") ? params["seq"].i : -1;
+        auto enc = encode_params(ap);
+        if (dora_node_send_output_bytes(node, "ack", nullptr, 0, ARROW_DEVICE_ROCM, enc.data(),
+                                        enc.size()) != 0) {
+          std::fprintf(stderr, "sink: ack failed: %s\n", dora_gpu_last_error());
+          ++errors;
+        }
+      }
       // consecutive inputs mostly share (input, size): skip the keyed lookup then
       const char* id = dora_event_id(ev);
       if (!last || len != last_len || last_id != id) {
@@ -145,7 +157,6 @@ int main() {
       if (params.count("csum") && params.count("verify") && dev)
         verify(p, len, static_cast<uint64_t>(params["csum"].i), s);
       const bool ack = params.count("ack") != 0;
-      const int64_t seq = params.count("seq") ? params["seq"].i : -1;
       if (params.count("csum") && params.count("verify_late") && dev) {
         held.push_back({ev, p, len, static_cast<uint64_t>(params["csum"].i), &s});
       } else {
@@ -155,14 +166,6 @@ int main() {
       }
       ++n_inputs;
       if (ack) {
-        std::map<std::string, Param> ap;
-        ap["seq"].i = seq;
-        auto enc = encode_params(ap);
-        if (dora_node_send_output_bytes(node, "ack", nullptr, 0, ARROW_DEVICE_ROCM, enc.data(),
-                                        enc.size()) != 0) {
-          std::fprintf(stderr, "sink: ack failed: %s\n", dora_gpu_last_error());
-          ++errors;
-        }
         for (Held& h : held) {
           verify(h.p, h.len, h.csum, *h.s);
           dora_event_free(h.ev);
