@@ -281,6 +281,29 @@ def run_native_ladder(launcher, gpu, n=1000, timeout=120.0):
     return out
 
 
+def edge_rates(sinks):
+    """Per receiving edge: payload GB/s of its back-to-back (throughput) series, from the sink's
+    own first/last receipt stamps, and the bytes it pulled over xGMI or received by broadcast."""
+    out = []
+    for sname, r in sorted(sinks.items()):
+        if not r:
+            continue
+        tp = [s for s in r.get("series", []) if s["input"] == "throughput" and s["n"] > 1]
+        gbps = None
+        if tp:
+            s = max(tp, key=lambda x: x["n"])
+            span_ns = s["last_ns"] - s["first_ns"]
+            # n receipts span n - 1 message intervals
+            gbps = round((s["n"] - 1) * s["size"] / span_ns, 3) if span_ns > 0 else None
+        moved = r.get("pull_bytes", 0) + (r.get("bcast_received", 0) and
+                                          sum(x["n"] * x["size"] for x in r.get("series", [])))
+        out.append({"sink": sname, "GBps": gbps, "pulls": r.get("pulls", 0),
+                    "pull_bytes": r.get("pull_bytes", 0),
+                    "bcast_received": r.get("bcast_received", 0),
+                    "xgmi_frac": round(gbps / XGMI_LINK_GBPS, 4) if gbps and moved else None})
+    return out
+
+
 def summarize_cross(name, src, sinks, codes, logs):
     lat, verified, mismatches, dropped, errors = {}, 0, 0, 0, 0
     for sname, r in sinks.items():
@@ -297,22 +320,32 @@ def summarize_cross(name, src, sinks, codes, logs):
                     {"sink": sname, "p50_us": s["p50_us"], "p99_us": s["p99_us"],
                      "e2e_p50_us": s["full_p50_us"], "e2e_p99_us": s["full_p99_us"], "n": s["n"]})
     per_rx = src.get("tp_per_receiver_GBps", 0.0)
+    pulls = sum((r or {}).get("pulls", 0) for r in sinks.values())
+    pull_bytes = sum((r or {}).get("pull_bytes", 0) for r in sinks.values())
+    bcast_rx = sum((r or {}).get("bcast_received", 0) for r in sinks.values())
+    # An xGMI roofline only when bytes crossed a link: with every stage on one GPU (a one-GPU
+    # rehearsal without forced pulls) nothing did, and a fraction of the link peak means nothing.
+    crossed = pulls > 0 or bcast_rx > 0
+    roof = ({"bound": "xgmi", "achieved": per_rx, "peak": XGMI_LINK_GBPS, "unit": "GB/s",
+             "frac": round(per_rx / XGMI_LINK_GBPS, 4)} if crossed else None)
     res = {"ok": bool(src.get("ok")) and errors == 0 and mismatches == 0,
            "receivers": src.get("receivers"), "msg_bytes": src.get("tp_size"),
            "tp_msgs": src.get("tp_n"), "delivered_GBps": src.get("tp_delivered_GBps"),
            "per_link_GBps": per_rx,
-           "roofline": {"bound": "xgmi", "achieved": per_rx, "peak": XGMI_LINK_GBPS,
-                        "unit": "GB/s", "frac": round(per_rx / XGMI_LINK_GBPS, 4)},
+           "roofline": roof,
+           "edges": edge_rates(sinks),
            "latency_us": lat, "parity": {"verified_msgs": verified, "mismatches": mismatches},
            "dropped_inputs": dropped, "errors": errors, "exit_codes": codes,
            "source_send_phase_us": src.get("send_phase_us"),
            # transfer path actually taken: pulls per receiver, or RCCL broadcast group traffic
-           "pulls": sum((r or {}).get("pulls", 0) for r in sinks.values()),
+           "pulls": pulls, "pull_bytes": pull_bytes,
            "bcast": {"groups": src.get("bcast_groups", 0), "sent": src.get("bcast_sent", 0),
-                     "received": sum((r or {}).get("bcast_received", 0) for r in sinks.values()),
+                     "received": bcast_rx,
                      "error": src.get("bcast_error") or next(
                          (r.get("bcast_error") for r in sinks.values()
                           if r and r.get("bcast_error")), "")}}
+    if not crossed:
+        res["note"] = "no byte crossed a GPU link (every stage on one GPU): roofline null"
     if logs:
         res["logs"] = logs
     return res

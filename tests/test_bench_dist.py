@@ -73,14 +73,35 @@ def test_summarize_cross():
     import bench
     src = {"ok": True, "receivers": 2, "tp_size": 100, "tp_n": 10, "tp_delivered_GBps": 200.0,
            "tp_per_receiver_GBps": 100.0, "send_phase_us": {}}
-    sink = {"errors": 0, "dropped_inputs": 0, "series": [
+    sink = {"errors": 0, "dropped_inputs": 0, "pulls": 13, "pull_bytes": 1300, "series": [
         {"input": "latency", "size": 100, "n": 5, "p50_us": 10.0, "p99_us": 20.0,
-         "full_p50_us": 12.0, "full_p99_us": 22.0, "verified": 2, "mismatches": 0},
-        {"input": "throughput", "size": 0, "n": 3, "p50_us": 1.0, "p99_us": 1.0,
-         "full_p50_us": 0, "full_p99_us": 0, "verified": 0, "mismatches": 0}]}
+         "full_p50_us": 12.0, "full_p99_us": 22.0, "verified": 2, "mismatches": 0,
+         "first_ns": 0, "last_ns": 500},
+        {"input": "throughput", "size": 100, "n": 11, "p50_us": 1.0, "p99_us": 1.0,
+         "full_p50_us": 0, "full_p99_us": 0, "verified": 0, "mismatches": 0,
+         "first_ns": 1000, "last_ns": 2000}]}
     r = bench.summarize_cross("c4", src, {"sink1": sink, "sink2": sink}, {"source": 0}, {})
     assert r["ok"] and r["parity"]["verified_msgs"] == 4
     assert r["roofline"]["frac"] == round(100.0 / bench.XGMI_LINK_GBPS, 4)
     assert len(r["latency_us"]["100"]) == 2
+    # per edge: 10 intervals of 100 B in 1000 ns = 1 GB/s, over a link (pulls > 0)
+    assert [e["GBps"] for e in r["edges"]] == [1.0, 1.0]
+    assert r["edges"][0]["xgmi_frac"] == round(1.0 / bench.XGMI_LINK_GBPS, 4)
+    assert r["pull_bytes"] == 2600
     bad = dict(sink, series=[dict(sink["series"][0], mismatches=1)])
     assert not bench.summarize_cross("c4", src, {"s": bad}, {}, {})["ok"]
+
+
+def test_summarize_cross_without_link_traffic_has_no_roofline():
+    """A run whose stages all sat on one GPU (no pull, no broadcast) moved nothing over xGMI:
+    its roofline is null and the edges carry no link fraction."""
+    import bench
+    src = {"ok": True, "receivers": 1, "tp_size": 100, "tp_n": 10, "tp_delivered_GBps": 900.0,
+           "tp_per_receiver_GBps": 900.0, "send_phase_us": {}}
+    sink = {"errors": 0, "dropped_inputs": 0, "pulls": 0, "pull_bytes": 0, "series": [
+        {"input": "throughput", "size": 100, "n": 11, "p50_us": 1.0, "p99_us": 1.0,
+         "full_p50_us": 0, "full_p99_us": 0, "verified": 1, "mismatches": 0,
+         "first_ns": 1000, "last_ns": 2000}]}
+    r = bench.summarize_cross("c4", src, {"sink1": sink}, {"source": 0}, {})
+    assert r["roofline"] is None and "no byte crossed" in r["note"]
+    assert r["edges"][0]["xgmi_frac"] is None
