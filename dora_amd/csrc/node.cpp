@@ -597,6 +597,18 @@ struct dora_node {
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
   bool compact = false;                     // send_output uses compacting plans
+  // Plans of recent device-array sends by plan_key (a sender re-sending the same buffers, e.g. a
+  // ring of preallocated frames, plans each once): the plan and its serialized type info
+  struct CachedPlan {
+    std::vector<uint64_t> key;
+    dora_plan* plan = nullptr;
+    std::vector<uint8_t> ti;
+    uint64_t last_use = 0;
+  };
+  std::vector<CachedPlan> plan_cache;
+  std::unordered_map<uint64_t, size_t> plan_index;  // hash of a key -> its plan_cache entry
+  std::vector<uint64_t> plan_key_buf;
+  uint64_t plan_clock = 0, plan_hits = 0;
   // RCCL broadcast groups of this node's fan-out outputs (rank 0 of each), DORA_GPU_FANOUT=rccl
   std::map<std::string, dora::BcastComm*> bcast_out;
   uint64_t bcast_seq = 0;
@@ -1534,7 +1546,7 @@ void form_bcast_groups(dora_node* n) {
 }
 
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
-                  size_t params_len) {
+                  size_t params_len, const std::vector<uint8_t>* ti_pre = nullptr) {
   dora_sample* s = nullptr;
   const uint64_t t0 = mono_ns();
   int rc = alloc_sample(n, plan->size, &s, plan->fill_size());
@@ -1577,8 +1589,12 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     t2 = t3 = mono_ns();
   }
   std::vector<uint8_t>& ti = n->ti_buf;
-  ti.clear();
-  serialize_type_info(plan->root, ti);
+  if (ti_pre) {
+    ti.assign(ti_pre->begin(), ti_pre->end());
+  } else {
+    ti.clear();
+    serialize_type_info(plan->root, ti);
+  }
   DropToken tok{};
   const bool traced = trace_enabled() && s->slot;
   rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
@@ -1760,6 +1776,9 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   n->bcast_out.clear();
   for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
   for (auto* s : n->cache) dora::free_slot(n, s);
+  for (auto& e : n->plan_cache) delete e.plan;
+  n->plan_cache.clear();
+  n->plan_index.clear();
   dora::harvest_all(n);
   for (auto& p : n->timing) {
     (void)hipEventDestroy(p.start);
@@ -1834,13 +1853,57 @@ int dora_node_send_output(dora_node* n, const char* output_id, const struct Arro
                           const uint8_t* params, size_t params_len) {
   if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
+  const bool device = device_type == ARROW_DEVICE_ROCM && n->core->device >= 0;
+  const bool cacheable = device && !n->compact && array && schema;
+  uint64_t h = 0;
+  bool keyed = false;
+  if (cacheable && dora::plan_key(array, schema, n->plan_key_buf)) {
+    keyed = true;
+    h = 0xcbf29ce484222325ull;
+    for (uint64_t w : n->plan_key_buf) h = (h ^ w) * 0x100000001b3ull;
+    auto it = n->plan_index.find(h);
+    if (it != n->plan_index.end()) {
+      auto& e = n->plan_cache[it->second];
+      if (e.key == n->plan_key_buf) {
+        e.last_use = ++n->plan_clock;
+        ++n->plan_hits;
+        return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti);
+      }
+      keyed = false;  // a hash collision: plan this one afresh, uncached
+    }
+  }
   dora_plan* plan = nullptr;
   int rc = (n->compact && device_type == ARROW_DEVICE_ROCM)
                ? dora::build_plan_compact(array, schema, device_type, &plan)
                : dora::build_plan(array, schema, device_type, &plan,
-                                  device_type == ARROW_DEVICE_ROCM && n->core->device >= 0 &&
-                                      dora::validity_in_sample());
+                                  device && dora::validity_in_sample());
   if (rc != DORA_OK) return rc;
+  if (keyed && !plan->read_device) {
+    // keep it: a later send of the same buffers reuses plan and type info.  64 entries cover a
+    // sender rotating over a few dozen preallocated arrays (C3 bench: 24)
+    constexpr size_t kPlanCache = 64;
+    size_t slot = n->plan_cache.size();
+    if (slot >= kPlanCache) {
+      slot = 0;
+      for (size_t k = 1; k < n->plan_cache.size(); ++k)
+        if (n->plan_cache[k].last_use < n->plan_cache[slot].last_use) slot = k;
+      auto& old = n->plan_cache[slot];
+      uint64_t oh = 0xcbf29ce484222325ull;
+      for (uint64_t w : old.key) oh = (oh ^ w) * 0x100000001b3ull;
+      n->plan_index.erase(oh);
+      delete old.plan;
+      old = dora_node::CachedPlan();
+    } else {
+      n->plan_cache.emplace_back();
+    }
+    auto& e = n->plan_cache[slot];
+    e.key = n->plan_key_buf;
+    e.plan = plan;
+    dora::serialize_type_info(plan->root, e.ti);
+    e.last_use = ++n->plan_clock;
+    n->plan_index[h] = slot;
+    return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti);
+  }
   rc = dora::pack_and_send(n, output_id, plan, params, params_len);
   delete plan;
   return rc;
@@ -1855,7 +1918,6 @@ int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void*
   dora_plan plan;
   plan.dev = device_type;
   plan.size = len;
-  plan.root.sig = "C";
   {
     ArrowSchema u8{};
     u8.format = "C";
@@ -2026,6 +2088,13 @@ int dora_node_dataflow_counters(dora_node* n, const char* node_id, uint64_t* slo
   if (slots_created) *slots_created = e.slots_created.load(std::memory_order_relaxed);
   if (ipc_opens) *ipc_opens = e.ipc_opens.load(std::memory_order_relaxed);
   if (dropped_inputs) *dropped_inputs = e.dropped_inputs.load(std::memory_order_relaxed);
+  return DORA_OK;
+}
+
+int dora_node_plan_cache_stats(dora_node* n, uint64_t* hits, uint64_t* entries) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (hits) *hits = n->plan_hits;
+  if (entries) *entries = n->plan_cache.size();
   return DORA_OK;
 }
 

@@ -22,64 +22,68 @@ namespace dora {
 
 namespace {
 
-bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+bool starts_with(const char* s, const char* p) { return std::strncmp(s, p, std::strlen(p)) == 0; }
+bool eq(const char* a, const char* b) { return std::strcmp(a, b) == 0; }
 
 }  // namespace
 
 // arrow-data 53.2.0 `layout()`; throws std::domain_error for types outside the parity set.
-Layout layout_of(const std::string& f) {
+// Matched on the C format string without building a std::string (a plan walks it per node).
+Layout layout_of(const char* f) {
   Layout l;
   auto fixed = [&](uint32_t w, uint32_t a) { l.specs.push_back({BufSpec::Fixed, w, a}); };
-  if (f == "n") {
+  const bool one = f[0] && !f[1];  // single-character primitive formats
+  if (one && f[0] == 'n') {
     l.can_null = false;
-  } else if (f == "b") {
+  } else if (one && f[0] == 'b') {
     l.specs.push_back({BufSpec::Bitmap, 0, 1});
-  } else if (f == "c" || f == "C") {
+  } else if (one && (f[0] == 'c' || f[0] == 'C')) {
     fixed(1, 1);
-  } else if (f == "s" || f == "S" || f == "e") {
+  } else if (one && (f[0] == 's' || f[0] == 'S' || f[0] == 'e')) {
     fixed(2, 2);
-  } else if (f == "i" || f == "I" || f == "f" || f == "tdD" || f == "tts" || f == "ttm" ||
-             f == "tiM") {
+  } else if ((one && (f[0] == 'i' || f[0] == 'I' || f[0] == 'f')) || eq(f, "tdD") ||
+             eq(f, "tts") || eq(f, "ttm") || eq(f, "tiM")) {
     fixed(4, 4);
-  } else if (f == "l" || f == "L" || f == "g" || f == "tdm" || f == "ttu" || f == "ttn" ||
-             starts_with(f, "ts") || starts_with(f, "tD")) {
+  } else if ((one && (f[0] == 'l' || f[0] == 'L' || f[0] == 'g')) || eq(f, "tdm") ||
+             eq(f, "ttu") || eq(f, "ttn") || starts_with(f, "ts") || starts_with(f, "tD")) {
     fixed(8, 8);
-  } else if (f == "tiD") {
+  } else if (eq(f, "tiD")) {
     fixed(8, 4);  // IntervalDayTime {i32, i32}
-  } else if (f == "tin") {
+  } else if (eq(f, "tin")) {
     fixed(16, 8);  // IntervalMonthDayNano {i32, i32, i64}
   } else if (starts_with(f, "d:")) {
     // "d:precision,scale[,bitwidth]"; i128 / i256 have align 8 on the pinned Rust 1.76
     int commas = 0;
-    size_t last = 0;
-    for (size_t i = 0; i < f.size(); ++i)
-      if (f[i] == ',') ++commas, last = i;
-    int bw = commas >= 2 ? std::stoi(f.substr(last + 1)) : 128;
-    if (bw != 128 && bw != 256) throw std::invalid_argument("decimal bit width " + f);
+    const char* last = nullptr;
+    for (const char* p = f; *p; ++p)
+      if (*p == ',') ++commas, last = p;
+    const int bw = commas >= 2 ? std::atoi(last + 1) : 128;
+    if (bw != 128 && bw != 256) throw std::invalid_argument(std::string("decimal bit width ") + f);
     fixed(static_cast<uint32_t>(bw / 8), 8);
   } else if (starts_with(f, "w:")) {
-    fixed(static_cast<uint32_t>(std::stoul(f.substr(2))), 1);
-  } else if (f == "z" || f == "u") {
+    fixed(static_cast<uint32_t>(std::strtoul(f + 2, nullptr, 10)), 1);
+  } else if (one && (f[0] == 'z' || f[0] == 'u')) {
     fixed(4, 4);
     l.specs.push_back({BufSpec::Var, 0, 1});
     l.offsets_first = true;
-  } else if (f == "Z" || f == "U") {
+  } else if (one && (f[0] == 'Z' || f[0] == 'U')) {
     fixed(8, 8);
     l.specs.push_back({BufSpec::Var, 0, 1});
     l.offsets_first = true;
-  } else if (f == "+l" || f == "+m") {
+  } else if (eq(f, "+l") || eq(f, "+m")) {
     fixed(4, 4);
     l.offsets_first = true;
-  } else if (f == "+L") {
+  } else if (eq(f, "+L")) {
     fixed(8, 8);
     l.offsets_first = true;
-  } else if (starts_with(f, "+w:") || f == "+s") {
+  } else if (starts_with(f, "+w:") || eq(f, "+s")) {
     // children only
-  } else if (f == "+r") {
+  } else if (eq(f, "+r")) {
     l.can_null = false;
   } else {
     // views (vz/vu: the reference's zip drops variadic buffers), unions, list views
-    throw std::domain_error("arrow format '" + f + "' is outside the supported parity set");
+    throw std::domain_error(std::string("arrow format '") + f +
+                            "' is outside the supported parity set");
   }
   return l;
 }
@@ -250,7 +254,7 @@ uint64_t pad_to(uint64_t x, const BufSpec& sp) {
 void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t& next,
           std::vector<Segment>& segs, TypeInfoNode& ti) {
   if (!a || !s || !s->format) throw std::invalid_argument("null ArrowArray/ArrowSchema node");
-  const std::string fmt = s->format;
+  const char* fmt = s->format;
   const bool is_dict = s->dictionary != nullptr;
   Layout l = layout_of(fmt);  // dictionary: layout(key type) == layout(index format)
   if (is_dict) l.offsets_first = false;
@@ -260,16 +264,15 @@ void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t&
   const uint64_t total = len + off;
   const int64_t begin = l.can_null ? 1 : 0;
   if (a->n_buffers < begin + static_cast<int64_t>(l.specs.size()))
-    throw std::invalid_argument("ArrowArray for '" + fmt + "' has too few buffers");
+    throw std::invalid_argument(std::string("ArrowArray for '") + fmt + "' has too few buffers");
 
-  ti.sig = schema_sig(s);
   serialize_schema(s, true, ti.schema);
   ti.len = len;
   ti.offset = off;
   ti.null_count = 0;
   ti.has_validity = false;
 
-  std::vector<uint64_t> lens;
+  uint64_t lens[3] = {0, 0, 0};
   for (size_t k = 0; k < l.specs.size(); ++k) {
     const BufSpec& sp = l.specs[k];
     const void* p = a->buffers[begin + static_cast<int64_t>(k)];
@@ -299,7 +302,7 @@ void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t&
       const uint64_t bits = sp.kind == BufSpec::Bitmap ? 1 : uint64_t(sp.width) * 8;
       blen = (total * bits + 7) / 8;
     }
-    lens.push_back(blen);
+    lens[k] = blen;
     if (!p && blen != 0)
       throw std::invalid_argument("buffer " + std::to_string(begin + k) + " of '" + fmt +
                                   "' is null but has length " + std::to_string(blen));
@@ -338,11 +341,11 @@ void walk(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, uint64_t&
     walk(a->dictionary, s->dictionary, rd, next, segs, ti.children.back());
   } else {
     if (a->n_children != s->n_children)
-      throw std::invalid_argument("array/schema child count mismatch for '" + fmt + "'");
-    for (int64_t i = 0; i < a->n_children; ++i) {
-      ti.children.emplace_back();
-      walk(a->children[i], s->children[i], rd, next, segs, ti.children.back());
-    }
+      throw std::invalid_argument(std::string("array/schema child count mismatch for '") + fmt +
+                                  "'");
+    ti.children.resize(static_cast<size_t>(a->n_children));
+    for (int64_t i = 0; i < a->n_children; ++i)
+      walk(a->children[i], s->children[i], rd, next, segs, ti.children[static_cast<size_t>(i)]);
   }
 }
 
@@ -373,7 +376,6 @@ void walk_compact(const ArrowArray* a, const ArrowSchema* s, const Reader& rd, u
   const int64_t begin = l.can_null ? 1 : 0;
   if (a->n_buffers < begin + static_cast<int64_t>(l.specs.size()))
     throw std::invalid_argument("ArrowArray for '" + fmt + "' has too few buffers");
-  ti.sig = schema_sig(s);
   serialize_schema(s, true, ti.schema);
   ti.len = len;
   ti.offset = 0;
@@ -532,6 +534,43 @@ int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, Arrow
 
 namespace {
 
+uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < n; ++i) h = (h ^ uint8_t(p[i])) * 0x100000001b3ull;
+  return h ^ n;
+}
+
+bool key_node(const ArrowArray* a, const ArrowSchema* s, std::vector<uint64_t>& o) {
+  if (!a || !s || !s->format || o.size() > 4096) return false;
+  const size_t fl = std::strlen(s->format);
+  o.push_back(reinterpret_cast<uintptr_t>(s));
+  o.push_back(hash_bytes(s->format, fl));
+  o.push_back(s->name ? hash_bytes(s->name, std::strlen(s->name)) : 0);
+  o.push_back(static_cast<uint64_t>(s->flags));
+  o.push_back(s->metadata ? hash_bytes(s->metadata, metadata_len(s->metadata)) : 0);
+  o.push_back(static_cast<uint64_t>(a->length));
+  o.push_back(static_cast<uint64_t>(a->offset));
+  o.push_back(static_cast<uint64_t>(a->null_count));
+  o.push_back(static_cast<uint64_t>(a->n_buffers) | (uint64_t(a->n_children) << 32));
+  o.push_back(static_cast<uint64_t>(s->n_children) | (uint64_t(s->dictionary != nullptr) << 32) |
+              (uint64_t(a->dictionary != nullptr) << 33));
+  for (int64_t k = 0; k < a->n_buffers; ++k) o.push_back(reinterpret_cast<uintptr_t>(a->buffers[k]));
+  if (s->dictionary) return a->dictionary && key_node(a->dictionary, s->dictionary, o);
+  if (a->n_children != s->n_children) return false;
+  for (int64_t i = 0; i < a->n_children; ++i)
+    if (!key_node(a->children[i], s->children[i], o)) return false;
+  return true;
+}
+
+}  // namespace
+
+bool plan_key(const ArrowArray* array, const ArrowSchema* schema, std::vector<uint64_t>& out) {
+  out.clear();
+  return key_node(array, schema, out);
+}
+
+namespace {
+
 // Validity tail of a plan with deferred bitmaps: 64-B aligned after the sample, in walk order.
 void place_validity(TypeInfoNode& t, const std::vector<const void*>& src, size_t& k,
                     uint64_t& next, std::vector<Segment>& segs) {
@@ -566,6 +605,7 @@ int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceTy
       // no device bytes read (e.g. fixed-width / nested arrays with in-sample validity): the
       // collecting walk is the plan; otherwise replay it with the gathered bytes
       done = rd.reqs.empty();
+      p->read_device = !done;
       if (!done) {
         rd.staged = gather_to_host(rd.reqs, rd.total);
         rd.mode = Reader::REPLAY;
@@ -616,7 +656,6 @@ int dora_gpu_plan_bytes(const void* src, size_t len, ArrowDeviceType device_type
   p->dev = device_type;
   p->size = len;
   // ArrowTypeInfo::byte_array(len), libraries/message/src/metadata.rs:74-87
-  p->root.sig = "C";
   {
     ArrowSchema u8{};
     u8.format = "C";

@@ -18,15 +18,27 @@ struct BufSpec {
   uint32_t align;  // FixedWidth alignment (arrow-data layout())
 };
 
+// At most three buffer specs per Arrow layout: a fixed-capacity list (no heap allocation per
+// planned node).
+struct SpecList {
+  BufSpec v[3];
+  size_t n = 0;
+  void push_back(const BufSpec& b) { v[n++] = b; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const BufSpec& operator[](size_t i) const { return v[i]; }
+  const BufSpec* begin() const { return v; }
+  const BufSpec* end() const { return v + n; }
+};
+
 struct Layout {
-  std::vector<BufSpec> specs;
+  SpecList specs;
   bool can_null = true;
   bool offsets_first = false;  // first non-null buffer is an offsets buffer of len+1 entries
 };
 
 // ArrowTypeInfo (libraries/message/src/metadata.rs:51-59) with the data type as a signature.
 struct TypeInfoNode {
-  std::string sig;                  // canonical signature (comparison key)
   std::vector<uint8_t> schema;      // serialized DataType (see serialize_schema)
   uint64_t len = 0;
   uint64_t null_count = 0;
@@ -90,7 +102,14 @@ void serialize_type_info(const TypeInfoNode& t, std::vector<uint8_t>& out);
 void serialize_schema(const ArrowSchema* s, bool top, std::vector<uint8_t>& out);
 std::string schema_sig(const ArrowSchema* s);
 uint64_t metadata_len(const char* meta);
-Layout layout_of(const std::string& format);
+// Everything a plan of (array, schema) depends on when it reads no array bytes, as words: per
+// node in walk order the schema's identity and strings (hashed), flags, and the array's length,
+// offset, null count, buffer addresses and child counts.  Equal keys give equal plans (a node's
+// plan cache, node.cpp).  False when the tree is too large to key.
+bool plan_key(const ArrowArray* array, const ArrowSchema* schema, std::vector<uint64_t>& out);
+
+Layout layout_of(const char* format);
+inline Layout layout_of(const std::string& format) { return layout_of(format.c_str()); }
 int build_plan(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
                dora_plan** out, bool validity_in_sample = false);
 int build_plan_compact(const ArrowArray* array, const ArrowSchema* schema, ArrowDeviceType dev,
@@ -103,6 +122,7 @@ struct dora_plan {
   bool compact = false;  // built by dora_gpu_plan_compact (carries transform segments)
   uint64_t size = 0;      // required_data_size: the reference sample
   uint64_t ext_size = 0;  // bytes to allocate and fill incl. a validity tail (0: == size)
+  bool read_device = false;  // planning read bytes of the array (last offsets, bitmaps)
   std::vector<dora::Segment> segs;
   dora::TypeInfoNode root;
   uint64_t fill_size() const { return ext_size > size ? ext_size : size; }

@@ -286,6 +286,12 @@ class Node:
              byref(c))
         return {"slots_created": a.value, "ipc_opens": b.value, "dropped_inputs": c.value}
 
+    def plan_cache_stats(self) -> dict:
+        """Device-array sends served by the node's plan cache (dora_node_plan_cache_stats)."""
+        a, b = c_uint64(), c_uint64()
+        call("dora_node_plan_cache_stats", self.handle, byref(a), byref(b))
+        return {"hits": a.value, "entries": b.value}
+
     def fill_paths(self) -> dict:
         """Fills by dispatch path: raw AQL packets vs hipLaunchKernel (dora_node_fill_paths)."""
         a, h = c_uint64(), c_uint64()

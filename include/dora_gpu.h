@@ -317,6 +317,11 @@ int dora_node_dataflow_counters(dora_node* node, const char* node_id, uint64_t* 
  * sources below DORA_GPU_AQL_MAX_BYTES, default 32 MiB, <= 8 segments) or hipLaunchKernel on
  * the node's fill streams (larger, host sources, compacting transforms, relays). */
 int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_packs);
+/* dora_node_send_output of device arrays keeps the plans of recent sends that read no array
+ * bytes (fixed-width and nested arrays with known null counts), keyed by everything such a plan
+ * depends on (schema strings and flags, lengths, offsets, null counts, buffer addresses): a
+ * sender re-sending the same buffers plans each once.  Sends served from it, plans kept. */
+int dora_node_plan_cache_stats(dora_node* node, uint64_t* hits, uint64_t* entries);
 /* Cross-GPU edges: an input whose slot lives on another GPU is pulled over xGMI
  * into a local receive slot on first access (dora_event_data / dora_event_array) and the
  * producer's token is returned at once; dora_node_forward pulls it straight into an outgoing

@@ -607,6 +607,45 @@ def _roundtrip_through_node(launcher, names, env=None):
     return out
 
 
+def test_plan_cache_repeated_and_reused_addresses(launcher):
+    """The node's plan cache: the same device array sent three times is planned once and every
+    copy arrives intact; arrays allocated afterwards (possibly at the freed addresses, with
+    other types, lengths and null counts) get plans of their own."""
+    import threading
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from tests.golden import recipes
+    names = ["point_cloud_small", "struct_nulls_sliced", "list_i64_nulls", "i32_nulls_1000",
+             "f64_sliced_nulls", "fixed_size_list", "deep_nesting", "point_cloud_small"]
+    assert set(names) <= set(recipes.CASES)
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["x"]},
+        {"id": "dst", "path": "dynamic", "inputs": {"x": {"source": "src/x", "queue_size": 1000}}},
+    ]}
+    with Dataflow(desc, launcher=launcher) as df:
+        box = {}
+        t = threading.Thread(target=lambda: box.update(dst=Node("dst", dataflow=df.shm, device=0)))
+        t.start()
+        src = Node("src", dataflow=df.shm, device=0)
+        t.join(60)
+        dst = box["dst"]
+        for name in names:
+            arr = recipes.build(name)
+            with DeviceArray.from_pyarrow(arr) as da:
+                for k in range(3):
+                    src.send_output("x", da, {"name": name, "k": k})
+                    ev = dst.next(timeout=30)
+                    assert ev["metadata"] == {"name": name, "k": k}
+                    assert ev["value"].to_pyarrow().equals(arr), (name, k)
+                    del ev
+        stats = src.plan_cache_stats()
+        src.close()
+        dst.close()
+        df.wait(30)
+    assert stats["hits"] >= 2 * len(names), stats
+
+
 def test_in_sample_validity_type_info_and_roundtrip(launcher):
     """Device arrays sent by a node carry their validity bitmaps in the sample's tail (tag 2);
     the receiver's ArrowTypeInfo (dora_event_type_info, inline form restored from the slot) is
