@@ -643,7 +643,9 @@ def test_plan_cache_repeated_and_reused_addresses(launcher):
         src.close()
         dst.close()
         df.wait(30)
-    assert stats["hits"] >= 2 * len(names), stats
+    # arrays whose plan reads device bytes (slices exported with an unknown null count) are
+    # planned every time; the others twice from the cache
+    assert stats["entries"] >= 4 and stats["hits"] >= 2 * stats["entries"], stats
 
 
 def test_in_sample_validity_type_info_and_roundtrip(launcher):
