@@ -1,0 +1,68 @@
+"""The reference-side Rust binding (integration/rust/): no Rust toolchain in this image, so the
+crates are checked as text against the C ABI they bind — every function of include/dora_gpu.h
+is declared in dora-gpu-sys/src/ffi.rs with the same parameter count, the generated file is
+current, and the safe crate names only symbols the header declares."""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUST = os.path.join(ROOT, "integration", "rust")
+sys.path.insert(0, os.path.join(RUST))
+
+
+def _header_prototypes():
+    import gen_ffi
+    return {name: (0 if args.strip() in ("", "void") else len(args.split(",")))
+            for _, name, args in gen_ffi.prototypes(open(gen_ffi.HEADER).read())}
+
+
+def _rust_externs(path):
+    txt = open(path).read()
+    block = txt[txt.index('extern "C" {'):]
+    out = {}
+    for m in re.finditer(r"pub fn (\w+)\(([^)]*)\)", block):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if not args else len(args.split(", "))
+    return out
+
+
+def test_generated_ffi_is_current():
+    r = subprocess.run([sys.executable, os.path.join(RUST, "gen_ffi.py"), "--check"])
+    assert r.returncode == 0, "run integration/rust/gen_ffi.py: ffi.rs is stale"
+
+
+def test_every_header_function_is_declared_with_its_arity():
+    want = _header_prototypes()
+    got = _rust_externs(os.path.join(RUST, "dora-gpu-sys", "src", "ffi.rs"))
+    assert set(got) == set(want), (sorted(set(want) - set(got)), sorted(set(got) - set(want)))
+    assert got == want
+    # part of what the library exports (test_plan_host.py; the rest is the operator API of
+    # include/dora_operator_api.h, which the reference's own C operator crate binds)
+    from tests.test_plan_host import header_functions
+    assert set(want) <= header_functions()
+
+
+def test_safe_crate_uses_only_declared_symbols():
+    declared = set(_header_prototypes())
+    src = os.path.join(RUST, "dora-node-api-gpu", "src")
+    used = set()
+    for f in os.listdir(src):
+        used |= set(re.findall(r"sys::(dora_\w+)\s*\(", open(os.path.join(src, f)).read()))
+    assert used and used <= declared, sorted(used - declared)
+
+
+def test_device_ipc_wire_order_matches_wire_h():
+    """DeviceIpc::encode writes the fields in WBuf::data's order (dora_amd/csrc/wire.h)."""
+    wire = open(os.path.join(ROOT, "dora_amd", "csrc", "wire.h")).read()
+    c_body = wire[wire.index("void data(const DataMsg& d)"):wire.index("void metadata(")]
+    c_fields = re.findall(r"d\.ipc\.(\w+)", c_body)
+    rs = open(os.path.join(RUST, "dora-node-api-gpu", "src", "device_ipc.rs")).read()
+    r_body = rs[rs.index("pub fn encode("):rs.index("pub fn decode(")]
+    r_fields = re.findall(r"self\.(\w+)", r_body)
+    rename = {"drop_token": "token"}
+    r_fields = [rename.get(f, f) for f in r_fields if f != "fill"]
+    c_fields = [f for f in c_fields if f not in ("fill", "flag_node", "flag_index", "epoch",
+                                                  "event")]
+    assert r_fields == c_fields, (r_fields, c_fields)
