@@ -161,6 +161,9 @@ _SIGS = {
     "dora_daemon_run": (c_int, [c_void_p, c_int64]),
     "dora_daemon_request_stop": (c_int, [c_void_p]),
     "dora_daemon_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_daemon_listen_port": (c_int, [c_void_p, POINTER(c_int)]),
+    "dora_daemon_remote_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64),
+                                         POINTER(c_uint64)]),
     "dora_daemon_free": (None, [c_void_p]),
 }
 

@@ -9,7 +9,10 @@
 //   * CloseOutputs / OutputsDone -> InputClosed / AllInputsClosed;
 //   * PendingNodes: nodes get Ready once every node of the dataflow has subscribed.
 // Unlike the reference (F8, lib.rs:1361-1376) it never opens or copies a sample: device samples
-// are routed as IPC handles, so the daemon touches no payload bytes at all.
+// are routed as IPC handles, so the routing thread touches no payload bytes at all.  Outputs
+// with receivers under another machine's daemon go through interdaemon.h: a forwarder thread
+// stages them to the host and sends InterDaemonEvent::Output (lib.rs:976-1000); remote nodes
+// feeding local inputs are proxy nodes of the gateway, which re-sends their messages here.
 #include <signal.h>
 #include <sys/types.h>
 
@@ -28,6 +31,7 @@
 
 #include "bcast.h"
 #include "common.h"
+#include "interdaemon.h"
 #include "dora_gpu.h"
 #include "shm.h"
 #include "trace.h"
@@ -137,7 +141,23 @@ class Daemon {
       ev_.emplace_back(region_.get(), &e.events);
       drop_.emplace_back(region_.get(), &e.drops);
     }
+    bool any_remote = false;
+    for (auto& m : remote_) any_remote |= !m.empty();
+    if (any_remote) fwd_.reset(new Forwarder(region_.get(), dataflow_id_, peers_));
+    if (listen_port_ >= 0 || !proxies_.empty())
+      gw_.reset(new Gateway(shm, dataflow_id_, listen_host_, listen_port_ < 0 ? 0 : listen_port_,
+                            proxies_));
   }
+
+  ~Daemon() {
+    gw_.reset();  // proxies finish first (their outputs close), then the forwarder drains
+    fwd_.reset();
+  }
+
+  int listen_port() const { return gw_ ? gw_->port() : -1; }
+  uint64_t forwarded() const { return fwd_ ? fwd_->forwarded() : 0; }
+  uint64_t staged_bytes() const { return fwd_ ? fwd_->staged_bytes() : 0; }
+  uint64_t remote_received() const { return gw_ ? gw_->received() : 0; }
 
   // Returns 0 when every node is done, DORA_ERR_TIMEOUT after timeout_ms (<0: no timeout).
   int run(int64_t timeout_ms) {
@@ -166,6 +186,15 @@ class Daemon {
         }
       }
       work |= flush_overflow();
+      if (fwd_) {
+        released_.clear();
+        fwd_->take_released(&released_);
+        for (const DropToken& t : released_) {
+          auto it = tokens_.find(t);
+          if (it != tokens_.end() && it->second.release(kForwarder)) check_drop_token(t);
+        }
+        work |= !released_.empty();
+      }
       const uint64_t now = mono_ns();
       auto leave = [&](int rc) {
         if (idle_from && !work) add_idle_ns(now - idle_from);
@@ -221,6 +250,10 @@ class Daemon {
       uint32_t q;
     };
     std::vector<In> inputs;
+    struct Remote {
+      std::string node, out, machine;
+    };
+    std::vector<Remote> remote_lines;
     while (std::getline(in, line)) {
       std::istringstream ls(line);
       std::string kw;
@@ -244,6 +277,27 @@ class Daemon {
         ls >> x.node >> x.input >> x.src >> x.out >> x.q;
         if (ls.fail()) throw std::invalid_argument("bad input line: " + line);
         inputs.push_back(x);
+      } else if (kw == "dataflow") {
+        ls >> dataflow_id_;
+      } else if (kw == "listen") {  // listen <host> <port>: peer daemons connect here
+        ls >> listen_host_ >> listen_port_;
+        if (ls.fail()) throw std::invalid_argument("bad listen line: " + line);
+      } else if (kw == "machine") {  // machine <name> <host> <port>: a peer daemon
+        std::string name;
+        PeerAddr a;
+        ls >> name >> a.host >> a.port;
+        if (ls.fail()) throw std::invalid_argument("bad machine line: " + line);
+        peers_[name] = a;
+      } else if (kw == "remote") {  // remote <node> <output> <machine>: receivers over there
+        std::string node, out, machine;
+        ls >> node >> out >> machine;
+        if (ls.fail()) throw std::invalid_argument("bad remote line: " + line);
+        remote_lines.push_back({node, out, machine});
+      } else if (kw == "proxy") {  // proxy <node> <gpu>: a remote node feeding local inputs
+        ProxySpec p;
+        ls >> p.node_id >> p.device;
+        if (ls.fail()) throw std::invalid_argument("bad proxy line: " + line);
+        proxies_.push_back(p);
       } else {
         throw std::invalid_argument("unknown spec keyword: " + kw);
       }
@@ -259,12 +313,26 @@ class Daemon {
                                     x.src + "/" + x.out);
       outputs_[idx[x.src]][x.out].push_back({idx[x.node], x.input});
     }
+    remote_.resize(nodes_.size());
+    for (auto& r : remote_lines) {
+      if (!idx.count(r.node) || !nodes_[idx[r.node]].outputs.count(r.out))
+        throw std::invalid_argument("remote line names unknown output " + r.node + "/" + r.out);
+      if (!peers_.count(r.machine))
+        throw std::invalid_argument("remote line names unknown machine " + r.machine);
+      remote_[idx[r.node]][r.out].push_back(r.machine);
+    }
+    for (auto& p : proxies_) {
+      if (!idx.count(p.node_id)) throw std::invalid_argument("proxy of unknown node " + p.node_id);
+      const auto& outs = nodes_[idx[p.node_id]].outputs;
+      p.outputs.assign(outs.begin(), outs.end());
+    }
   }
 
   bool all_done() const {
     for (auto& n : nodes_)
       if (!n.done) return false;
-    return !nodes_.empty();
+    // messages still being staged / sent to other machines keep the daemon up
+    return !nodes_.empty() && (!fwd_ || fwd_->idle());
   }
 
   void push_event(int node, uint32_t kind, std::vector<uint8_t> payload) {
@@ -400,6 +468,19 @@ class Daemon {
         }
       }
     }
+    auto rit = remote_[i].find(output);
+    if (fwd_ && rit != remote_[i].end()) {
+      // receivers under other daemons (lib.rs:976-1000): the forwarder stages and sends it;
+      // it holds the token until its copy is done
+      ForwardJob job;
+      job.machines = rit->second;
+      job.node_id = nodes_[i].id;
+      job.output_id = std::string(output);
+      job.tail.assign(tail, tail + tail_len);
+      job.data = data;
+      if (ti) ti->add(kForwarder);
+      fwd_->push(std::move(job));
+    }
     if (ti) check_drop_token(data.ipc.token);
   }
 
@@ -411,7 +492,8 @@ class Daemon {
     const int32_t root_dev = h->nodes[i].device.load();
     std::set<int32_t> devs{root_dev};
     std::vector<Receiver> members;
-    bool ok = root_dev >= 0 && nodes_[i].outputs.count(output);
+    // outputs with receivers on other machines stay on pulls: their forwarder reads the slot
+    bool ok = root_dev >= 0 && nodes_[i].outputs.count(output) && !remote_[i].count(output);
     auto it = outputs_[i].find(output);
     if (ok && it != outputs_[i].end()) {
       for (const Receiver& rc : it->second) {
@@ -452,6 +534,15 @@ class Daemon {
 
   void close_output(int i, const std::string& output) {
     if (!nodes_[i].outputs.erase(output)) return;
+    auto rit = remote_[i].find(output);
+    if (fwd_ && rit != remote_[i].end()) {
+      ForwardJob job;
+      job.machines = rit->second;
+      job.node_id = nodes_[i].id;
+      job.closed = true;
+      job.closed_outputs = {output};
+      fwd_->push(std::move(job));
+    }
     auto it = outputs_[i].find(output);
     if (it == outputs_[i].end()) return;
     for (const Receiver& rc : it->second) {
@@ -505,6 +596,16 @@ class Daemon {
   std::pmr::unsynchronized_pool_resource token_pool_;
   std::pmr::unordered_map<DropToken, TokenInfo, DropTokenHash> tokens_{&token_pool_};
   WBuf ev_buf_;  // event encoding scratch, reused
+  // inter-daemon (interdaemon.h): per node, output -> machines with receivers; peers; proxies
+  static constexpr int kForwarder = -2;  // the forwarder's hold on a drop token
+  std::vector<std::map<std::string, std::vector<std::string>, std::less<>>> remote_;
+  std::map<std::string, PeerAddr> peers_;
+  std::vector<ProxySpec> proxies_;
+  std::string dataflow_id_ = "local", listen_host_ = "127.0.0.1";
+  int listen_port_ = -1;
+  std::unique_ptr<Forwarder> fwd_;
+  std::unique_ptr<Gateway> gw_;
+  std::vector<DropToken> released_;
   std::vector<RingReader> req_;
   std::vector<RingWriter> ev_, drop_;
   bool ready_sent_ = false;
@@ -550,6 +651,21 @@ int dora_daemon_stats(dora_daemon* d, uint64_t* routed, uint64_t* pending_tokens
   if (!d) return dora::fail(DORA_ERR_INVALID, "NULL daemon");
   if (routed) *routed = d->d->routed();
   if (pending_tokens) *pending_tokens = d->d->pending_tokens();
+  return DORA_OK;
+}
+
+int dora_daemon_listen_port(dora_daemon* d, int* port) {
+  if (!d || !port) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *port = d->d->listen_port();
+  return DORA_OK;
+}
+
+int dora_daemon_remote_stats(dora_daemon* d, uint64_t* forwarded, uint64_t* staged_bytes,
+                             uint64_t* received) {
+  if (!d) return dora::fail(DORA_ERR_INVALID, "NULL daemon");
+  if (forwarded) *forwarded = d->d->forwarded();
+  if (staged_bytes) *staged_bytes = d->d->staged_bytes();
+  if (received) *received = d->d->remote_received();
   return DORA_OK;
 }
 

@@ -475,7 +475,8 @@ void put64(std::vector<uint8_t>& o, uint64_t v) {
 }
 
 // One type-info node (serialize_type_info's layout) copied to `o` with tag-2 bitmaps inlined.
-void inline_ti(Cursor& c, std::vector<uint8_t>& o, const uint8_t* sample, uint64_t ext_len) {
+void inline_ti(Cursor& c, std::vector<uint8_t>& o, const uint8_t* sample, uint64_t ext_len,
+               bool host) {
   Cursor sc = c;
   const uint32_t sl = sc.u32();
   copy_bytes(c, o, 4 + size_t(sl) + 16);  // schema, len, null_count
@@ -487,8 +488,9 @@ void inline_ti(Cursor& c, std::vector<uint8_t>& o, const uint8_t* sample, uint64
     put64(o, vl);
     const size_t at = o.size();
     o.resize(at + vl);
-    if (vl) hip_ok(hipMemcpy(o.data() + at, sample + off, vl, hipMemcpyDeviceToHost),
-                   "validity read-back");
+    if (vl && host) std::memcpy(o.data() + at, sample + off, vl);
+    else if (vl) hip_ok(hipMemcpy(o.data() + at, sample + off, vl, hipMemcpyDeviceToHost),
+                        "validity read-back");
   } else {
     o.push_back(tag);
     if (tag == 1) {
@@ -504,7 +506,7 @@ void inline_ti(Cursor& c, std::vector<uint8_t>& o, const uint8_t* sample, uint64
   copy_bytes(c, o, 8 + 4 + 16 * size_t(nb));  // offset, buffer offsets
   const uint32_t nch = c.u32();
   for (int i = 0; i < 4; ++i) o.push_back(static_cast<uint8_t>(nch >> (8 * i)));
-  for (uint32_t k = 0; k < nch; ++k) inline_ti(c, o, sample, ext_len);
+  for (uint32_t k = 0; k < nch; ++k) inline_ti(c, o, sample, ext_len, host);
 }
 
 bool has_in_sample(const TiNode& t) {
@@ -517,7 +519,7 @@ bool has_in_sample(const TiNode& t) {
 }  // namespace
 
 int inline_type_info(const uint8_t* ti, size_t ti_len, const void* sample, uint64_t ext_len,
-                     std::vector<uint8_t>* out, bool* changed) {
+                     std::vector<uint8_t>* out, bool* changed, bool host) {
   return guarded([&] {
     *changed = false;
     Cursor c{ti, ti_len};
@@ -528,7 +530,7 @@ int inline_type_info(const uint8_t* ti, size_t ti_len, const void* sample, uint6
     Cursor w{ti, ti_len};
     std::vector<uint8_t> o;
     o.reserve(ti_len + 4096);
-    inline_ti(w, o, static_cast<const uint8_t*>(sample), ext_len);
+    inline_ti(w, o, static_cast<const uint8_t*>(sample), ext_len, host);
     out->swap(o);
     *changed = true;
   });

@@ -20,7 +20,9 @@ int import_sample(const void* sample, uint64_t sample_len, const uint8_t* type_i
 
 // The reference (inline) form of a type info: in-sample bitmaps (tag 2) read back from the
 // device sample into tag-1 bytes.  `*changed` = false (out untouched) when there were none.
+// `host`: the sample is in host memory (a staged copy), read without HIP.
 int inline_type_info(const uint8_t* type_info, size_t type_info_len, const void* sample,
-                     uint64_t ext_len, std::vector<uint8_t>* out, bool* changed);
+                     uint64_t ext_len, std::vector<uint8_t>* out, bool* changed,
+                     bool host = false);
 
 }  // namespace dora

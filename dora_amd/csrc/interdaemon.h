@@ -1,0 +1,149 @@
+// Inter-daemon data path: outputs whose receivers run under another machine's
+// daemon, the counterpart of `InterDaemonEvent` (libraries/message/src/daemon_to_daemon.rs:9-21)
+// and of the forwarding in `send_out` (binaries/daemon/src/lib.rs:955-1000).
+//
+// Sending side (Forwarder): the daemon hands every message of such an output to one forwarder
+// thread, in routing order.  A device sample is staged to the host there — wait for the
+// producer's fill (flag / event), map the slot (IPC, cached), one D2H copy — its validity
+// tail folded back into the inline ArrowTypeInfo, and the producer's drop token released
+// once the copy is done.  The message then leaves over a TCP connection per peer machine.
+// The daemon's routing thread never waits on any of this.
+//
+// Receiving side (Gateway): a listener accepts peer daemons; every remote source node that
+// feeds a local input has a proxy node in the local region, served by a thread of the gateway:
+// it re-sends each remote message on the proxy's output (a device sample uploaded H2D for GPU
+// proxies, an inline sample for host-only ones), so local receivers see an ordinary input;
+// OutputsClosed closes the proxy's outputs and, once all are closed, finishes the proxy.
+//
+// Wire (little endian, one frame = u64 length + payload; str / bytes = u64 length + bytes):
+//   u8 kind, str dataflow_id, str node_id,
+//   kind 0 Output:        str output_id, u16 metadata_version, u64 timestamp_ns,
+//                         bytes type_info (C ABI form, validity inline), bytes parameters,
+//                         u8 has_data [bytes data]
+//   kind 1 OutputsClosed: u32 n, n x str output_id
+// The reference frames bincode of Timestamped<InterDaemonEvent>; its InputsClosed names the
+// receiving inputs, ours the closed outputs (the receiving daemon maps them to its inputs).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "shm.h"
+#include "wire.h"
+
+namespace dora {
+
+enum : uint8_t { IDE_OUTPUT = 0, IDE_OUTPUTS_CLOSED = 1 };
+
+struct InterDaemonEvent {
+  uint8_t kind = IDE_OUTPUT;
+  std::string dataflow_id, node_id;
+  std::string output_id;                 // Output
+  std::vector<std::string> outputs;      // OutputsClosed
+  uint16_t meta_version = 0;
+  uint64_t timestamp_ns = 0;
+  std::vector<uint8_t> type_info, parameters;
+  bool has_data = false;
+  std::vector<uint8_t> data;
+};
+
+void encode_ide(const InterDaemonEvent& e, std::vector<uint8_t>& out);
+InterDaemonEvent decode_ide(const uint8_t* p, size_t n);  // throws on malformed input
+
+struct PeerAddr {
+  std::string host;
+  int port = 0;
+};
+
+// One message of a local output with remote receivers, as the daemon routed it.
+struct ForwardJob {
+  std::vector<std::string> machines;
+  std::string node_id, output_id;
+  std::vector<uint8_t> tail;  // the request's metadata + data bytes (REQ_SEND_MESSAGE tail)
+  DataMsg data;
+  bool closed = false;                   // OutputsClosed instead of a message
+  std::vector<std::string> closed_outputs;
+};
+
+class Forwarder {
+ public:
+  Forwarder(Region* region, std::string dataflow_id, std::map<std::string, PeerAddr> peers);
+  ~Forwarder();
+  void push(ForwardJob job);
+  // Drop tokens whose staging is done (the daemon releases the forwarder's hold on them).
+  void take_released(std::vector<DropToken>* out);
+  bool idle();  // queue empty and nothing in progress
+  uint64_t forwarded() const { return forwarded_.load(); }
+  uint64_t staged_bytes() const { return staged_bytes_.load(); }
+
+ private:
+  void loop();
+  void handle(ForwardJob& job);
+  bool stage(const ForwardJob& job, std::vector<uint8_t>* bytes, std::vector<uint8_t>* ti);
+  bool send_to(const std::string& machine, const std::vector<uint8_t>& frame);
+
+  Region* region_;
+  std::string dataflow_id_;
+  std::map<std::string, PeerAddr> peers_;
+  std::map<std::string, int> socks_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<ForwardJob> q_;
+  std::vector<DropToken> released_;
+  bool busy_ = false, stop_ = false;
+  std::atomic<uint64_t> forwarded_{0}, staged_bytes_{0};
+  // staging: IPC mappings of producers' slots, a pinned host buffer
+  std::map<std::string, void*> maps_;
+  uint8_t* pinned_ = nullptr;
+  uint64_t pinned_cap_ = 0;
+  std::thread th_;
+};
+
+// A remote source node served locally: its id, the local GPU its re-sent samples go to (-1:
+// host-only) and its outputs.
+struct ProxySpec {
+  std::string node_id;
+  int device = -1;
+  std::vector<std::string> outputs;
+};
+
+class Gateway {
+ public:
+  Gateway(std::string shm_name, std::string dataflow_id, std::string listen_host, int listen_port,
+          std::vector<ProxySpec> proxies);
+  ~Gateway();
+  int port() const { return port_; }
+  uint64_t received() const { return received_.load(); }
+
+ private:
+  struct Proxy {
+    ProxySpec spec;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<InterDaemonEvent> q;
+    std::thread th;
+  };
+  void accept_loop();
+  void read_loop(int fd);
+  void proxy_loop(Proxy* p);
+
+  std::string shm_, dataflow_id_;
+  int listen_fd_ = -1, port_ = 0;
+  std::atomic<bool> stop_{false};
+  std::map<std::string, std::unique_ptr<Proxy>> proxies_;
+  std::thread accept_th_;
+  std::mutex readers_mu_;
+  std::vector<std::thread> readers_;
+  std::vector<int> reader_fds_;
+  std::atomic<uint64_t> received_{0};
+};
+
+}  // namespace dora

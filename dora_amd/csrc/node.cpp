@@ -1145,7 +1145,7 @@ void put_metadata(WBuf& w, const std::vector<uint8_t>& ti, const uint8_t* params
 
 int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
                 const uint8_t* params, size_t params_len, dora_sample* sample,
-                DropToken* token_out = nullptr) {
+                DropToken* token_out = nullptr, uint64_t ts_override = 0) {
   handle_finished_drop_tokens(n);
   if (!n->outputs.count(output_id)) {
     delete sample;  // the sample is consumed either way
@@ -1154,7 +1154,9 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
                 "output is defined within your dataflow YAML file.",
                 output_id);
   }
-  const uint64_t ts = now_ns();  // Metadata::from_parameters(clock.new_timestamp(), ..) mod.rs:258
+  // Metadata::from_parameters(clock.new_timestamp(), ..) mod.rs:258; a proxy of a remote
+  // node keeps the producer's timestamp (the inter-daemon message's metadata)
+  const uint64_t ts = ts_override ? ts_override : now_ns();
   DataMsg d;
   Slot* slot = nullptr;
   if (sample) {
@@ -1615,6 +1617,17 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
 }
 
 }  // namespace
+
+// A remote node's message re-sent by its proxy (interdaemon.cpp): the metadata keeps the
+// producer's timestamp.
+int proxy_send(dora_node* n, const char* output_id, const uint8_t* ti, size_t ti_len,
+               const uint8_t* params, size_t params_len, dora_sample* sample, uint64_t ts) {
+  DORA_GUARD_BEGIN
+  std::vector<uint8_t> t(ti, ti + ti_len);
+  return send_sample(n, output_id, t, params, params_len, sample, nullptr, ts);
+  DORA_GUARD_END
+}
+
 }  // namespace dora
 
 extern "C" {

@@ -47,7 +47,10 @@ int main(int argc, char** argv) {
   }
   std::signal(SIGTERM, on_signal);
   std::signal(SIGINT, on_signal);
-  std::printf("{\"daemon\": \"ready\", \"shm\": \"%s\"}\n", shm.c_str());
+  int port = -1;
+  dora_daemon_listen_port(d, &port);
+  std::printf("{\"daemon\": \"ready\", \"shm\": \"%s\", \"listen_port\": %d}\n", shm.c_str(),
+              port);
   std::fflush(stdout);
   const uint64_t t_start = mono_ns_main();
   int rc;
@@ -68,10 +71,14 @@ int main(int argc, char** argv) {
   uint64_t idle = 0;
   dora_gpu_busy_stats(&idle, nullptr);
   const double busy_us = (double(mono_ns_main() - t_start) - double(idle)) / 1e3;
+  uint64_t fwd = 0, staged = 0, received = 0;
+  dora_daemon_remote_stats(d, &fwd, &staged, &received);
   std::printf("{\"daemon\": \"done\", \"rc\": %d, \"routed\": %llu, \"pending_tokens\": %llu, "
-              "\"busy_us\": %.1f, \"busy_us_per_routed\": %.3f}\n",
+              "\"busy_us\": %.1f, \"busy_us_per_routed\": %.3f, \"forwarded\": %llu, "
+              "\"staged_bytes\": %llu, \"remote_received\": %llu}\n",
               rc, (unsigned long long)routed, (unsigned long long)pending, busy_us,
-              routed ? busy_us / double(routed) : 0.0);
+              routed ? busy_us / double(routed) : 0.0, (unsigned long long)fwd,
+              (unsigned long long)staged, (unsigned long long)received);
   dora_daemon_free(d);
   return rc == 0 ? 0 : 1;
 }

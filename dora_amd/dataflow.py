@@ -39,7 +39,8 @@ class NodeSpec:
     inputs: Dict[str, tuple] = field(default_factory=dict)  # input -> (src_node, src_out, queue)
     outputs: List[str] = field(default_factory=list)
     env: Dict[str, str] = field(default_factory=dict)
-    gpu: int = 0
+    gpu: int = 0          # -1: host-only node
+    machine: str = ""     # `_unstable_deploy.machine` ("" = the default machine)
 
 
 SINGLE_OPERATOR_DEFAULT_ID = "op"  # descriptor/mod.rs:35
@@ -124,7 +125,9 @@ def parse_descriptor(desc) -> List[NodeSpec]:
                                  f"not one of its outputs")
             spec.env["DORA_GPU_SEND_STDOUT_AS"] = str(n["send_stdout_as"])
             spec.env.setdefault("PYTHONUNBUFFERED", "1")  # lines, not blocks, through the pipe
-        spec.gpu = int((n.get("_unstable_deploy") or {}).get("gpu", 0))
+        deploy = n.get("_unstable_deploy") or {}
+        spec.gpu = int(deploy.get("gpu", 0))
+        spec.machine = str(deploy.get("machine", ""))
         for inp, src in (n.get("inputs") or {}).items():
             q = DEFAULT_QUEUE_SIZE
             if isinstance(src, dict):
@@ -146,12 +149,44 @@ def parse_descriptor(desc) -> List[NodeSpec]:
     return nodes
 
 
-def daemon_spec(nodes: List[NodeSpec]) -> str:
-    lines = [f"node {n.id}" for n in nodes]
-    for n in nodes:
-        lines += [f"output {n.id} {o}" for o in n.outputs]
-    for n in nodes:
+def daemon_spec(nodes: List[NodeSpec], machine: Optional[str] = None,
+                machines: Optional[Dict[str, tuple]] = None, dataflow_id: str = "local") -> str:
+    """The daemon's spec for the nodes deployed on `machine` (None: every node is local).
+
+    A dataflow spanning machines (`_unstable_deploy.machine`, one daemon per machine): remote
+    nodes that feed local inputs become proxies of the local daemon, local outputs with remote
+    receivers get a `remote` line per machine, `machines` = {name: (host, port)} of the peer
+    daemons (this machine's entry is where it listens)."""
+    local = [n for n in nodes if machine is None or n.machine == machine]
+    local_ids = {n.id for n in local}
+    by_id = {n.id: n for n in nodes}
+    proxies = {}  # remote source node -> GPU of its first local receiver
+    for n in local:
+        for _, (src, _, _) in n.inputs.items():
+            if src not in local_ids:
+                proxies.setdefault(src, n.gpu)
+    lines = [f"dataflow {dataflow_id}"]
+    if machine is not None and machines:
+        for name, (host, port) in sorted(machines.items()):
+            if name == machine:
+                lines.append(f"listen {host} {port}")
+            else:
+                lines.append(f"machine {name} {host} {port}")
+    lines += [f"node {nid}" for nid in [n.id for n in local] + sorted(proxies)]
+    for nid in [n.id for n in local] + sorted(proxies):
+        lines += [f"output {nid} {o}" for o in by_id[nid].outputs]
+    for src, gpu in sorted(proxies.items()):
+        lines.append(f"proxy {src} {gpu}")
+    for n in local:
         lines += [f"input {n.id} {i} {s} {o} {q}" for i, (s, o, q) in n.inputs.items()]
+    remote = set()
+    for n in nodes:
+        if n.id in local_ids:
+            continue
+        for _, (src, out, _) in n.inputs.items():
+            if src in local_ids:
+                remote.add((src, out, n.machine))
+    lines += [f"remote {s} {o} {m}" for s, o, m in sorted(remote)]
     return "\n".join(lines) + "\n"
 
 
@@ -197,8 +232,15 @@ class _Proc:
 
 class Dataflow:
     def __init__(self, descriptor, ring_bytes: int = 4 << 20, name: Optional[str] = None,
-                 launcher=None, log_dir: Optional[str] = None):
-        self.nodes = parse_descriptor(descriptor)
+                 launcher=None, log_dir: Optional[str] = None, machine: Optional[str] = None,
+                 machines: Optional[Dict[str, tuple]] = None, dataflow_id: str = "local"):
+        """`machine`: run only the nodes deployed on this machine (`_unstable_deploy.machine`)
+        under this daemon; `machines` maps machine names to the (host, port) their daemons
+        listen on (port 0 for this machine: any free port, see `listen_port`)."""
+        self.all_nodes = parse_descriptor(descriptor)
+        self.machine, self.machines, self.dataflow_id = machine, machines, dataflow_id
+        self.nodes = [n for n in self.all_nodes if machine is None or n.machine == machine]
+        self.listen_port: Optional[int] = None
         self.shm = name or f"/dora-gpu-{os.getpid()}-{next(_counter)}"
         self.ring_bytes = ring_bytes
         self.launcher = launcher
@@ -219,6 +261,18 @@ class Dataflow:
         return {"DORA_GPU_DATAFLOW": self.shm, "DORA_NODE_ID": n.id,
                 "DORA_GPU_DEVICE": str(n.gpu)}
 
+    @staticmethod
+    def _ready_port(log: str) -> Optional[int]:
+        import json
+        for line in log.splitlines():
+            if '"ready"' in line:
+                try:
+                    p = json.loads(line).get("listen_port", -1)
+                    return p if p >= 0 else None
+                except ValueError:
+                    return None
+        return None
+
     def log(self, name: str) -> str:
         p = os.path.join(self.log_dir, f"{name}.log")
         return open(p).read() if os.path.exists(p) else ""
@@ -226,7 +280,7 @@ class Dataflow:
     def start(self, timeout: float = 30.0):
         fd, self._spec_file = tempfile.mkstemp(prefix="dora-gpu-spec-", suffix=".txt")
         with os.fdopen(fd, "w") as f:
-            f.write(daemon_spec(self.nodes))
+            f.write(daemon_spec(self.all_nodes, self.machine, self.machines, self.dataflow_id))
         dlog = os.path.join(self.log_dir, "_daemon.log")
         self.daemon = _Proc([resolve("dora-gpu-daemon"), "--shm", self.shm, "--spec",
                              self._spec_file, "--ring-bytes", str(self.ring_bytes)],
@@ -236,6 +290,7 @@ class Dataflow:
             if self.daemon.poll() is not None or time.time() > deadline:
                 raise RuntimeError(f"daemon failed to start: {self.log('_daemon')!r}")
             time.sleep(0.005)
+        self.listen_port = self._ready_port(self.log("_daemon"))
         for n in self.nodes:
             if n.path == "dynamic":
                 continue

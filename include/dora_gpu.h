@@ -370,7 +370,17 @@ int dora_node_send_profile(dora_node* node, double* out_us, size_t n_out, uint64
 /* ------------------------------------------------------------------------------------------ */
 typedef struct dora_daemon dora_daemon;
 /* Create the dataflow region `shm_name` ("/name").  `spec` lines:
- *   node <id> | output <node> <output> | input <node> <input> <src_node> <src_output> <queue> */
+ *   node <id> | output <node> <output> | input <node> <input> <src_node> <src_output> <queue>
+ * and, for dataflows spanning machines (InterDaemonEvent, libraries/message/src/
+ * daemon_to_daemon.rs:9-21; the reference's `_unstable_deploy.machine`):
+ *   dataflow <id>                      shared by the daemons of one dataflow
+ *   listen <host> <port>               accept peer daemons (port 0: any free port)
+ *   machine <name> <host> <port>       a peer daemon
+ *   remote <node> <output> <machine>   this output has receivers under that machine's daemon:
+ *                                      its messages are staged to the host and sent there
+ *   proxy <node> <gpu>                 <node> runs on another machine and feeds local inputs:
+ *                                      the daemon serves it, re-sending its messages locally
+ *                                      (device samples on GPU <gpu>, -1: inline host samples) */
 int dora_daemon_create(const char* shm_name, const char* spec, size_t ring_bytes,
                        dora_daemon** out);
 /* Route until every node is done (0), or timeout_ms elapses (DORA_ERR_TIMEOUT). */
@@ -378,6 +388,11 @@ int dora_daemon_run(dora_daemon* daemon, int64_t timeout_ms);
 /* Send Event::Stop to every node. */
 int dora_daemon_request_stop(dora_daemon* daemon);
 int dora_daemon_stats(dora_daemon* daemon, uint64_t* routed, uint64_t* pending_tokens);
+/* The port peer daemons connect to (-1: the spec has no `listen` and no `proxy` line). */
+int dora_daemon_listen_port(dora_daemon* daemon, int* port);
+/* Messages forwarded to other machines, device bytes staged for them, messages received. */
+int dora_daemon_remote_stats(dora_daemon* daemon, uint64_t* forwarded, uint64_t* staged_bytes,
+                             uint64_t* received);
 void dora_daemon_free(dora_daemon* daemon);
 
 #ifdef __cplusplus

@@ -14,7 +14,7 @@ const ARCH: &str = "gfx950";
 const LIB_SOURCES: &[&str] = &[
     "runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp", "bcast.cpp",
     "operator_api.cpp", "stdout_capture.cpp", "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp",
-    "aql.cpp",
+    "aql.cpp", "interdaemon.cpp",
 ];
 
 fn run(cmd: &mut Command) {
