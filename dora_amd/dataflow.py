@@ -245,6 +245,7 @@ class Dataflow:
         self.ring_bytes = ring_bytes
         self.launcher = launcher
         self.log_dir = log_dir or tempfile.mkdtemp(prefix="dora-gpu-logs-")
+        os.makedirs(self.log_dir, exist_ok=True)
         self.daemon: Optional[_Proc] = None
         self.procs: Dict[str, _Proc] = {}
         self._spec_file = None

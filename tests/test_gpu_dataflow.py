@@ -658,3 +658,75 @@ def test_in_sample_validity_type_info_and_roundtrip(launcher):
     for name, got, want, equal in _roundtrip_through_node(launcher, names):
         assert got == want, name
         assert equal, name
+
+
+def test_two_daemons_device_samples_bit_exact(launcher, tmp_path):
+    """A dataflow over two machines' daemons (here both on this box): machine A's forwarder
+    waits for each device sample's fill, maps the slot, stages it to the host (validity tails
+    folded back into the type info) and sends it over TCP; machine B's proxy uploads it into a
+    slot of its own and re-sends it.  4 MB payloads are checksummed by B's sink; point clouds
+    (nested, with nulls) arrive equal at a Python receiver."""
+    import threading
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from dora_amd.workloads import point_cloud
+    res = str(tmp_path / "sink.json")
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["data", "pc"],
+         "_unstable_deploy": {"machine": "A", "gpu": 0}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"data": {"source": "node/data", "queue_size": 1000}},
+         "env": {"DORA_BENCH_RESULT": res}, "_unstable_deploy": {"machine": "B", "gpu": 0}},
+        {"id": "recv", "path": "dynamic", "inputs": {"pc": {"source": "node/pc", "queue_size": 100}},
+         "_unstable_deploy": {"machine": "B", "gpu": 0}},
+    ]}
+    size, n_msgs = 4 << 20, 20
+    bufs, sums = _distinct_sources(4, size)
+    clouds = [point_cloud(3000, 5, seed=s) for s in (1, 2, 3)]
+    b = Dataflow(desc, machine="B", machines={"B": ("127.0.0.1", 0), "A": ("127.0.0.1", 1)},
+                 dataflow_id="df-gpu", launcher=launcher, log_dir=str(tmp_path / "B")).start()
+    a = Dataflow(desc, machine="A",
+                 machines={"A": ("127.0.0.1", 0), "B": ("127.0.0.1", b.listen_port)},
+                 dataflow_id="df-gpu", launcher=launcher, log_dir=str(tmp_path / "A")).start()
+    got, errs = [], []
+
+    def receiver():
+        try:
+            r = Node("recv", dataflow=b.shm, device=0)
+            for ev in r:
+                if ev["type"] == "INPUT":
+                    got.append((ev["metadata"]["seq"], ev["value"].to_pyarrow()))
+                    del ev
+            r.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    t = threading.Thread(target=receiver)
+    t.start()
+    try:
+        node = Node("node", dataflow=a.shm, device=0)
+        for k in range(n_msgs):
+            node.send_output_device_bytes("data", bufs[k % 4].ptr, size,
+                                          {"seq": k, "csum": sums[k % 4], "verify": True})
+        for k, pc in enumerate(clouds):
+            with DeviceArray.from_pyarrow(pc) as da:
+                node.send_output("pc", da, {"seq": k})
+        node.close()
+        t.join(60)
+        codes = {"A": a.wait(60), "B": b.wait(60)}
+        logs = {"A": a.log("_daemon"), "B": b.log("_daemon"), "sink": b.log("sink")}
+    finally:
+        a.stop()
+        b.stop()
+        for x in bufs:
+            x.free()
+    assert not errs, errs
+    assert codes["B"]["sink"] == 0 and codes["A"]["_daemon"] == 0 and codes["B"]["_daemon"] == 0, \
+        (codes, logs)
+    out = json.load(open(res))
+    assert sum(s["verified"] for s in out["series"]) == n_msgs, (out, logs)
+    assert sum(s["mismatches"] for s in out["series"]) == 0
+    assert [g[0] for g in got] == [0, 1, 2]
+    for (_, arr), pc in zip(got, clouds):
+        assert arr.equals(pc)
+    assert f'"forwarded": {n_msgs + 3 + 2}' in logs["A"], logs["A"]
