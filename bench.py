@@ -555,23 +555,38 @@ def main():
     barrier()
     device.set_device(local_rank)
     from dora_amd._lib import call
-    call("dora_gpu_device_sync")
+    presync = os.environ.get("DORA_BENCH_PRESYNC", "device")
+    if presync == "device":
+        call("dora_gpu_device_sync")
+    elif presync == "node":
+        node.sync()
     if not args.no_kernel_timing:
         node.region_begin()  # setup (profiling signals) before the clock starts
+    t0_ns = time.time_ns()
     t0 = time.perf_counter()
+    region_first_seq = seq
     for k in range(args.steps):
         meta = {"seq": seq, "t_start": time.time_ns()}
+        if k == 0:
+            meta["mark"] = True  # the sink stamps its receipt: start of the region's pipeline
         if k >= args.steps - late:
             meta.update({"csum": to_i64(csum), "verify_late": True})
         if k == args.steps - 1:
             meta["ack"] = True  # the sink acks the region's last message on receipt
         send(k, meta)
+        if k == 0:
+            t_first = time.perf_counter()
+            if os.environ.get("DORA_BENCH_FIRST_PHASES"):  # diagnosis: costs a call in the region
+                first_phases = node.send_profile()
         seq += 1
     t_sent = time.perf_counter()
+    t_sent_ns = time.time_ns()
     if not args.no_kernel_timing:
         node.region_mark()  # stop events after the last pack, while it is delivered
     wait_ack(seq - 1)
     t_acked = time.perf_counter()
+    t_acked_ns = time.time_ns()
+    region_ack_seq = seq - 1
     node.sync()  # every stream and AQL fill of this node complete (the ack implies it)
     elapsed = time.perf_counter() - t0
     barrier()
@@ -585,6 +600,9 @@ def main():
         # every message counted in `value` was delivered: the sink's queue dropped none
         "sink_dropped_in_region": sink_after["dropped_inputs"] - sink_before["dropped_inputs"],
         "host_send_loop_us": round((t_sent - t0) * 1e6, 1),
+        "first_send_us": round((t_first - t0) * 1e6, 1) if args.steps else None,
+        "first_send_phases_us": ({k: round(v, 2) for k, v in first_phases.items()}
+                                 if os.environ.get("DORA_BENCH_FIRST_PHASES") else None),
         "close_us": round((t_acked - t_sent) * 1e6, 1),
         "sync_us": round((t0 + elapsed - t_acked) * 1e6, 1),
         "late_verified_msgs": late}
@@ -608,6 +626,16 @@ def main():
     codes = df.wait(120)
     df.stop()
     sink = json.load(open(result_path)) if os.path.exists(result_path) else {"series": []}
+    # the close, split at the sink (realtime clocks of one host): last send -> the sink has the
+    # last message (its fill complete) -> ack sent -> the ack is back here
+    for a_seq, t_rx, t_ack in sink.get("acks", []):
+        if a_seq == region_first_seq:
+            region_setup["first_msg_receipt_us"] = round((t_rx - t0_ns) / 1e3, 1)
+        if a_seq == region_ack_seq:
+            region_setup["close_split_us"] = {
+                "last_send_to_sink_receipt": round((t_rx - t_sent_ns) / 1e3, 1),
+                "sink_receipt_to_ack_sent": round((t_ack - t_rx) / 1e3, 1),
+                "ack_sent_to_node": round((t_acked_ns - t_ack) / 1e3, 1)}
 
     t_max = max_over_ranks(elapsed)
     total_bytes = sum_over_ranks(float(args.steps * S))

@@ -1817,10 +1817,18 @@ int dora_node_sync(dora_node* n) {
       __builtin_ia32_pause();
     }
   c->aql_pending.clear();
+  // Spin on the query: the work is normally complete already (the caller saw its fill flags),
+  // and a blocking hipStreamSynchronize waits for an interrupt (~100-200 us) even then.
   std::vector<hipStream_t> ss = c->fill_streams;
   ss.push_back(c->stream);
-  for (hipStream_t s : ss)
-    if (hipStreamQuery(s) != hipSuccess) DORA_HIP(hipStreamSynchronize(s));
+  for (hipStream_t s : ss) {
+    const uint64_t q0 = dora::mono_ns();
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady && dora::mono_ns() - q0 < 20000000ull)
+      __builtin_ia32_pause();
+    if (e == hipErrorNotReady) DORA_HIP(hipStreamSynchronize(s));
+    else if (e != hipSuccess) DORA_HIP(e);
+  }
   return DORA_OK;
 }
 

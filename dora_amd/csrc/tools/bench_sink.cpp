@@ -10,6 +10,7 @@
 // At the end of the stream it writes one JSON document with per-(input, size) statistics.
 //   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE, DORA_BENCH_RESULT (path)
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -79,6 +80,9 @@ int main() {
     Series* s;
   };
   std::vector<Held> held;  // verify_late inputs, checksummed after the next ack
+  // (seq, receipt ns, ack sent ns) of inputs that asked for an ack: the bench splits its
+  // closing time into delivery and the ack's way back
+  std::vector<std::array<uint64_t, 3>> acks;
   auto verify = [&](const void* p, size_t len, uint64_t want, Series& s) {
     uint64_t c = 0;
     if (dora_gpu_csum64(p, len, csum_dev, st) == 0 &&
@@ -136,6 +140,10 @@ int main() {
           std::fprintf(stderr, "sink: ack failed: %s\n", dora_gpu_last_error());
           ++errors;
         }
+        if (acks.size() < 4096)
+          acks.push_back({uint64_t(ap["seq"].i), t, now_ns()});
+      } else if (params.count("mark") && acks.size() < 4096) {
+        acks.push_back({uint64_t(params.count("seq") ? params["seq"].i : -1), t, 0});
       }
       // consecutive inputs mostly share (input, size): skip the keyed lookup then
       const char* id = dora_event_id(ev);
@@ -224,7 +232,11 @@ int main() {
                  (unsigned long long)s.verified, (unsigned long long)s.mismatches);
     first = false;
   }
-  std::fprintf(f, "\n]}\n");
+  std::fprintf(f, "\n], \"acks\": [");
+  for (size_t k = 0; k < acks.size(); ++k)
+    std::fprintf(f, "%s[%llu, %llu, %llu]", k ? ", " : "", (unsigned long long)acks[k][0],
+                 (unsigned long long)acks[k][1], (unsigned long long)acks[k][2]);
+  std::fprintf(f, "]}\n");
   if (f != stdout) std::fclose(f);
   dora_gpu_free(csum_dev);
   dora_node_free(node);
