@@ -428,8 +428,19 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p->reserved2 = 0;
   p->completion_signal = done;
   // agent-scope fences: the pack reads device memory of this GPU and publishes its sample
-  // itself (write-through stores + fill flag); no barrier bit, so packs overlap
+  // itself (write-through stores + fill flag).  Below the barrier size no barrier bit, so packs
+  // of one queue overlap (ramps and signal tails hide behind each other); HBM-bound packs at or
+  // above it run one at a time per queue, like HIP stream order (more concurrent 40 MB copies
+  // only contend for HBM).
+  static const uint64_t barrier_bytes = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(0);
+  }();
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
+  const bool barrier = barrier_bytes && bytes >= barrier_bytes;
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                          (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
                           (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;

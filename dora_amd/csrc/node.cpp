@@ -285,6 +285,7 @@ struct NodeCore {
   std::vector<hipEvent_t> fill_events;
   std::vector<uint8_t> fill_dirty;
   hipEvent_t node_ev = nullptr;
+  hipEvent_t sync_ev = nullptr;  // dora_node_sync's marker
   size_t fill_next = 0;
   bool fill_streams_tried = false;
   // fills dispatched on the AQL queue and not yet seen complete (fence_fills waits for them)
@@ -483,6 +484,7 @@ struct NodeCore {
     }
     for (hipEvent_t e : fill_events) (void)hipEventDestroy(e);
     if (node_ev) (void)hipEventDestroy(node_ev);
+    if (sync_ev) (void)hipEventDestroy(sync_ev);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& kv : recv_pool) (void)hipFree(kv.second);
     if (fill_done) (void)hipFree(fill_done);
@@ -1817,16 +1819,26 @@ int dora_node_sync(dora_node* n) {
       __builtin_ia32_pause();
     }
   c->aql_pending.clear();
-  // Spin on the query: the work is normally complete already (the caller saw its fill flags),
-  // and a blocking hipStreamSynchronize waits for an interrupt (~100-200 us) even then.
+  // Mark each stream and spin on the marker: the work is normally complete already (the caller
+  // saw its fill flags), yet a bare hipStreamQuery reports a stream of signal-less kernel
+  // dispatches busy for ~200 us, and a blocking synchronise waits for an interrupt.
   std::vector<hipStream_t> ss = c->fill_streams;
   ss.push_back(c->stream);
+  if (!c->sync_ev && hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    c->sync_ev = nullptr;
+  }
   for (hipStream_t s : ss) {
+    if (!c->sync_ev || hipEventRecord(c->sync_ev, s) != hipSuccess) {
+      (void)hipGetLastError();
+      DORA_HIP(hipStreamSynchronize(s));
+      continue;
+    }
     const uint64_t q0 = dora::mono_ns();
     hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady && dora::mono_ns() - q0 < 20000000ull)
+    while ((e = hipEventQuery(c->sync_ev)) == hipErrorNotReady && dora::mono_ns() - q0 < 20000000ull)
       __builtin_ia32_pause();
-    if (e == hipErrorNotReady) DORA_HIP(hipStreamSynchronize(s));
+    if (e == hipErrorNotReady) DORA_HIP(hipEventSynchronize(c->sync_ev));
     else if (e != hipSuccess) DORA_HIP(e);
   }
   return DORA_OK;
