@@ -55,10 +55,6 @@ def parse():
                     help="N>1: skip the C4 fan-out / C5 chain runs after the timed region")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch kernel stamps (roofline then unmeasured)")
-    ap.add_argument("--stamp-window", type=int, default=64,
-                    help="after the timed region, send this many more messages with every "
-                         "pack stamped (per-launch kernel durations; stamping costs host time, "
-                         "so it stays out of the timed region)")
     return ap.parse_args()
 
 
@@ -609,19 +605,8 @@ def main():
     stats = node.stats()
     stats["send_phase_us"] = {k: round(v, 2) for k, v in node.send_profile().items()}
     stats["fill_paths"] = node.fill_paths()
-    # ---- stamped window (untimed): every pack's own start/stop ----
-    intervals = []
-    if not args.no_kernel_timing and args.stamp_window > 0:
-        node.set_timing_period(1)
-        node.set_profiling(True)
-        for k in range(args.stamp_window):
-            send(k, {"seq": seq, "t_start": time.time_ns()})
-            seq += 1
-        node.send_output("throughput", b"", {"seq": seq, "ack": True})
-        wait_ack(seq)
-        seq += 1
-        intervals = node.pack_intervals()
-    pack = node.pack_stats()
+    # the timed region's packs, each from its own stamps (first workgroup start -> fill signal)
+    intervals = node.pack_intervals() if region else []
     node.close()
     codes = df.wait(120)
     df.stop()
@@ -648,13 +633,13 @@ def main():
         launcher.close()
     barrier()
     value = total_bytes / t_max / 1e9
-    avg_pack_ms = pack["total_ms"] / max(pack["count"], 1)
-    per_launch = 2.0 * S / (avg_pack_ms * 1e-3) / 1e9 if pack["count"] else 0.0
+    own_ms = [b - a for a, b in intervals]
+    avg_pack_ms = sum(own_ms) / len(own_ms) if own_ms else 0.0
     busy_ms = busy_union_ms(intervals)
-    # Packs of consecutive sends overlap on the fill streams, so one launch's own duration is
-    # not the device time it costs: achieved = algorithmic bytes of the timed region's packs /
-    # their device span (first pack's start stamp -> the last pack's end on every fill stream,
-    # HIP events), i.e. device time per launch = span / packs.
+    # Packs of consecutive sends overlap (in flight on several queues), so one launch's own
+    # duration is not the device time it costs: achieved = algorithmic bytes of the timed
+    # region's packs / their device span (earliest pack start -> latest fill signal, from the
+    # packs' own s_memrealtime stamps), i.e. device time per launch = span / packs.
     span_ms = region["span_ms"] if region else 0.0
     packs = region["packs"] if region else 0
     achieved = 2.0 * S * packs / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
@@ -695,21 +680,20 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic[1] if traffic else None,
-                     "traffic_source": traffic[0] if traffic else None, "kernel": "pack_kernel",
+                     "traffic_source": traffic[0] if traffic else None,
+                     "kernel": ("dora_aql_pack1_u4 (AQL)" if stats["fill_paths"]["aql"]
+                                else "pack_kernel (HIP fill streams)"),
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
                      "region_packs": packs, "region_span_us": round(span_ms * 1e3, 1),
-                     "timing": "timed region: hipExtLaunchKernel start stamp of its first pack "
-                               "-> HIP events after its last pack on every fill stream; "
-                               "achieved = 2 S x packs / span",
-                     "stamped_window": {"packs": pack["count"],
-                                        "avg_kernel_us": round(avg_pack_ms * 1e3, 3),
-                                        "achieved_per_launch": round(per_launch, 1),
-                                        "busy_us_per_launch": round(
-                                            busy_ms * 1e3 / max(len(intervals), 1), 3),
-                                        "note": "every pack stamped (untimed, host-bound): "
-                                                "own kernel durations overlap across the fill "
-                                                "streams; busy = union of the intervals"},
-                     "fill_streams": int(os.environ.get("DORA_GPU_FILL_STREAMS", "3")),
+                     "timing": "every timed pack stamps its first workgroup's start and its "
+                               "fill signal (s_memrealtime, 100 MHz) into its fill flag's line; "
+                               "span = earliest start -> latest signal; achieved = 2 S x packs "
+                               "/ span",
+                     "per_pack": {"packs": len(intervals),
+                                  "own_us": round(avg_pack_ms * 1e3, 3),
+                                  "busy_us": round(busy_ms * 1e3 / max(len(intervals), 1), 3),
+                                  "note": "own = one pack's start -> signal (concurrent packs "
+                                          "overlap); busy = union of the intervals per pack"},
                      "algorithmic_bytes_per_launch": 2 * S},
         "parity": {"verified_msgs": verified, "mismatches": mismatches,
                    "timed_region_verified": verified - min(3, args.warmup)},

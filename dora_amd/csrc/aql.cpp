@@ -69,7 +69,7 @@ struct AqlQueue {
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
   uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
-  uint64_t next = 0;
+  uint64_t next = 0, next_big = 0;
   Use uses[kRingSlots];
   std::atomic<bool> failed{false};
   bool profiling = false;
@@ -393,7 +393,19 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     __builtin_ia32_sfence();
     *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
   }
-  const size_t qi = size_t(a->next % uint64_t(a->nq));
+  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
+  // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
+  // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
+  // the barrier; profiles/r02_aql_big_ab.jsonl).  Smaller packs overlap freely on all queues.
+  static const uint64_t barrier_bytes = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
+  }();
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
+  const bool big = barrier_bytes && bytes >= barrier_bytes;
+  const size_t qi = big ? size_t(a->next_big++ % uint64_t(std::min(a->nq, 3)))
+                        : size_t(a->next % uint64_t(a->nq));
   hsa_queue_t* const q = a->qs[qi];
   // Wait for a free packet slot before reserving one: a reserved packet must be written, or the
   // command processor stalls at its INVALID header for good.  This process is the queue's only
@@ -432,13 +444,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // of one queue overlap (ramps and signal tails hide behind each other); HBM-bound packs at or
   // above it run one at a time per queue, like HIP stream order (more concurrent 40 MB copies
   // only contend for HBM).
-  static const uint64_t barrier_bytes = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(0);
-  }();
-  uint64_t bytes = 0;
-  for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
-  const bool barrier = barrier_bytes && bytes >= barrier_bytes;
+  const bool barrier = big;
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                           (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
                           (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |

@@ -489,12 +489,13 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
     static uint8_t* scratch = nullptr;
     static uint64_t epoch = 0;
     if (!scratch) {
-      DORA_HIP(hipMalloc(&scratch, 8 + dora::kMaxSignalWgs * 4));
-      DORA_HIP(hipMemset(scratch, 0, 8 + dora::kMaxSignalWgs * 4));
+      // the flag owns a 64-byte line (epoch + the two launch stamps), the done words follow
+      DORA_HIP(hipMalloc(&scratch, 64 + dora::kMaxSignalWgs * 4));
+      DORA_HIP(hipMemset(scratch, 0, 64 + dora::kMaxSignalWgs * 4));
       DORA_HIP(hipDeviceSynchronize());
     }
     dora::FillSignal sig{reinterpret_cast<uint64_t*>(scratch), ++epoch,
-                         reinterpret_cast<uint32_t*>(scratch + 8)};
+                         reinterpret_cast<uint32_t*>(scratch + 64)};
     return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                              static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream),
                              nullptr, nullptr, &sig, nullptr);

@@ -96,6 +96,7 @@ struct Slot {
   hipIpcMemHandle_t handle;
   int flag = -1;              // FillFlag index in the node's region entry (async sends)
   uint64_t fill_epoch = 0;    // epoch the last fill into this slot stores into `flag`
+  uint64_t region_epoch = 0;  // that fill belongs to a timed region: harvest its stamps
   hipEvent_t done = nullptr;  // fallback: interprocess completion event of the last fill
   hipIpcEventHandle_t done_handle;
   // node-stream work on the slot with no fill flag (a broadcast group's pack + broadcast):
@@ -159,14 +160,16 @@ bool validity_in_sample() {
   return v;
 }
 
-// Packs below this many bytes (32 MiB) are dispatched on the process's own AQL queues (aql.h)
-// instead of hipLaunchKernel (DORA_GPU_AQL_MAX_BYTES; DORA_GPU_AQL=0 disables).  Larger packs
-// are GPU-bound and keep the fill streams (3 hardware queues; 40.96 MB: 13.2 us per pack there
-// vs 13.4 on two AQL queues, 16 MB: 6.0 vs 5.7, profiles/r01_stream_probe.jsonl, r01_aql_probe).
+// Packs of device sources are dispatched on the process's own AQL queues (aql.h) instead of
+// hipLaunchKernel: ~0.5 us of host time instead of 3-5, and no 12-20 us first launch after an
+// idle period (profiles/r02_aql_big_ab.jsonl).  Packs >= 32 MiB run in order per queue there
+// (aql.cpp), which keeps the 40.96 MB packs at the fill streams' device time.
+// DORA_GPU_AQL_MAX_BYTES caps the size (larger packs go to the HIP fill streams);
+// DORA_GPU_AQL=0 disables the path.
 uint64_t aql_max_bytes() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_MAX_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
+    return e ? std::strtoull(e, nullptr, 10) : ~uint64_t(0);
   }();
   return v;
 }
@@ -290,6 +293,21 @@ struct NodeCore {
   bool fill_streams_tried = false;
   // fills dispatched on the AQL queue and not yet seen complete (fence_fills waits for them)
   std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>> aql_pending;
+  // every kernel-signalled fill not yet seen complete (AQL and fill streams): dora_node_sync
+  // waits for their flags instead of synchronising streams
+  std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>> flag_pending;
+  std::vector<uint8_t> fill_unsignalled;  // per fill stream: work not covered by a fill flag
+
+  static void note(std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>>& v,
+                   const std::atomic<uint64_t>* f, uint64_t epoch) {
+    if (v.size() >= 64) {
+      size_t k = 0;
+      for (auto& x : v)
+        if (x.first->load(std::memory_order_acquire) < x.second) v[k++] = x;
+      v.resize(k);
+    }
+    v.push_back({f, epoch});
+  }
   RingWriter req;
   RingReader ev;
   RingReader drops;
@@ -421,6 +439,7 @@ struct NodeCore {
         fill_events.push_back(e);
       }
       fill_dirty.assign(fill_streams.size(), 0);
+      fill_unsignalled.assign(fill_streams.size(), 0);
     }
     (void)hipGetLastError();
   }
@@ -444,13 +463,8 @@ struct NodeCore {
   }
 
   void note_aql_fill(const std::atomic<uint64_t>* f, uint64_t epoch) {
-    if (aql_pending.size() >= 64) {
-      size_t k = 0;
-      for (auto& x : aql_pending)
-        if (x.first->load(std::memory_order_acquire) < x.second) aql_pending[k++] = x;
-      aql_pending.resize(k);
-    }
-    aql_pending.push_back({f, epoch});
+    note(aql_pending, f, epoch);
+    note(flag_pending, f, epoch);
   }
 
   // Order every fill launched so far before work queued on the node stream from now on.
@@ -535,6 +549,7 @@ struct dora_sample {
   uint64_t ext_len = 0;      // slot bytes filled: len + the validity tail (0: len)
   uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
   uint64_t epoch = 0;
+  bool stamped = false;  // the pack kernel stamps its start / signal time into the flag line
 };
 
 namespace dora {
@@ -585,6 +600,9 @@ struct dora_node {
   // end records a stop event on every fill stream once the packs queued there have finished.
   bool region_armed = false, region_started = false, region_marked = false;
   uint64_t region_aql = 0;  // packs of the region dispatched on the AQL queue
+  // kernel stamps (s_memrealtime ticks) of the region's packs, harvested from their flag lines
+  uint64_t region_stamped = 0, region_unstamped = 0, region_tmin = 0, region_tmax = 0;
+  std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
   bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
@@ -631,6 +649,26 @@ namespace {
 // Before a slot is refilled or freed, wait for its last fill (normally long complete: one load).
 // False when the fill did not complete within `timeout_ns` — the slot must then be neither
 // reused nor freed (a kernel may still write it).
+// The stamps of a timed region's pack, read from its flag line before the slot's next fill
+// overwrites them (the flag must already show the pack's epoch).
+void harvest_region_stamp(dora_node* n, Slot* s) {
+  if (!s->region_epoch || s->flag < 0) return;
+  const FillFlag& ff = n->core->region->hdr()->nodes[n->core->idx].fill[s->flag];
+  if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch) {
+    const uint64_t a = ff.t_start, b = ff.t_end;
+    if (b >= a && a) {
+      if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
+      if (!n->region_stamped || b > n->region_tmax) n->region_tmax = b;
+      ++n->region_stamped;
+      if (n->region_ticks.size() < 2 * (1u << 16)) {
+        n->region_ticks.push_back(a);
+        n->region_ticks.push_back(b);
+      }
+    }
+  }
+  s->region_epoch = 0;
+}
+
 bool wait_slot_idle(dora_node* n, Slot* s, uint64_t timeout_ns = 10000000000ull) {
   const uint64_t t0 = mono_ns();
   if (s->flag >= 0 && s->fill_epoch) {
@@ -639,6 +677,7 @@ bool wait_slot_idle(dora_node* n, Slot* s, uint64_t timeout_ns = 10000000000ull)
       if (mono_ns() - t0 > timeout_ns) return false;
       __builtin_ia32_pause();
     }
+    harvest_region_stamp(n, s);
   }
   if (s->done && hipEventQuery(s->done) == hipErrorNotReady &&
       hipEventSynchronize(s->done) != hipSuccess) {
@@ -1387,6 +1426,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
         s->epoch = sig.epoch;
         s->fill = FILL_FLAG;
         s->slot->fill_epoch = sig.epoch;
+        s->stamped = true;
         return DORA_OK;
       }
     }
@@ -1401,8 +1441,12 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     s->epoch = sig.epoch;
     s->fill = FILL_FLAG;
     s->slot->fill_epoch = sig.epoch;
+    s->stamped = true;
+    NodeCore::note(n->core->flag_pending, n->core->flag_host(s->slot->flag), sig.epoch);
     return DORA_OK;
   }
+  for (size_t i = 0; i < n->core->fill_streams.size(); ++i)
+    if (n->core->fill_streams[i] == st) n->core->fill_unsignalled[i] = 1;
   hipError_t e = order_fill(n, s, st);
   if (e != hipSuccess) return fail(DORA_ERR_HIP, "fill signal: %s", hipGetErrorString(e));
   return DORA_OK;
@@ -1572,8 +1616,11 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
                        (n->timing_seq++ % period) == 0;
     TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
     hipEvent_t t_start = tp ? tp->start : nullptr, t_stop = tp ? tp->stop : nullptr;
+    // Timed region: packs that signal their own fill stamp their device time into the flag
+    // line; only packs that cannot (kernel signal off, transforms) need timing events
+    const bool stampable = kernel_signal() && n->core->fill_done && !plan->compact;
     if (n->region_armed && plan->dev != ARROW_DEVICE_CPU) {
-      if (!n->region_started && !tp) {  // first pack of the region: its start is the origin
+      if (!stampable && !n->region_started && !tp) {  // its start is the fallback's origin
         t_start = n->region_start;
         n->region_started = true;
       }
@@ -1589,6 +1636,10 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       add_to_cache(n, s->slot);
       delete s;
       return rc;
+    }
+    if (n->region_armed && plan->dev != ARROW_DEVICE_CPU) {
+      if (s->stamped) s->slot->region_epoch = s->epoch;
+      else ++n->region_unstamped;
     }
     t2 = t3 = mono_ns();
   }
@@ -1673,11 +1724,16 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
       }
     }
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
-    // A node with outputs creates its fill streams now, right after the node stream and before
-    // anything touches the null stream: HIP maps a process's streams onto its 4 hardware queues
-    // in creation order, and fill streams created later share one (40.96 MB: 13.2 -> 15.0-15.2
-    // us device time per pack).  A node that only receives keeps its single stream.
-    if (e.outputs[0] != 0) core->ensure_fill_streams();
+    // Fill streams are created on first use: device-source packs go to the AQL queues, so only
+    // host sources, compacting transforms and node-stream-ordered fills need them, and a node
+    // that never sends such a pack holds one HIP hardware queue, not four.  With
+    // DORA_GPU_AQL=0 or a size cap (DORA_GPU_AQL_MAX_BYTES) a node with outputs creates them
+    // up front: HIP maps streams onto its 4 hardware queues in creation order, and fill streams
+    // created late share one (40.96 MB: 13.2 -> 15.0-15.2 us device time per pack, r01).
+    const char* aql_env = std::getenv("DORA_GPU_AQL");
+    const bool aql_off = aql_env && *aql_env == '0';
+    if (e.outputs[0] != 0 && (aql_off || dora::aql_max_bytes() != ~uint64_t(0)))
+      core->ensure_fill_streams();
     if (dora::async_sends()) {
       // host-register the control region so this node's stream can write fill epochs into it
       void* dev = nullptr;
@@ -1809,38 +1865,27 @@ int dora_node_sync(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return DORA_OK;
   dora::NodeCore* c = n->core.get();
-  // AQL fills: their flags; HIP fills and the node stream: query first (an idle stream costs
-  // no blocking wait), then synchronise what is still running
+  // Kernel-signalled fills (AQL and fill streams): their flags.  A stream query or synchronise
+  // would wait for HIP to notice the kernels' completion, ~100-200 us after the flags are up.
   const uint64_t t0 = dora::mono_ns();
-  for (auto& x : c->aql_pending)
-    while (x.first->load(std::memory_order_acquire) < x.second) {
-      if (dora::mono_ns() - t0 > 10000000000ull)
-        return dora::fail(DORA_ERR_TIMEOUT, "a fill did not complete within 10 s");
-      __builtin_ia32_pause();
-    }
-  c->aql_pending.clear();
-  // Mark each stream and spin on the marker: the work is normally complete already (the caller
-  // saw its fill flags), yet a bare hipStreamQuery reports a stream of signal-less kernel
-  // dispatches busy for ~200 us, and a blocking synchronise waits for an interrupt.
-  std::vector<hipStream_t> ss = c->fill_streams;
-  ss.push_back(c->stream);
-  if (!c->sync_ev && hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) != hipSuccess) {
-    (void)hipGetLastError();
-    c->sync_ev = nullptr;
+  for (auto* v : {&c->aql_pending, &c->flag_pending}) {
+    for (auto& x : *v)
+      while (x.first->load(std::memory_order_acquire) < x.second) {
+        if (dora::mono_ns() - t0 > 10000000000ull)
+          return dora::fail(DORA_ERR_TIMEOUT, "a fill did not complete within 10 s");
+        __builtin_ia32_pause();
+      }
+    v->clear();
   }
-  for (hipStream_t s : ss) {
-    if (!c->sync_ev || hipEventRecord(c->sync_ev, s) != hipSuccess) {
-      (void)hipGetLastError();
-      DORA_HIP(hipStreamSynchronize(s));
-      continue;
-    }
-    const uint64_t q0 = dora::mono_ns();
-    hipError_t e;
-    while ((e = hipEventQuery(c->sync_ev)) == hipErrorNotReady && dora::mono_ns() - q0 < 20000000ull)
-      __builtin_ia32_pause();
-    if (e == hipErrorNotReady) DORA_HIP(hipEventSynchronize(c->sync_ev));
-    else if (e != hipSuccess) DORA_HIP(e);
+  // work no flag covers: fills signalled by the stream (kernel signal off, transforms, host
+  // sources) and whatever the caller queued on the node stream
+  for (size_t i = 0; i < c->fill_streams.size(); ++i) {
+    if (!c->fill_unsignalled[i]) continue;
+    DORA_HIP(hipStreamSynchronize(c->fill_streams[i]));
+    c->fill_unsignalled[i] = 0;
   }
+  if (hipStreamQuery(c->stream) == hipErrorNotReady) DORA_HIP(hipStreamSynchronize(c->stream));
+  (void)hipGetLastError();
   return DORA_OK;
 }
 
@@ -2151,13 +2196,8 @@ int dora_node_region_begin(dora_node* n) {
   n->region_armed = true;
   n->region_started = false;
   n->region_packs = n->region_bytes = n->region_aql = 0;
-  if (dora::AqlQueue* q = dora::aql_queue(n->core->device)) {
-    // AQL packs of the region carry completion signals with dispatch timestamps
-    uint64_t a = 0, b = 0, c = 0;
-    (void)dora::aql_profile_take(q, &a, &b, &c);
-    int rc = dora::aql_profile_enable(q, true);
-    if (rc != DORA_OK) return rc;
-  }
+  n->region_stamped = n->region_unstamped = n->region_tmin = n->region_tmax = 0;
+  n->region_ticks.clear();
   return DORA_OK;
 }
 
@@ -2183,7 +2223,7 @@ int region_record_stops(dora_node* n) {
 int dora_node_region_mark(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (!n->region_armed) return dora::fail(DORA_ERR_INVALID, "no region begun");
-  if (!n->region_started || n->region_aql) return DORA_OK;  // AQL packs carry their own stamps
+  if (!n->region_started || !n->region_unstamped) return DORA_OK;  // stamped packs need none
   return dora::region_record_stops(n);
 }
 
@@ -2196,23 +2236,24 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
   *span_ms = 0;
   if (packs) *packs = n->region_packs;
   if (bytes) *bytes = n->region_bytes;
-  if (dora::AqlQueue* q = dora::aql_queue(n->core->device)) {
-    uint64_t first = 0, last = 0, count = 0;
-    int rc = dora::aql_profile_take(q, &first, &last, &count);
-    (void)dora::aql_profile_enable(q, false);
-    if (rc != DORA_OK) return rc;
-    if (count && n->region_aql) {
-      // packs on the AQL queue: first dispatch start -> last end of their own timestamps (the
-      // region's HIP-launched packs, if any, are not in this span)
-      *span_ms = double(last - first) / 1e6;
-      if (packs) *packs = count;
-      if (bytes && n->region_packs) *bytes = n->region_bytes / n->region_packs * count;
-      return DORA_OK;
-    }
+  if (!n->region_unstamped) {
+    // every pack stamped its own device time: first workgroup start of the earliest to the
+    // signal of the last (s_memrealtime); harvest the stamps not yet read at slot reuse
+    std::vector<dora::Slot*> live(n->cache.begin(), n->cache.end());
+    for (auto& kv : n->sent_out) live.push_back(kv.second);
+    for (dora::Slot* s : live)
+      if (s->region_epoch && !dora::wait_slot_idle(n, s))
+        return dora::fail(DORA_ERR_TIMEOUT, "a timed pack did not complete within 10 s");
+    if (n->region_stamped)
+      *span_ms = double(n->region_tmax - n->region_tmin) / dora::kRealtimeHz * 1e3;
+    if (packs) *packs = n->region_stamped;
+    if (bytes && n->region_packs) *bytes = n->region_bytes / n->region_packs * n->region_stamped;
+    return DORA_OK;
   }
   if (!n->region_started) return DORA_OK;
-  // stop = the end of the last pack on each fill stream (and the node stream), recorded by
-  // dora_node_region_mark right after the last send, or now
+  // fallback (packs without kernel stamps): the first pack's start event to events recorded
+  // after the last pack on each fill stream and the node stream, by dora_node_region_mark right
+  // after the last send, or now
   if (!marked) {
     int rc = dora::region_record_stops(n);
     if (rc != DORA_OK) return rc;
@@ -2230,6 +2271,14 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
 
 int dora_node_pack_intervals(dora_node* n, double* out_ms, size_t cap, size_t* count) {
   if (!n || !count || (!out_ms && cap)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (!n->region_ticks.empty()) {
+    // the last timed region's packs, from their own stamps, ms after the earliest start
+    const size_t pairs = n->region_ticks.size() / 2;
+    *count = pairs;
+    for (size_t i = 0; i < 2 * std::min(cap, pairs); ++i)
+      out_ms[i] = double(n->region_ticks[i] - n->region_tmin) / dora::kRealtimeHz * 1e3;
+    return DORA_OK;
+  }
   dora::harvest_all(n);
   const size_t pairs = n->intervals.size() / 2;
   *count = pairs;

@@ -210,14 +210,26 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
 // boundary per message on ROCm 7.
 // `blk`/`nblk`: this workgroup and the launch's workgroup count, passed in so that the AQL
 // kernels need no hidden kernel arguments.
+// Workgroup 0 also stamps the launch (s_memrealtime, 100 MHz) into the flag's line: its own
+// start, taken on entry, and the time it signals — the fill's device time without a profiled
+// queue or timing events.
+__device__ __forceinline__ void stamp_fill(uint64_t* flag, uint64_t t_start) {
+  __hip_atomic_store(flag + 1, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(flag + 2, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class A>
-__device__ __forceinline__ void signal_fill(const A& a, uint32_t blk, uint32_t nblk) {
+__device__ __forceinline__ void signal_fill(const A& a, uint32_t blk, uint32_t nblk,
+                                            uint64_t t_start) {
   const uint32_t e = static_cast<uint32_t>(a.epoch);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sample stores are complete
   __syncthreads();
   if (nblk == 1) {  // nothing to wait for but this workgroup's own stores
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+      stamp_fill(a.flag, t_start);
       __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     return;
   }
   if (threadIdx.x == 0) __hip_atomic_store(a.done + blk, e, __ATOMIC_RELAXED,
@@ -257,17 +269,23 @@ __device__ __forceinline__ void signal_fill(const A& a, uint32_t blk, uint32_t n
   // Relaxed: everything this store publishes is already written through (sample stores and done
   // words are device-scope write-through and complete), and it issues only after every done
   // word was observed; a release would write back this XCD's whole L2 for nothing.
-  if (threadIdx.x == 0 && ok)
+  if (threadIdx.x == 0 && ok) {
+    stamp_fill(a.flag, t_start);
     __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // A pack launch: its workgroups stride over the chunks; a signalling launch (NT >= 2) then
 // signals the fill flag.
 template <int U, int NT, class A>
 __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t nblk) {
+  uint64_t t_start = 0;
+  if constexpr (NT >= 2) {
+    if (blk == 0) t_start = __builtin_amdgcn_s_memrealtime();
+  }
   for (uint32_t c = blk; c < args.n_chunks; c += nblk) pack_chunk<U, NT>(args, c);
   if constexpr (NT >= 2) {
-    if (args.flag) signal_fill(args, blk, nblk);  // all-zero arguments are a no-op
+    if (args.flag) signal_fill(args, blk, nblk, t_start);  // all-zero arguments are a no-op
   }
 }
 

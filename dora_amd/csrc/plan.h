@@ -76,7 +76,8 @@ struct Segment {
 
 // Fill signal written by a pack launch itself (kernels.hip): once every workgroup's stores are
 // complete, a system-scope store of `epoch` into `flag` (device view of a host-registered fill
-// flag).  `done` = kMaxSignalWgs device words owned by this flag (zeroed once).
+// flag), preceded by the launch's start / signal times into flag[1], flag[2] (the flag must own
+// 24 bytes).  `done` = kMaxSignalWgs device words owned by this flag (zeroed once).
 struct FillSignal {
   uint64_t* flag;
   uint64_t epoch;

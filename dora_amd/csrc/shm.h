@@ -38,12 +38,16 @@ struct RingHdr {
 constexpr size_t kListLen = 2048;
 constexpr uint32_t kFillFlags = 64;  // per node: one per live device slot
 
-// A fill-completion word: the owner's stream writes the send epoch here (hipStreamWriteValue64
-// into the host-registered region) once the pack that filled the slot has completed; receivers
-// poll it with plain loads.  One cache line each.
+// A fill-completion word: the pack kernel that filled the slot stores the send epoch here (into
+// the host-registered region) once every workgroup's stores are complete; receivers poll it with
+// plain loads.  The same line carries the pack's first workgroup's start and its signal time
+// (s_memrealtime, 100 MHz ticks): device timing of the fill without profiling the queue.  One
+// cache line each.
 struct FillFlag {
   alignas(64) std::atomic<uint64_t> epoch;
+  uint64_t t_start, t_end;
 };
+constexpr double kRealtimeHz = 100e6;  // s_memrealtime
 
 struct NodeEntry {
   FillFlag fill[kFillFlags];

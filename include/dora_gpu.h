@@ -346,13 +346,17 @@ int dora_node_bcast_stats(dora_node* node, uint64_t* groups_out, uint64_t* group
 int dora_node_set_profiling(dora_node* node, int enable);
 int dora_node_set_timing_period(dora_node* node, uint64_t period);
 int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);
-/* (start, stop) of each stamped pack in ms after profiling was enabled, `cap` pairs at most
- * (kernels on different fill streams overlap: their union is the pack busy time). */
+/* (start, stop) of each pack of the last timed region in ms after its earliest start, from the
+ * packs' own stamps (below); without a region, of each event-stamped pack in ms after
+ * profiling was enabled.  `cap` pairs at most (concurrent packs overlap: their union is the
+ * pack busy time). */
 int dora_node_pack_intervals(dora_node* node, double* out_ms, size_t cap, size_t* count);
-/* Device span of a run of sends: from the start of the first pack launched after
- * region_begin (hipExtLaunchKernel start stamp) to the end of the last pack on every fill
- * stream (HIP events recorded by region_end, which waits for them); packs and sample bytes
- * launched in between. */
+/* Device span of a run of sends: every pack that signals its own fill also stamps its first
+ * workgroup's start and its signal time (s_memrealtime, 100 MHz) into its fill flag's line;
+ * the span is the earliest start to the latest signal over the packs sent between region_begin
+ * and region_end (which waits for them).  Packs that cannot stamp (kernel signal off,
+ * compacting transforms) fall back to HIP events: the first pack's start stamp to events
+ * recorded after the last pack on every stream.  Packs and sample bytes timed. */
 int dora_node_region_begin(dora_node* node);
 /* Wait until every fill this node launched (AQL packets, fill streams) and the work on its node
  * stream have completed (new; the node-scoped counterpart of a device synchronise). */

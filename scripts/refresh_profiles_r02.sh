@@ -13,6 +13,6 @@ bash scripts/run_steps.sh \
  "r02_bench1000:300:python bench.py --steps 1000 --no-cpu-baseline > $o/bench1000.json" \
  "r02_c3:300:python bench.py --workload c3 --no-cpu-baseline > $o/c3.json" \
  "r02_prof:300:rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof -o run -- python bench.py --no-ladder --no-cpu-baseline --steps 200 --warmup 20 > $o/prof_run.json" \
- "r02_fetch:120:timeout -s KILL 110 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/pmc_fetch -o run -- python bench.py --no-cpu-baseline --no-ladder --steps 40 --warmup 5 --stamp-window 0 > $o/pmc_fetch.json" \
- "r02_write:120:timeout -s KILL 110 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/pmc_write -o run -- python bench.py --no-cpu-baseline --no-ladder --steps 40 --warmup 5 --stamp-window 0 > $o/pmc_write.json" \
+ "r02_fetch:120:timeout -s KILL 110 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/pmc_fetch -o run -- python bench.py --no-cpu-baseline --no-ladder --steps 40 --warmup 5 > $o/pmc_fetch.json" \
+ "r02_write:120:timeout -s KILL 110 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/pmc_write -o run -- python bench.py --no-cpu-baseline --no-ladder --steps 40 --warmup 5 > $o/pmc_write.json" \
  "r02_c3prof:300:rocprofv3 --kernel-trace --stats --output-format csv -d $o/c3prof -o run -- python bench.py --workload c3 --no-ladder --no-cpu-baseline --steps 1000 > $o/c3prof_run.json"

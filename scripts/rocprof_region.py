@@ -2,8 +2,8 @@
 """Pack-kernel timing of bench.py's timed region from a rocprofv3 kernel trace — the
 independent check of bench.py's `roofline` (device span of the region / packs).
 
-bench.py --no-ladder packs, in order: `--warmup` messages, the `--steps` timed messages, then
-`--stamp-window` stamped ones.  The timed packs overlap on the node's fill streams, so besides
+bench.py --no-ladder packs, in order: a 4 KB cold-start message, `--warmup` messages, 24 refill
+messages, then the `--steps` timed ones (pass --warmup W+24).  The timed packs overlap, so besides
 each kernel's own mean duration this reports the region's device span (first start -> last end)
 per pack and the union of the kernels' intervals per pack.
 
@@ -38,10 +38,15 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--min-grid", type=int, default=1024 * 256,
+                    help="work-items of a headline pack launch (1024 workgroups x 256)")
     ap.add_argument("--size", type=int, default=40960000)
     a = ap.parse_args()
     f = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if "pack_kernel" in r["Kernel_Name"]]
+    # the headline packs: pack kernels (HIP `pack_kernel` or AQL `dora_aql_pack*`) of the
+    # headline's grid (the cold-start / small packs of the same kernels have smaller grids)
+    rows = [r for r in csv.DictReader(open(f))
+            if "pack" in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= a.min_grid]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
     region = iv[a.warmup:a.warmup + a.steps]
