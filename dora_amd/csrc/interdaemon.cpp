@@ -262,16 +262,22 @@ bool Forwarder::send_to(const std::string& machine, const std::vector<uint8_t>& 
     std::fprintf(stderr, "dora-gpu daemon: no address for machine `%s`\n", machine.c_str());
     return false;
   }
+  const uint64_t now = mono_ns();
+  auto d = down_until_.find(machine);
+  if (d != down_until_.end() && now < d->second) return false;  // unreachable a moment ago
   for (int attempt = 0; attempt < 2; ++attempt) {
     auto s = socks_.find(machine);
     int fd = s != socks_.end() ? s->second : -1;
     if (fd < 0) {
-      fd = connect_peer(p->second, 30000);
+      // the first connection waits for a peer that starts later; a reconnection does not
+      fd = connect_peer(p->second, down_until_.count(machine) ? 1000 : 30000);
       if (fd < 0) {
         std::fprintf(stderr, "dora-gpu daemon: cannot connect to machine `%s` (%s:%d)\n",
                      machine.c_str(), p->second.host.c_str(), p->second.port);
+        down_until_[machine] = mono_ns() + 5000000000ull;  // its messages are dropped for 5 s
         return false;
       }
+      down_until_[machine] = 0;
       socks_[machine] = fd;
     }
     const uint64_t len = frame.size();
@@ -383,6 +389,15 @@ Gateway::~Gateway() {
   if (listen_fd_ >= 0) ::close(listen_fd_);
 }
 
+bool Gateway::peers_gone() const {
+  static const uint64_t grace_ns = [] {
+    const char* e = std::getenv("DORA_GPU_PEER_GRACE_MS");
+    return uint64_t(e ? std::strtoull(e, nullptr, 10) : 10000) * 1000000ull;
+  }();
+  return ever_connected_.load() && conns_.load() == 0 &&
+         mono_ns() - last_disconnect_ns_.load() > grace_ns;
+}
+
 void Gateway::accept_loop() {
   while (!stop_) {
     pollfd pf{listen_fd_, POLLIN, 0};
@@ -392,6 +407,8 @@ void Gateway::accept_loop() {
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     std::lock_guard<std::mutex> g(readers_mu_);
+    conns_.fetch_add(1);
+    ever_connected_.store(true);
     reader_fds_.push_back(fd);
     readers_.emplace_back([this, fd] { read_loop(fd); });
   }
@@ -428,6 +445,8 @@ void Gateway::read_loop(int fd) {
     p->cv.notify_one();
   }
   ::close(fd);
+  last_disconnect_ns_.store(mono_ns());
+  conns_.fetch_sub(1);
 }
 
 void Gateway::proxy_loop(Proxy* p) {
@@ -445,11 +464,21 @@ void Gateway::proxy_loop(Proxy* p) {
       p->cv.wait_for(g, std::chrono::milliseconds(100), [&] { return stop_ || !p->q.empty(); });
       if (p->q.empty()) {
         if (stop_) break;
-        continue;
+        if (peers_gone()) {
+          // the remote node's daemon went away without closing its outputs: close them here
+          std::fprintf(stderr, "dora-gpu daemon: peers of proxy `%s` gone; closing its outputs\n",
+                       p->spec.node_id.c_str());
+          e.kind = IDE_OUTPUTS_CLOSED;
+          e.outputs = open;
+        } else {
+          continue;
+        }
+      } else {
+        e = std::move(p->q.front());
+        p->q.pop_front();
       }
-      e = std::move(p->q.front());
-      p->q.pop_front();
     }
+
     if (e.kind == IDE_OUTPUTS_CLOSED) {
       std::vector<const char*> ids;
       for (const auto& o : e.outputs) {

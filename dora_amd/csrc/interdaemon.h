@@ -94,6 +94,7 @@ class Forwarder {
   std::string dataflow_id_;
   std::map<std::string, PeerAddr> peers_;
   std::map<std::string, int> socks_;
+  std::map<std::string, uint64_t> down_until_;  // a peer that refused us: skip it until then
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<ForwardJob> q_;
@@ -138,6 +139,13 @@ class Gateway {
   std::string shm_, dataflow_id_;
   int listen_fd_ = -1, port_ = 0;
   std::atomic<bool> stop_{false};
+  // peer connections: once every peer that connected has gone for longer than the grace period
+  // (DORA_GPU_PEER_GRACE_MS, default 10 s) the proxies close their outputs — a crashed remote
+  // daemon never sends OutputsClosed, and the local dataflow must still finish
+  std::atomic<int> conns_{0};
+  std::atomic<bool> ever_connected_{false};
+  std::atomic<uint64_t> last_disconnect_ns_{0};
+  bool peers_gone() const;
   std::map<std::string, std::unique_ptr<Proxy>> proxies_;
   std::thread accept_th_;
   std::mutex readers_mu_;

@@ -139,3 +139,52 @@ def test_wrong_dataflow_id_is_ignored(tmp_path):
         a.stop()
         b.stop()
     assert "ignored" in b.log("_daemon")
+
+
+def test_crashed_peer_daemon_closes_remote_inputs(tmp_path, monkeypatch):
+    """A remote daemon that dies without sending OutputsClosed (killed) must not strand the
+    local receivers: once every peer connection has been gone for the grace period
+    (DORA_GPU_PEER_GRACE_MS) the proxy closes its outputs and the local dataflow finishes.
+    The reference only ends the connection's read loop on EOF/reset
+    (binaries/daemon/src/inter_daemon.rs:136-139) and leaves the receivers waiting; here the
+    receivers see INPUT_CLOSED (a deliberate deviation)."""
+    monkeypatch.setenv("DORA_GPU_PEER_GRACE_MS", "300")
+    desc = _desc(1)
+    b = Dataflow(desc, machine="B", machines={"B": ("127.0.0.1", 0), "A": ("127.0.0.1", 1)},
+                 dataflow_id="df-crash", log_dir=str(tmp_path / "B")).start()
+    a = Dataflow(desc, machine="A",
+                 machines={"A": ("127.0.0.1", 0), "B": ("127.0.0.1", b.listen_port)},
+                 dataflow_id="df-crash", log_dir=str(tmp_path / "A")).start()
+    try:
+        box = {}
+        lt = threading.Thread(target=lambda: box.update(local=_open(a, "local")))
+        lt.start()
+        rt = threading.Thread(target=lambda: box.update(dst=_open(b, "dst0")))
+        rt.start()
+        src = _open(a, "src")
+        lt.join(30)
+        rt.join(30)
+        for i in range(5):
+            src.send_output("data", bytes([i]) * 100, {"seq": i})
+        dst = box["dst"]
+        seqs = []
+        while len(seqs) < 5:
+            ev = dst.next(timeout=30)
+            assert ev is not None and ev["type"] == "INPUT", ev
+            seqs.append(ev["metadata"]["seq"])
+        assert seqs == list(range(5))
+        a.daemon.kill()  # no OutputsClosed ever leaves machine A
+        t0 = time.time()
+        closed = set()
+        while closed != {"data", "side"}:
+            ev = dst.next(timeout=30)
+            assert ev is not None, "remote inputs never closed after the peer daemon died"
+            if ev["type"] == "INPUT_CLOSED":
+                closed.add(ev["id"])
+        assert time.time() - t0 < 20
+        dst.close()
+        assert b.wait(30)["_daemon"] == 0, b.log("_daemon")
+    finally:
+        a.stop()
+        b.stop()
+    assert "gone; closing its outputs" in b.log("_daemon")
