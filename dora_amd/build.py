@@ -134,6 +134,36 @@ def build_tools(verbose: bool = False):
     return out
 
 
+PYEXT_SOURCE = "pyext.cpp"
+
+
+def build_pyext(verbose: bool = False) -> str:
+    """dora_amd/_dora_node<EXT_SUFFIX>: the Python node's per-send path as a CPython extension
+    (the reference's Python node is a native PyO3 module), linked against libdora_gpu.so in
+    dora_amd/lib (rpath $ORIGIN/lib) so it shares the library ctypes loads."""
+    import sysconfig
+    lib = build(verbose)
+    inc = sysconfig.get_paths()["include"]
+    os.makedirs(OBJ, exist_ok=True)
+    src = os.path.join(CSRC, PYEXT_SOURCE)
+    obj = os.path.join(OBJ, "pyext.cpp.o")
+    if _newer(obj, [src, *_headers()]):
+        cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", *CXXFLAGS,
+               f"-I{inc}", "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    out = os.path.join(ROOT, "dora_amd", "_dora_node" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if _newer(out, [obj, lib]):
+        cmd = [HIPCC, "-shared", "-fPIC", "-o", out, obj, f"-L{LIB}", "-ldora_gpu",
+               "-Wl,-rpath,$ORIGIN/lib"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return out
+
+
 if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
+    print(build_pyext(verbose="-v" in sys.argv))
     print(build_tools(verbose="-v" in sys.argv))

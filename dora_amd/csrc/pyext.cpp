@@ -1,0 +1,197 @@
+// dora_amd._dora_node: the per-send hot path of the Python node API as a CPython extension.
+//
+// The reference's Python node is a native extension too (PyO3: apis/python/node/src/lib.rs:
+// 157-185 `send_output`, whose metadata goes through pydict_to_metadata,
+// apis/python/operator/src/lib.rs:165-186).  Through ctypes a send paid ~1 us encoding the
+// parameters in Python and ~0.9 us of ctypes argument conversion; here both are one METH_FASTCALL
+// call.  The GIL is released around the library call: a send may wait for drop tokens that
+// another Python thread of the same process returns.
+//
+// Every function returns the library's status code; dora_amd/node.py raises on non-zero (the
+// message comes from dora_gpu_last_error), so error behaviour is the ctypes path's.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "dora_gpu.h"
+
+namespace {
+
+void put_u32(std::string& o, uint32_t v) { o.append(reinterpret_cast<const char*>(&v), 4); }
+void put_u64(std::string& o, uint64_t v) { o.append(reinterpret_cast<const char*>(&v), 8); }
+
+// MetadataParameters encoding (include/dora_gpu.h, dora_node_send_output_sample): u32 count,
+// then per entry in sorted key order: u64 key length, key, u8 tag (0 bool, 1 int, 2 string),
+// value (u8 | i64 | u64 length + utf-8).  Anything else is stringified (str(v)), as
+// pydict_to_metadata does.  Same bytes as dora_amd.node.encode_parameters_py.
+bool encode(PyObject* meta, std::string& out) {
+  out.clear();
+  if (meta == nullptr || meta == Py_None) return true;
+  if (!PyDict_Check(meta)) {
+    PyErr_SetString(PyExc_TypeError, "metadata must be a dict or None");
+    return false;
+  }
+  if (PyDict_GET_SIZE(meta) == 0) return true;
+  PyObject* keys = PyDict_Keys(meta);
+  if (!keys) return false;
+  if (PyList_Sort(keys) < 0) {
+    Py_DECREF(keys);
+    return false;
+  }
+  const Py_ssize_t n = PyList_GET_SIZE(keys);
+  put_u32(out, uint32_t(n));
+  bool ok = true;
+  for (Py_ssize_t i = 0; ok && i < n; ++i) {
+    PyObject* k = PyList_GET_ITEM(keys, i);
+    PyObject* ks = PyUnicode_Check(k) ? (Py_INCREF(k), k) : PyObject_Str(k);
+    if (!ks) {
+      ok = false;
+      break;
+    }
+    Py_ssize_t kl = 0;
+    const char* kb = PyUnicode_AsUTF8AndSize(ks, &kl);
+    if (!kb) {
+      Py_DECREF(ks);
+      ok = false;
+      break;
+    }
+    put_u64(out, uint64_t(kl));
+    out.append(kb, size_t(kl));
+    Py_DECREF(ks);
+    PyObject* v = PyDict_GetItemWithError(meta, k);  // borrowed
+    if (!v) {
+      ok = false;
+      break;
+    }
+    if (PyBool_Check(v)) {
+      out.push_back(char(0));
+      out.push_back(char(v == Py_True ? 1 : 0));
+    } else if (PyLong_Check(v)) {
+      const long long x = PyLong_AsLongLong(v);
+      if (x == -1 && PyErr_Occurred()) {
+        ok = false;  // OverflowError, as struct.pack("<q") raises
+        break;
+      }
+      out.push_back(char(1));
+      put_u64(out, uint64_t(x));
+    } else {
+      PyObject* s = PyUnicode_Check(v) ? (Py_INCREF(v), v) : PyObject_Str(v);
+      if (!s) {
+        ok = false;
+        break;
+      }
+      Py_ssize_t sl = 0;
+      const char* sb = PyUnicode_AsUTF8AndSize(s, &sl);
+      if (!sb) {
+        Py_DECREF(s);
+        ok = false;
+        break;
+      }
+      out.push_back(char(2));
+      put_u64(out, uint64_t(sl));
+      out.append(sb, size_t(sl));
+      Py_DECREF(s);
+    }
+  }
+  Py_DECREF(keys);
+  return ok;
+}
+
+thread_local std::string t_params;
+
+bool as_ptr(PyObject* o, void** p) {
+  if (o == Py_None) {
+    *p = nullptr;
+    return true;
+  }
+  *p = PyLong_AsVoidPtr(o);
+  return !(*p == nullptr && PyErr_Occurred());
+}
+
+const char* as_cstr(PyObject* o) {
+  if (PyBytes_Check(o)) return PyBytes_AS_STRING(o);
+  if (PyUnicode_Check(o)) return PyUnicode_AsUTF8(o);
+  PyErr_SetString(PyExc_TypeError, "output id must be str or bytes");
+  return nullptr;
+}
+
+PyObject* py_encode_parameters(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 1) {
+    PyErr_SetString(PyExc_TypeError, "encode_parameters(metadata)");
+    return nullptr;
+  }
+  if (!encode(args[0], t_params)) return nullptr;
+  return PyBytes_FromStringAndSize(t_params.data(), Py_ssize_t(t_params.size()));
+}
+
+// send_bytes(handle, output_id, data_ptr, len, device_type, metadata) -> status
+PyObject* py_send_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 6) {
+    PyErr_SetString(PyExc_TypeError,
+                    "send_bytes(handle, output_id, data_ptr, len, device_type, metadata)");
+    return nullptr;
+  }
+  void *h = nullptr, *data = nullptr;
+  if (!as_ptr(args[0], &h) || !as_ptr(args[2], &data)) return nullptr;
+  const char* oid = as_cstr(args[1]);
+  if (!oid) return nullptr;
+  const size_t len = PyLong_AsSize_t(args[3]);
+  if (len == size_t(-1) && PyErr_Occurred()) return nullptr;
+  const long dev = PyLong_AsLong(args[4]);
+  if (dev == -1 && PyErr_Occurred()) return nullptr;
+  std::string& params = t_params;
+  if (!encode(args[5], params)) return nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = dora_node_send_output_bytes(static_cast<dora_node*>(h), oid, data, len,
+                                   static_cast<ArrowDeviceType>(dev),
+                                   reinterpret_cast<const uint8_t*>(params.data()), params.size());
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
+// send_array(handle, output_id, array_addr, schema_addr, device_type, metadata) -> status
+PyObject* py_send_array(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 6) {
+    PyErr_SetString(PyExc_TypeError,
+                    "send_array(handle, output_id, array_addr, schema_addr, device_type, metadata)");
+    return nullptr;
+  }
+  void *h = nullptr, *arr = nullptr, *sch = nullptr;
+  if (!as_ptr(args[0], &h) || !as_ptr(args[2], &arr) || !as_ptr(args[3], &sch)) return nullptr;
+  const char* oid = as_cstr(args[1]);
+  if (!oid) return nullptr;
+  const long dev = PyLong_AsLong(args[4]);
+  if (dev == -1 && PyErr_Occurred()) return nullptr;
+  std::string& params = t_params;
+  if (!encode(args[5], params)) return nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = dora_node_send_output(static_cast<dora_node*>(h), oid,
+                             static_cast<const struct ArrowArray*>(arr),
+                             static_cast<const struct ArrowSchema*>(sch),
+                             static_cast<ArrowDeviceType>(dev),
+                             reinterpret_cast<const uint8_t*>(params.data()), params.size());
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
+PyMethodDef methods[] = {
+    {"encode_parameters", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_encode_parameters)),
+     METH_FASTCALL, "MetadataParameters bytes of a dict (bool / int / str, else str(v))."},
+    {"send_bytes", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_bytes)),
+     METH_FASTCALL, "dora_node_send_output_bytes with parameters encoded from a dict."},
+    {"send_array", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_array)),
+     METH_FASTCALL, "dora_node_send_output with parameters encoded from a dict."},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_dora_node",
+                      "Per-send hot path of dora_amd.node (native, like the reference's PyO3 node).",
+                      -1, methods, nullptr, nullptr, nullptr, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__dora_node(void) { return PyModule_Create(&module); }

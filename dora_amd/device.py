@@ -133,6 +133,14 @@ class DeviceArray:
             self._schema = self.export_schema()
         return self._schema
 
+    def send_addrs(self):
+        """(ArrowArray address, borrowed ArrowSchema address) for the native send path."""
+        addrs = self.__dict__.get("_addrs")
+        if addrs is None:
+            addrs = self._addrs = (ctypes.addressof(self.array),
+                                   ctypes.addressof(self.borrowed_schema()))
+        return addrs
+
     def to_pyarrow(self):
         """Download to host memory and import into pyarrow (F12: pyarrow cannot import ROCm)."""
         import pyarrow as pa
@@ -168,6 +176,7 @@ class DeviceArray:
         if self._schema is not None:
             release_schema(self._schema)
             self._schema = None
+        self.__dict__.pop("_addrs", None)
         self._keepalive = None
 
     def __del__(self):

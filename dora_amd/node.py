@@ -25,6 +25,15 @@ from .arrow_c import ArrowArray, ArrowSchema, CArray
 from .device import DeviceArray, DeviceBuffer
 from .type_info import decode
 
+try:
+    from . import _dora_node as _fast
+except ImportError as e:  # no fallback: the send path is native
+    raise ImportError(f"dora_amd._dora_node is missing ({e}): build it with "
+                      "`python -m dora_amd.build`") from e
+
+# MetadataParameters bytes of a dict, natively (the send paths encode inside _fast)
+encode_parameters = _fast.encode_parameters
+
 EVENT_TYPES = {0: "STOP", 1: "INPUT", 2: "INPUT_CLOSED", 3: "ERROR", 4: "ALL_INPUTS_CLOSED"}
 
 
@@ -36,10 +45,10 @@ _TAG_STR = struct.Struct("<BQ").pack
 _KEYS: dict = {}  # encoded key prefix by key (u64 length + utf-8)
 
 
-def encode_parameters(metadata: Optional[dict]) -> bytes:
+def encode_parameters_py(metadata: Optional[dict]) -> bytes:
     """MetadataParameters encoding (pydict_to_metadata, apis/python/operator/src/lib.rs:165-186:
-    bool / int / str, anything else stringified).  On every send: precompiled structs and
-    cached key prefixes keep it ~1 us."""
+    bool / int / str, anything else stringified), in Python: the statement of the format that
+    tests hold the native encoder (`encode_parameters`, csrc/pyext.cpp) to."""
     if not metadata:
         return b""
     out = [_U32(len(metadata))]
@@ -139,32 +148,31 @@ class Node:
 
     # -------------------------------------------------------------------------------- sending
     def send_output(self, output_id: str, data, metadata: Optional[dict] = None):
-        params = encode_parameters(metadata)
-        pb = params
-        oid = output_id.encode()
-        if isinstance(data, (bytes, bytearray, memoryview)):
+        if isinstance(data, DeviceArray):
+            a, s = data.send_addrs()
+            rc = _fast.send_array(self.handle, output_id, a, s, ARROW_DEVICE_ROCM, metadata)
+        elif isinstance(data, (bytes, bytearray, memoryview)):
             buf = ctypes.create_string_buffer(bytes(data), len(data))
-            call("dora_node_send_output_bytes", self.handle, oid, buf, len(data), ARROW_DEVICE_CPU,
-                 pb, len(params))
-        elif isinstance(data, DeviceArray):
-            call("dora_node_send_output", self.handle, oid, byref(data.array),
-                 byref(data.borrowed_schema()), ARROW_DEVICE_ROCM, pb, len(params))
+            rc = _fast.send_bytes(self.handle, output_id, ctypes.addressof(buf), len(data),
+                                  ARROW_DEVICE_CPU, metadata)
         elif isinstance(data, DeviceBuffer):
-            call("dora_node_send_output_bytes", self.handle, oid, data.ptr, data.size,
-                 ARROW_DEVICE_ROCM, pb, len(params))
+            rc = _fast.send_bytes(self.handle, output_id, data.ptr, data.size, ARROW_DEVICE_ROCM,
+                                  metadata)
         elif hasattr(data, "_export_to_c"):
             with CArray.from_pyarrow(data) as c:
-                call("dora_node_send_output", self.handle, oid, byref(c.array), byref(c.schema),
-                     ARROW_DEVICE_CPU, pb, len(params))
+                rc = _fast.send_array(self.handle, output_id, ctypes.addressof(c.array),
+                                      ctypes.addressof(c.schema), ARROW_DEVICE_CPU, metadata)
         else:
             raise TypeError("data must be bytes, a pyarrow.Array, a DeviceArray or a DeviceBuffer")
+        if rc:
+            _lib.check(rc)
 
     def send_output_device_bytes(self, output_id: str, ptr: int, n: int,
                                  metadata: Optional[dict] = None):
         """send_output_raw with an HBM source: one pack kernel into a fresh device sample."""
-        params = encode_parameters(metadata)
-        call("dora_node_send_output_bytes", self.handle, output_id.encode(), ptr, n,
-             ARROW_DEVICE_ROCM, params, len(params))
+        rc = _fast.send_bytes(self.handle, output_id, ptr, n, ARROW_DEVICE_ROCM, metadata)
+        if rc:
+            _lib.check(rc)
 
     def set_compact(self, enable: bool = True):
         """Send device arrays with compacting plans (slices move only their own bytes)."""

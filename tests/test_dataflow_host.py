@@ -10,7 +10,7 @@ import pytest
 
 from dora_amd import _lib
 from dora_amd.dataflow import daemon_spec, parse_descriptor
-from dora_amd.node import Node, decode_parameters, encode_parameters
+from dora_amd.node import Node, decode_parameters, encode_parameters, encode_parameters_py
 
 
 class InProcessDaemon:
@@ -57,6 +57,25 @@ def test_parameters_roundtrip():
     assert decode_parameters(encode_parameters(p)) == {"a": True, "b": -5, "c": "hello",
                                                        "d": "2.5"}
     assert encode_parameters(None) == b""
+
+
+def test_native_parameter_encoding_matches_python():
+    """The native encoder (csrc/pyext.cpp, used by every send) writes the same bytes as the
+    Python statement of the format, for every value kind pydict_to_metadata handles
+    (apis/python/operator/src/lib.rs:165-186) and for non-str keys / big ints."""
+    class Odd:
+        def __str__(self):
+            return "odd\u00e9"
+    cases = [None, {}, {"seq": 0}, {"b": False, "a": True, "c": -1},
+             {"t_start": 1760000000123456789, "seq": 2 ** 63 - 1, "neg": -2 ** 63},
+             {"s": "", "u": "h\u00e9llo \u2603", "f": 2.5, "l": [1, 2], "o": Odd(), "n": None},
+             {"k" * 300: "v" * 5000}, {3: "int key", 1: "x"}]
+    for p in cases:
+        assert encode_parameters(p) == encode_parameters_py(p), p
+    with pytest.raises(OverflowError):
+        encode_parameters({"big": 2 ** 64})
+    with pytest.raises(TypeError):
+        encode_parameters([("a", 1)])
 
 
 def test_descriptor_validation():
