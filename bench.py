@@ -51,6 +51,8 @@ def parse():
                     help="throughput ladder: back-to-back messages per size (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
+    ap.add_argument("--src-offset", type=int, default=0,
+                    help="c2 diagnosis: source bytes start this far past a 256-B boundary")
     ap.add_argument("--no-cross-gpu", action="store_true",
                     help="N>1: skip the C4 fan-out / C5 chain runs after the timed region")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -96,6 +98,15 @@ class Ranks:
 
     def sum(self, x: float) -> float:
         return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist else x
+
+
+def aql_kernel_name(workload: str, body: int) -> str:
+    """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*:
+    8 loads in flight per lane for 8-32 MB bodies, else 4; one segment at offset 0 -> pack1)."""
+    v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
+    u = 8 if v.startswith("u8") else 4 if v.startswith("u4") else (
+        8 if (8 << 20) <= body < (32 << 20) else 4)
+    return f"dora_aql_pack{'1' if workload == 'c2' else ''}_u{u} (AQL)"
 
 
 def pmc_traffic(msg_bytes: int):
@@ -287,10 +298,14 @@ def edge_rates(sinks):
         tp = [s for s in r.get("series", []) if s["input"] == "throughput" and s["n"] > 1]
         gbps = None
         if tp:
-            s = max(tp, key=lambda x: x["n"])
-            span_ns = s["last_ns"] - s["first_ns"]
+            s = max(tp, key=lambda x: x.get("burst_n", x["n"]))
+            # the longest burst between two acks is the back-to-back phase (earlier receipts of
+            # the same input and size, the warmup, would stretch the span over the latency phase)
+            n, first, last = (s["burst_n"], s["burst_first_ns"], s["burst_last_ns"]) \
+                if s.get("burst_n", 0) > 1 else (s["n"], s["first_ns"], s["last_ns"])
+            span_ns = last - first
             # n receipts span n - 1 message intervals
-            gbps = round((s["n"] - 1) * s["size"] / span_ns, 3) if span_ns > 0 else None
+            gbps = round((n - 1) * s["size"] / span_ns, 3) if span_ns > 0 else None
         moved = r.get("pull_bytes", 0) + (r.get("bcast_received", 0) and
                                           sum(x["n"] * x["size"] for x in r.get("series", [])))
         out.append({"sink": sname, "GBps": gbps, "pulls": r.get("pulls", 0),
@@ -407,15 +422,16 @@ def main():
         S = args.size
         nsrc = args.sources or max(2, min(16, (640 << 20) // max(S, 1)))
         srcs = []
+        off = args.src_offset
         for _ in range(nsrc):  # rotate > 512 MiB of sources so the Infinity Cache cannot hold them
-            b = device.DeviceBuffer(S)
-            device.fill_splitmix(b.ptr, S, payload_seed(S), stream)
+            b = device.DeviceBuffer(S + off)
+            device.fill_splitmix(b.ptr + off, S, payload_seed(S), stream)
             srcs.append(b)
         stream.sync()
-        csum = device.csum64(srcs[0].ptr, S, stream)
+        csum = device.csum64(srcs[0].ptr + off, S, stream)
 
         def send(k, meta):
-            node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr, S, meta)
+            node.send_output_device_bytes("throughput", srcs[k % nsrc].ptr + off, S, meta)
     else:
         # C3: List<Struct<x,y,z:f32,intensity:u8>> 1M-point clouds resident in HBM; each send is
         # plan (host DFS + validity read-back for the type info) + nested pack kernel
@@ -681,7 +697,7 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic[1] if traffic else None,
                      "traffic_source": traffic[0] if traffic else None,
-                     "kernel": ("dora_aql_pack1_u4 (AQL)" if stats["fill_paths"]["aql"]
+                     "kernel": (aql_kernel_name(args.workload, S) if stats["fill_paths"]["aql"]
                                 else "pack_kernel (HIP fill streams)"),
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
                      "region_packs": packs, "region_span_us": round(span_ms * 1e3, 1),

@@ -40,7 +40,12 @@ struct Variant {
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
-std::atomic<uint32_t> g_signal_grid{0};  // workgroups of a signalling launch (0: kSignalGrid)
+uint32_t env_u32(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
+}
+// workgroups of a signalling launch (0: kSignalGrid; DORA_GPU_SIGNAL_GRID, dora_gpu_pack_tune)
+std::atomic<uint32_t> g_signal_grid{env_u32("DORA_GPU_SIGNAL_GRID")};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win

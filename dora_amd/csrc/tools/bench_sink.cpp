@@ -25,6 +25,17 @@ namespace {
 struct Series {
   std::vector<double> lat_us, full_us;
   uint64_t first_ns = 0, last_ns = 0, n = 0, bytes = 0, verified = 0, mismatches = 0;
+  // bursts: receipts between two acks (the source's barriers delimit its warmup, latency and
+  // throughput phases); the longest one is the throughput phase, whose rate the bench reports
+  uint64_t b_first = 0, b_last = 0, b_n = 0, tp_first = 0, tp_last = 0, tp_n = 0;
+  void close_burst() {
+    if (b_n > tp_n) {
+      tp_n = b_n;
+      tp_first = b_first;
+      tp_last = b_last;
+    }
+    b_n = b_first = b_last = 0;
+  }
 };
 
 double pct(std::vector<double> v, double p) {
@@ -160,6 +171,9 @@ int main() {
       if (!s.first_ns) s.first_ns = t;
       s.last_ns = t;
       ++s.n;
+      if (!s.b_first) s.b_first = t;
+      s.b_last = t;
+      ++s.b_n;
       s.bytes += len;
       const bool dev = dora_event_is_device(ev);
       if (params.count("csum") && params.count("verify") && dev)
@@ -173,6 +187,8 @@ int main() {
         t_free += mono() - tf0;
       }
       ++n_inputs;
+      if (ack)
+        for (auto& kv : stats) kv.second.close_burst();
       if (ack) {
         for (Held& h : held) {
           verify(h.p, h.len, h.csum, *h.s);
@@ -218,18 +234,22 @@ int main() {
                (unsigned long long)pulls, (unsigned long long)pull_bytes,
                (unsigned long long)bgroups, (unsigned long long)brecv, json_safe(berr).c_str());
   bool first = true;
+  for (auto& kv : stats) kv.second.close_burst();
   for (auto& kv : stats) {
     Series& s = kv.second;
     std::fprintf(f,
                  "%s\n {\"input\": \"%s\", \"size\": %llu, \"n\": %llu, \"p50_us\": %.3f, "
                  "\"p99_us\": %.3f, \"mean_us\": %.3f, \"min_us\": %.3f, \"full_p50_us\": %.3f, "
                  "\"full_p99_us\": %.3f, \"first_ns\": %llu, \"last_ns\": %llu, \"verified\": "
-                 "%llu, \"mismatches\": %llu}",
+                 "%llu, \"mismatches\": %llu, \"burst_n\": %llu, \"burst_first_ns\": %llu, "
+                 "\"burst_last_ns\": %llu}",
                  first ? "" : ",", kv.first.first.c_str(), (unsigned long long)kv.first.second,
                  (unsigned long long)s.n, pct(s.lat_us, 0.5), pct(s.lat_us, 0.99), mean(s.lat_us),
                  pct(s.lat_us, 0.0), pct(s.full_us, 0.5), pct(s.full_us, 0.99),
                  (unsigned long long)s.first_ns, (unsigned long long)s.last_ns,
-                 (unsigned long long)s.verified, (unsigned long long)s.mismatches);
+                 (unsigned long long)s.verified, (unsigned long long)s.mismatches,
+                 (unsigned long long)s.tp_n, (unsigned long long)s.tp_first,
+                 (unsigned long long)s.tp_last);
     first = false;
   }
   std::fprintf(f, "\n], \"acks\": [");

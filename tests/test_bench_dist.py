@@ -105,3 +105,17 @@ def test_summarize_cross_without_link_traffic_has_no_roofline():
     r = bench.summarize_cross("c4", src, {"sink1": sink}, {"source": 0}, {})
     assert r["roofline"] is None and "no byte crossed" in r["note"]
     assert r["edges"][0]["xgmi_frac"] is None
+
+
+def test_edge_rate_uses_the_throughput_burst():
+    """The sink's series of one (input, size) also holds the warmup receipts, seconds before the
+    back-to-back phase; the edge rate comes from the longest burst between two acks (r02 N=2
+    rehearsal: 1.25 GB/s over the whole series vs ~1300 GB/s delivered)."""
+    import bench
+    sink = {"pulls": 200, "pull_bytes": 200 * 100, "series": [
+        {"input": "throughput", "size": 100, "n": 13, "first_ns": 0, "last_ns": 10 ** 9 + 2000,
+         "burst_n": 11, "burst_first_ns": 10 ** 9 + 1000, "burst_last_ns": 10 ** 9 + 2000}]}
+    e = bench.edge_rates({"sink1": sink})[0]
+    assert e["GBps"] == 1.0 and e["xgmi_frac"] == round(1.0 / bench.XGMI_LINK_GBPS, 4)
+    old = {"pulls": 0, "series": [dict(sink["series"][0], burst_n=0)]}  # older sinks: whole series
+    assert bench.edge_rates({"s": old})[0]["GBps"] == round(12 * 100 / (10 ** 9 + 2000), 3)
