@@ -51,6 +51,8 @@ def parse():
                     help="throughput ladder: back-to-back messages per size (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
+    ap.add_argument("--c3-lists", type=int, default=0,
+                    help="c3 diagnosis: lists per cloud (15: every buffer at 0 mod 16)")
     ap.add_argument("--src-offset", type=int, default=0,
                     help="c2 diagnosis: source bytes start this far past a 256-B boundary")
     ap.add_argument("--no-cross-gpu", action="store_true",
@@ -438,7 +440,7 @@ def main():
         from dora_amd.arrow_utils import Plan
         from dora_amd.device import DeviceArray
         from dora_amd.workloads import point_cloud
-        cloud = point_cloud()
+        cloud = point_cloud(n_lists=args.c3_lists) if args.c3_lists else point_cloud()
         nsrc = args.sources or 24
         srcs = [DeviceArray.from_pyarrow(cloud) for _ in range(nsrc)]
         with Plan.of(srcs[0]) as p:

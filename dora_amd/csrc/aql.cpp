@@ -28,7 +28,7 @@ namespace dora {
 
 // kernels.hip: the AQL kernels' argument block for `n` segments (<= aql_max_segments()).
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid, int* unroll);
+                   uint8_t* out, size_t cap, uint32_t* grid, int* unroll, uint64_t dst_cap);
 size_t aql_args_size();
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
                     uint32_t* grid, int* unroll);
@@ -339,7 +339,7 @@ void aql_forget_flags(int device, const void* base, size_t size) {
 }
 
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-             const std::atomic<uint64_t>* flag_host, bool profile) {
+             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   std::lock_guard<std::mutex> g(a->mu);
   // the argument slot of the dispatch kRingSlots back must have completed
@@ -361,7 +361,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // one segment at sample offset 0: the preloaded kernels, arguments from host memory
   const bool one = a->hring && n == 1 && segs[0].dst_off == 0;
   int rc = one ? build_aql_args1(segs[0], dst, sig, args, &grid, &unroll)
-               : build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll);
+               : build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll, dst_cap);
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};
   static const bool no_prof = [] {

@@ -27,10 +27,11 @@ AqlQueue* aql_queue(int device);
 // Dispatch one signalling pack of `n` (<= 8) device-source copy segments into `dst`; the launch
 // stores `sig.epoch` into `sig.flag` when the sample is complete.  `flag_host` is the host view
 // of that flag (kernarg slots are recycled once the launch that used them has signalled).
+// `dst_cap`: bytes writable from `dst` (0: unknown; see launch_pack).
 // With `profile`, the packet carries a completion signal whose dispatch times
 // aql_profile_take() reports.
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-             const std::atomic<uint64_t>* flag_host, bool profile);
+             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0);
 
 // Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
 // region about to be unmapped), after waiting (bounded) for those fills to signal.

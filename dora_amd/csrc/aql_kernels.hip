@@ -27,11 +27,8 @@ template <int U>
 __device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t len,
                                       uint64_t* flag, uint32_t* done, uint64_t epoch,
                                       uint32_t chunk_bytes, uint32_t grid) {
-  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
-  const uint64_t A0 = (base + 15) & ~uint64_t(15);
-  const uint64_t A1 = (base + len) & ~uint64_t(15);
-  const uint64_t body = A1 > A0 ? A1 - A0 : 0;
-  const uint64_t nc = body ? (body + chunk_bytes - 1) / chunk_bytes : 1;
+  const uint64_t nc =
+      dora::pack::segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, len, chunk_bytes);
   dora::pack::PackArgsT<1> a;
   a.dst = dst;
   a.flag = flag;
@@ -41,6 +38,7 @@ __device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t
   a.nseg = 1;
   a.chunk_bytes = chunk_bytes;
   a.grid = grid;
+  a.edge_mask = 0;  // a tail unit past `len` may lie outside the destination: bytes one by one
   a.chunk_end[0] = static_cast<uint32_t>(nc);
   a.seg[0] = {src, 0, len};
   dora::pack::pack_body<U, 2>(a, __builtin_amdgcn_workgroup_id_x(), grid);

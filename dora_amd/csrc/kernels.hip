@@ -40,6 +40,15 @@ struct Variant {
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
 std::atomic<int> g_nt{-1};          // -1 = default (off) / env
 std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
+// DORA_GPU_LINE_CHUNKS=0: body chunks start at the first aligned unit (pack_device.h kLine)
+bool line_chunks() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_LINE_CHUNKS");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 uint32_t env_u32(const char* name) {
   const char* e = std::getenv(name);
   return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
@@ -140,7 +149,7 @@ uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
   if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
     uint64_t v = std::strtoull(e, nullptr, 10);
-    if (v >= 16 && v % 16 == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
+    if (v >= kLine && v % kLine == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
   }
   // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
   // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
@@ -214,6 +223,28 @@ unsigned grid_for(uint64_t items) {
 
 }  // namespace
 
+// Boundary units written whole (PackArgsT::edge_mask) for one launch holding every segment of
+// its plan: a segment's unaligned head / tail unit is stitched when it lies inside the writable
+// destination [dst, dst + cap).  Segments must be sorted by destination offset and disjoint, as
+// plans are (else nothing is stitched), so every byte of such a unit belongs to a segment of
+// this launch or is padding.  cap 0 (unknown extent, host destinations): nothing is stitched.
+uint64_t edge_mask(const Segment* segs, size_t n, const uint8_t* dst, uint64_t cap) {
+  if (!cap || n > 32) return 0;
+  for (size_t k = 1; k < n; ++k)
+    if (segs[k].dst_off < segs[k - 1].dst_off + segs[k - 1].len) return 0;
+  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  auto inside = [&](uint64_t unit) { return unit >= base && unit + 16 <= base + cap; };
+  uint64_t mask = 0;
+  for (size_t k = 0; k < n; ++k) {
+    const uint64_t d0 = base + segs[k].dst_off, d1 = d0 + segs[k].len;
+    if (d1 == d0) continue;
+    const uint64_t A0 = (d0 + 15) & ~uint64_t(15);
+    if (A0 > d0 && inside(A0 - 16)) mask |= uint64_t(1) << (2 * k);
+    if (A0 < d1 && (d1 & 15) && inside(d1 & ~uint64_t(15))) mask |= uint64_t(2) << (2 * k);
+  }
+  return mask;
+}
+
 // Launch the pack of `n` segments into `dst` (device).  Copy segments with device sources go
 // to pack_kernel in batches of kMaxSegs, transform segments (compacting plans) to
 // transform_kernel; host sources are DMA'd with hipMemcpyAsync.  With timing events the
@@ -221,7 +252,7 @@ unsigned grid_for(uint64_t items) {
 // begin into `ev_start` and the last kernel's end into `ev_stop`.
 int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_t* dst,
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
-                const FillSignal* signal, bool* signalled) {
+                const FillSignal* signal, bool* signalled, uint64_t dst_cap) {
   if (signalled) *signalled = false;
   bool any_x = false;
   for (size_t i = 0; i < n_in; ++i) any_x |= segs_in[i].op != SEG_COPY;
@@ -258,16 +289,14 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     for (size_t k = 0; k < m; ++k) {
       const Segment& s = segs[i + k];
       a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
-      const uint64_t base = reinterpret_cast<uintptr_t>(dst);
-      const uint64_t A0 = (base + s.dst_off + 15) & ~uint64_t(15);
-      const uint64_t A1 = (base + s.dst_off + s.len) & ~uint64_t(15);
-      const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
-      const uint64_t nc = std::max<uint64_t>(1, (bodyb + a.chunk_bytes - 1) / a.chunk_bytes);
-      chunks += nc;
+      chunks += segment_chunks(reinterpret_cast<uintptr_t>(dst), s.dst_off, s.len, a.chunk_bytes,
+                               line_chunks());
       if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
       a.chunk_end[k] = static_cast<uint32_t>(chunks);
     }
-    a.nseg = static_cast<uint32_t>(m);
+    a.nseg = static_cast<uint32_t>(m) | (line_chunks() ? 0u : kUnitChunks);
+    // one launch holding the whole plan: its boundary units may be written whole
+    if (!any_x && m == n) a.edge_mask = edge_mask(segs, n, dst, dst_cap);
     const bool first = launch == 0, last = launch + 1 == n_launch;
     a.n_chunks = static_cast<uint32_t>(chunks);
     uint64_t grid = chunks;
@@ -383,7 +412,8 @@ size_t aql_args_size() { return sizeof(AqlPackArgs); }
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid_out, int* unroll_out) {
+                   uint8_t* out, size_t cap, uint32_t* grid_out, int* unroll_out,
+                   uint64_t dst_cap) {
   if (n == 0 || n > size_t(kMaxAqlSegs)) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   if (cap < sizeof(AqlPackArgs)) return fail(DORA_ERR_INVALID, "AQL pack: argument buffer");
   AqlPackArgs a;
@@ -402,14 +432,12 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   for (size_t k = 0; k < n; ++k) {
     const Segment& s = segs[k];
     a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
-    const uint64_t A0 = (base + s.dst_off + 15) & ~uint64_t(15);
-    const uint64_t A1 = (base + s.dst_off + s.len) & ~uint64_t(15);
-    const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
-    chunks += std::max<uint64_t>(1, (bodyb + a.chunk_bytes - 1) / a.chunk_bytes);
+    chunks += segment_chunks(base, s.dst_off, s.len, a.chunk_bytes, line_chunks());
     if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
     a.chunk_end[k] = static_cast<uint32_t>(chunks);
   }
-  a.nseg = static_cast<uint32_t>(n);
+  a.nseg = static_cast<uint32_t>(n) | (line_chunks() ? 0u : kUnitChunks);
+  a.edge_mask = edge_mask(segs, n, dst, dst_cap);
   a.n_chunks = static_cast<uint32_t>(chunks);
   const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
   const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
@@ -434,11 +462,8 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
   Variant var = pack_variant();
   if (var.unroll == 0) var.unroll = (sg.len >= (8u << 20) && sg.len < (32u << 20)) ? 8 : 4;
   const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, var.unroll);
-  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
-  const uint64_t A0 = (base + 15) & ~uint64_t(15);
-  const uint64_t A1 = (base + sg.len) & ~uint64_t(15);
-  const uint64_t bodyb = A1 > A0 ? A1 - A0 : 0;
-  const uint64_t chunks = std::max<uint64_t>(1, (bodyb + chunk_bytes - 1) / chunk_bytes);
+  const uint64_t chunks =
+      segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
   const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
   const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
@@ -503,11 +528,11 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                          reinterpret_cast<uint32_t*>(scratch + 64)};
     return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                              static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream),
-                             nullptr, nullptr, &sig, nullptr);
+                             nullptr, nullptr, &sig, nullptr, dst_len);
   }
   return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                            static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream), nullptr,
-                           nullptr);
+                           nullptr, nullptr, nullptr, dst_len);
 }
 
 int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal) {
@@ -519,7 +544,8 @@ int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal) {
 int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
   if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8)
     return dora::fail(DORA_ERR_INVALID, "unroll must be 0, 2, 4 or 8");
-  if (chunk_bytes % 16) return dora::fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 16");
+  if (chunk_bytes % dora::pack::kLine)
+    return dora::fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 128 (a cache line)");
   dora::g_unroll.store(unroll);
   dora::g_nt.store(nontemporal < 0 ? -1 : (nontemporal ? 1 : 0));
   dora::g_chunk.store(chunk_bytes);

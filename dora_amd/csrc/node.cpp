@@ -1401,7 +1401,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     // the caller orders what follows on `st` (a broadcast-group send): no fill flag
     ++n->hip_packs;
     return launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start, t_stop,
-                       nullptr, nullptr);
+                       nullptr, nullptr, slot_bytes(s->slot->cap));
   }
   FillSignal sig{};
   const FillSignal* sp = nullptr;
@@ -1419,7 +1419,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     if (AqlQueue* q = aql_queue(n->core->device)) {
       const std::atomic<uint64_t>* fh = n->core->flag_host(s->slot->flag);
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed) == DORA_OK) {
+                   n->region_armed, slot_bytes(s->slot->cap)) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -1435,7 +1435,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   ++n->hip_packs;
   bool signalled = false;
   int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start,
-                       t_stop, sp, &signalled);
+                       t_stop, sp, &signalled, slot_bytes(s->slot->cap));
   if (rc != DORA_OK) return rc;
   if (signalled) {
     s->epoch = sig.epoch;

@@ -29,6 +29,27 @@ constexpr int kMaxAqlSegs = 8;     // segments of an AQL-dispatched pack (smalle
 // Workgroups of a signalling pack (r01 sweep, profiles/r01_signal_sweep.jsonl: 1024 beats 512
 // and 2048-4096 at 16-40 MB, flat at 4 MB).
 constexpr uint32_t kSignalGrid = 1024;
+// Chunk windows start on a cache line: a segment's body is cut into chunks from the 128-byte
+// line holding its first aligned unit, so every wave's 1 KiB store covers whole lines (64-byte
+// HBM write sectors) and no two waves write parts of one sector.  A body at 16 mod 64 — C3's
+// x/y/z/intensity after 68 bytes of list offsets — otherwise gave every wave store two partial
+// sectors, each a read-modify-write in the memory controller: ~10 % of the pack's device time
+// (profiles/r02_c3_edges_ab.jsonl, the same cloud with every buffer at 0 mod 64).
+constexpr uint64_t kLine = 128;
+
+// Bit 31 of PackArgsT::nseg: chunks start at the first aligned unit instead (the r01 layout;
+// DORA_GPU_LINE_CHUNKS=0, an A/B knob).
+constexpr uint32_t kUnitChunks = 1u << 31;
+
+// Chunks of one segment [d0, d0 + len) of a destination at `base` (host and device agree).
+__host__ __device__ inline uint64_t segment_chunks(uint64_t base, uint64_t d0, uint64_t len,
+                                                   uint64_t chunk_bytes, bool line = true) {
+  const uint64_t A0 = (base + d0 + 15) & ~uint64_t(15);
+  const uint64_t A1 = (base + d0 + len) & ~uint64_t(15);
+  if (A1 <= A0) return 1;
+  const uint64_t O = line ? A0 & ~(kLine - 1) : A0;
+  return (A1 - O + chunk_bytes - 1) / chunk_bytes;
+}
 
 struct PackSeg {
   const uint8_t* src;
@@ -46,6 +67,9 @@ struct PackArgsT {
   uint32_t nseg;
   uint32_t chunk_bytes;  // multiple of 16
   uint32_t grid;         // workgroups launched (AQL kernels cannot read gridDim)
+  // Bits 2k / 2k+1: the 16-byte unit holding segment k's unaligned head / tail bytes is written
+  // whole (edge_mask(), kernels.hip); clear: those bytes are stored one by one.
+  uint64_t edge_mask;
   uint32_t chunk_end[MAXSEG];
   PackSeg seg[MAXSEG];
 };
@@ -104,33 +128,36 @@ __device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
 
 // Body copy of `nunits` 16-byte units: dst 16-aligned, source `sp` 16-aligned (DW: 4-aligned).
 // U loads of 16 B per lane in flight before the stores.
+// Units [skip, nunits) are copied; the first `skip` (< 8, a chunk starting mid-line) only keep
+// the lanes' windows on whole lines, their addresses are never dereferenced.
 template <int U, int NT, bool DW = false>
-__device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t nunits) {
+__device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t skip,
+                                             uint64_t nunits) {
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) v[u] = ld16<NT, DW>(sp + 16 * i);
+      if (i >= skip && i < nunits) v[u] = ld16<NT, DW>(sp + 16 * i);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16<NT>(dp + 16 * i, v[u]);
+      if (i >= skip && i < nunits) st16<NT>(dp + 16 * i, v[u]);
     }
   }
 }
 
 template <int U, int NT, int Q>
 __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
-                                             uint64_t nunits) {
+                                             uint64_t skip, uint64_t nunits) {
   // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 lo[U], hi[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) {
+      if (i >= skip && i < nunits) {
         lo[u] = ld16<NT>(sbase + 16 * i);
         hi[u] = ld16<NT>(sbase + 16 * i + 16);
       }
@@ -138,15 +165,27 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i < nunits) st16<NT>(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
+      if (i >= skip && i < nunits) st16<NT>(dp + 16 * i, funnel<Q>(lo[u], hi[u], b));
     }
   }
 }
 
+// Byte `o` (sample offset) of a stitched boundary unit: from the segment that holds it, else
+// the byte the destination already has (padding stays as it was, arrow_utils.rs:48).
+template <class A>
+__device__ __forceinline__ uint8_t unit_byte(const A& a, uint64_t o) {
+  for (uint32_t k = 0; k < (a.nseg & ~kUnitChunks); ++k) {
+    const PackSeg g = a.seg[k];
+    if (o - g.dst_off < g.len) return g.src[o - g.dst_off];  // unsigned: o in [dst_off, +len)
+  }
+  return a.dst[o];
+}
+
 template <int U, int NT, class A>
 __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
+  const uint32_t nseg = args.nseg & ~kUnitChunks;
   uint32_t s = 0;
-  while (s + 1 < args.nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
+  while (s + 1 < nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
   const PackSeg sg = args.seg[s];
   const uint32_t c = chunk - (s ? args.chunk_end[s - 1] : 0u);
 
@@ -161,42 +200,74 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
   const uint8_t* const src = sg.src;  // source byte of sample offset d is src[d - d0]
 
   if (c == 0) {
-    // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1), byte by byte (< 16 each).
-    const uint64_t hend = a0 < d1 ? a0 : d1;
-    const uint64_t nhead = hend - d0;
-    if (threadIdx.x < nhead) st1<NT>(dst + d0 + threadIdx.x, src[threadIdx.x]);
-    if (a0 < d1) {
+    // Unaligned head [d0, min(a0, d1)) and tail [max(a1, a0), d1) (< 16 bytes each).  Their
+    // 16-byte units (shared with the neighbouring segment or padding) are either written whole —
+    // "stitched": one lane-group gathers the unit's 16 bytes from every segment that holds one
+    // and one lane stores it with the body's full-width store — or byte by byte.  Sub-dword
+    // write-through stores made a C3 pack ~10 % slower than the same sample with every buffer at
+    // 0 mod 16 (profiles/r02_c3_edges_ab.jsonl).
+    const uint32_t em = static_cast<uint32_t>(args.edge_mask >> (2 * s)) & 3u;
+    const bool has_head = d1 > d0 && a0 > d0;
+    const bool has_tail = a0 < d1 && ((base + d1) & 15u) != 0;
+    const bool st_head = has_head && (em & 1u), st_tail = has_tail && (em & 2u);
+    const uint32_t t = threadIdx.x;
+    if (has_head && !st_head) {
+      const uint64_t hend = a0 < d1 ? a0 : d1;
+      if (t < hend - d0) st1<NT>(dst + d0 + t, src[t]);
+    }
+    if (has_tail && !st_tail) {
       const uint64_t t0 = a1 > a0 ? a1 : a0;
-      const uint64_t ntail = d1 - t0;
-      if (threadIdx.x >= 64 && threadIdx.x - 64 < ntail) {
-        const uint64_t d = t0 + (threadIdx.x - 64);
+      if (t >= 64 && t - 64 < d1 - t0) {
+        const uint64_t d = t0 + (t - 64);
         st1<NT>(dst + d, src[d - d0]);
       }
     }
+    if (st_head || st_tail) {  // uniform over the workgroup
+      __shared__ u32x4 unit[2];
+      uint8_t* const ub = reinterpret_cast<uint8_t*>(unit);
+      const uint64_t H = a0 - 16;                            // head unit (sample offset)
+      const uint64_t T = ((base + d1) & ~uint64_t(15)) - base;  // tail unit
+      // a unit shared with the previous segment is written by that segment (the lowest one
+      // holding a byte of it); a tail unit always belongs to its segment
+      const bool own_head = st_head && (s == 0 || args.seg[s - 1].dst_off + args.seg[s - 1].len <= H);
+      if (own_head && t < 16) ub[t] = unit_byte(args, H + t);
+      if (st_tail && t >= 64 && t < 80) ub[16 + (t - 64)] = unit_byte(args, T + (t - 64));
+      __syncthreads();
+      if (own_head && t == 0) st16<NT>(dst + H, unit[0]);
+      if (st_tail && t == 64) st16<NT>(dst + T, unit[1]);
+      __syncthreads();  // unit[] is reused by this workgroup's next segment
+    }
   }
   if (a0 >= a1) return;
-  const uint64_t b0 = a0 + uint64_t(c) * args.chunk_bytes;
-  if (b0 >= a1) return;
-  const uint64_t b1 = (a1 - b0) > args.chunk_bytes ? b0 + args.chunk_bytes : a1;
-  const uint64_t nunits = (b1 - b0) >> 4;
-  uint8_t* dp = dst + b0;
-  const uint8_t* sp = src + (b0 - d0);
+  // chunk c covers [O + c * chunk_bytes, +chunk_bytes) of the body, O = the line of its first
+  // aligned unit (kLine; segment_chunks counts them the same way).  Absolute addresses: O may
+  // lie before the destination's base.
+  const uint64_t E0 = base + a0, E1 = base + a1;  // the body, absolute (A0, A1 when non-empty)
+  const uint64_t O = (args.nseg & kUnitChunks) ? E0 : E0 & ~(kLine - 1);
+  const uint64_t B0 = O + uint64_t(c) * args.chunk_bytes;
+  if (B0 >= E1) return;
+  const uint64_t B1 = (E1 - B0) > args.chunk_bytes ? B0 + args.chunk_bytes : E1;
+  const uint64_t skip = B0 < E0 ? (E0 - B0) >> 4 : 0;
+  const uint64_t nunits = (B1 - B0) >> 4;
+  uint8_t* dp = reinterpret_cast<uint8_t*>(B0);
+  // the source byte of B0 (before src for skipped units: never dereferenced)
+  const uint8_t* sp = src + (static_cast<int64_t>(B0 - base) - static_cast<int64_t>(d0));
   const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15);
   if (r == 0) {
-    copy_aligned<U, NT>(dp, sp, nunits);
+    copy_aligned<U, NT>(dp, sp, skip, nunits);
     return;
   }
   if ((r & 3) == 0) {  // whole-dword disagreement: one 16-B load at the source address
-    copy_aligned<U, NT, true>(dp, sp, nunits);
+    copy_aligned<U, NT, true>(dp, sp, skip, nunits);
     return;
   }
   const uint8_t* sbase = sp - r;
   const uint32_t b = r & 3;
   switch (r >> 2) {
-    case 0: copy_shifted<U, NT, 0>(dp, sbase, b, nunits); break;
-    case 1: copy_shifted<U, NT, 1>(dp, sbase, b, nunits); break;
-    case 2: copy_shifted<U, NT, 2>(dp, sbase, b, nunits); break;
-    default: copy_shifted<U, NT, 3>(dp, sbase, b, nunits); break;
+    case 0: copy_shifted<U, NT, 0>(dp, sbase, b, skip, nunits); break;
+    case 1: copy_shifted<U, NT, 1>(dp, sbase, b, skip, nunits); break;
+    case 2: copy_shifted<U, NT, 2>(dp, sbase, b, skip, nunits); break;
+    default: copy_shifted<U, NT, 3>(dp, sbase, b, skip, nunits); break;
   }
 }
 

@@ -87,10 +87,12 @@ constexpr uint32_t kMaxSignalWgs = 4096;
 
 // Launch the pack of `segs` into `dst` on `stream` (kernels.hip).  With `signal`, the last
 // launch writes the fill flag itself when it can (`*signalled` says whether it did; compacting
-// transforms and host sources leave it to the caller).
+// transforms and host sources leave it to the caller).  `dst_cap`: bytes writable from `dst`
+// (0: unknown), which lets the boundary units of the segments be written whole.
 int launch_pack(const Segment* segs, size_t n, ArrowDeviceType dev, uint8_t* dst,
                 hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
-                const FillSignal* signal = nullptr, bool* signalled = nullptr);
+                const FillSignal* signal = nullptr, bool* signalled = nullptr,
+                uint64_t dst_cap = 0);
 
 // Pack device segments into `dst` (device or mapped host memory) and return once complete,
 // waiting on the launch's own fill signal instead of a blocking stream synchronise.

@@ -259,3 +259,42 @@ def test_compact_pack_roundtrip(dev, arr):
             assert host.offset == 0
     finally:
         plan.close(); buf.free(); da.close()
+
+
+def _regions(info):
+    out = [(b.offset, b.len) for b in info.buffer_offsets]
+    for c in info.child_data:
+        out += _regions(c)
+    return out
+
+
+@pytest.mark.parametrize("name", _all_cases())
+@pytest.mark.parametrize("slack", [0, 48])
+def test_stitched_edges_keep_regions_and_padding(dev, name, slack):
+    """Boundary units written whole (pack_device.h: a segment's unaligned head/tail unit is
+    gathered from every segment holding a byte of it and stored at full width when it lies in
+    the writable destination): every region equals the oracle's, and every byte outside the
+    regions — padding between buffers and the slack past the sample — keeps the poison."""
+    from oracle.pack_ref import pack
+    from tests.golden import recipes
+    from dora_amd.arrow_utils import Plan
+    from dora_amd.device import DeviceArray, DeviceBuffer
+    arr = recipes.build(name)
+    want, info = pack(arr)
+    da = DeviceArray.from_pyarrow(arr)
+    plan = Plan.of(da)
+    n = plan.size
+    buf = DeviceBuffer(n + slack + 1)
+    try:
+        buf.fill(0xC7, dev)
+        plan.pack(buf.ptr, n + slack, dev)
+        dev.sync()
+        got = buf.to_bytes(n + slack + 1)
+        covered = bytearray(n + slack + 1)
+        for off, ln in _regions(info):
+            assert got[off:off + ln] == want[off:off + ln], (name, off, ln)
+            covered[off:off + ln] = b"\x01" * ln
+        stale = [i for i in range(n + slack + 1) if not covered[i] and got[i] != 0xC7]
+        assert not stale, (name, stale[:16])
+    finally:
+        plan.close(); buf.free(); da.close()
