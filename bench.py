@@ -102,6 +102,32 @@ class Ranks:
         return self._reduce(x, self.dist.ReduceOp.SUM) if self.dist else x
 
 
+def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
+    """hipMemcpyAsync device-to-device of `size` bytes, `reps` back-to-back copies from `n_src`
+    rotating sources (beyond the 256 MB Infinity Cache at the headline size), timed with events
+    on one stream: the plain copy rate of this box right now, in 2·S bytes per second (TB/s)."""
+    from dora_amd import device
+    from dora_amd._lib import call
+    srcs = [device.DeviceBuffer(size) for _ in range(n_src)]
+    dst = device.DeviceBuffer(size)
+    e0, e1 = device.Event(), device.Event()
+    try:
+        for k in range(3):
+            call("dora_gpu_memcpy_async", dst.ptr, srcs[k % n_src].ptr, size, stream.handle)
+        e0.record(stream)
+        for k in range(reps):
+            call("dora_gpu_memcpy_async", dst.ptr, srcs[k % n_src].ptr, size, stream.handle)
+        e1.record(stream)
+        e1.sync()
+        us = e0.elapsed_ms(e1) * 1e3 / reps
+        return {"bytes": size, "us_per_copy": round(us, 3),
+                "TBps_2S": round(2 * size / (us * 1e-6) / 1e12, 3)}
+    finally:
+        e0.close(); e1.close(); dst.free()
+        for b in srcs:
+            b.free()
+
+
 def aql_kernel_name(workload: str, body: int) -> str:
     """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*:
     8 loads in flight per lane for 8-32 MB bodies, else 4; one segment at offset 0 -> pack1)."""
@@ -457,6 +483,8 @@ def main():
     def wait_ack(seq, timeout=60.0):
         node.wait_input("ack", "seq", seq, timeout)
 
+    copy_cal = box_copy_rate(S, stream)
+
     # ---- cold start: the very first message (device queues, code object, the sink's first IPC
     # mapping), reported on its own so the ladders below measure a warm data plane ----
     seq = 0
@@ -697,6 +725,8 @@ def main():
         "throughput_per_size_native": native,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "vs_box_copy": (round(achieved / (copy_cal["TBps_2S"] * 1e3), 3)
+                                     if copy_cal and copy_cal.get("TBps_2S") else None),
                      "traffic": traffic[1] if traffic else None,
                      "traffic_source": traffic[0] if traffic else None,
                      "kernel": (aql_kernel_name(args.workload, S) if stats["fill_paths"]["aql"]
@@ -716,6 +746,9 @@ def main():
         "parity": {"verified_msgs": verified, "mismatches": mismatches,
                    "timed_region_verified": verified - min(3, args.warmup)},
         "cold_start_us": round(cold_start_us, 1),
+        # the same box's plain device copy of the message size, measured right before the run:
+        # boxes differ (and GPUs are shared), so the pack's rate reads against this
+        "box_copy": copy_cal,
         "cold_start_send_us": round(cold_send_us, 1),
         "timed_region": region_setup,
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
