@@ -484,6 +484,9 @@ def main():
         node.wait_input("ack", "seq", seq, timeout)
 
     copy_cal = box_copy_rate(S, stream)
+    # the same at the mid sizes, where per-message dispatch rather than HBM binds
+    copy_mid = {str(z): box_copy_rate(z, stream) for z in (4 << 20, 16 << 20)
+                if z != S and not args.no_ladder}
 
     # ---- cold start: the very first message (device queues, code object, the sink's first IPC
     # mapping), reported on its own so the ladders below measure a warm data plane ----
@@ -749,6 +752,7 @@ def main():
         # the same box's plain device copy of the message size, measured right before the run:
         # boxes differ (and GPUs are shared), so the pack's rate reads against this
         "box_copy": copy_cal,
+        "box_copy_mid": copy_mid,
         "cold_start_send_us": round(cold_send_us, 1),
         "timed_region": region_setup,
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},

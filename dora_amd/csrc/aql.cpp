@@ -439,16 +439,25 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p->kernarg_address = slot;
   p->reserved2 = 0;
   p->completion_signal = done;
-  // agent-scope fences: the pack reads device memory of this GPU and publishes its sample
-  // itself (write-through stores + fill flag).  Below the barrier size no barrier bit, so packs
+  // agent-scope acquire: the pack reads device memory of this GPU; it publishes its sample
+  // itself (write-through stores + fill flag), so no release (below).  Below the barrier size no barrier bit, so packs
   // of one queue overlap (ramps and signal tails hide behind each other); HBM-bound packs at or
   // above it run one at a time per queue, like HIP stream order (more concurrent 40 MB copies
   // only contend for HBM).
   const bool barrier = big;
+  // No release fence at the end of a pack: its sample, done words and fill flag are all stored
+  // write-through (sc1 / system scope) and complete before the flag is set, so the kernel-end
+  // L2 write-back has nothing of the pack's to publish — and costs C3 ~8 % of its device time
+  // (5.18-5.41 -> 4.81-4.83 us per cloud, profiles/r02_release_ab.jsonl; 4 / 16 MB unchanged).
+  // DORA_GPU_AQL_RELEASE=agent restores it (A/B knob).
+  static const uint32_t release = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_RELEASE");
+    return uint32_t(e && std::string(e) == "agent" ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE);
+  }();
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                           (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
                           (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                          (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                          (release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
                    __ATOMIC_RELEASE);
