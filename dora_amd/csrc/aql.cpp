@@ -454,9 +454,15 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     const char* e = std::getenv("DORA_GPU_AQL_RELEASE");
     return uint32_t(e && std::string(e) == "agent" ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE);
   }();
+  // DORA_GPU_AQL_ACQUIRE=none: measurement knob only (a pack could then read source lines a
+  // stale L2 still holds)
+  static const uint32_t acquire = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_ACQUIRE");
+    return uint32_t(e && std::string(e) == "none" ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT);
+  }();
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                           (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
-                          (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                          (acquire << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
