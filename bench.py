@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
                     help="c2: UInt8 payloads (BASELINE configs[1], default); c3: nested "
                          "List<Struct<x,y,z,intensity>> 1M-point clouds (configs[2])")
-    ap.add_argument("--lat-n", type=int, default=50, help="latency-mode messages per size")
+    ap.add_argument("--lat-n", type=int, default=1000,
+                    help="latency-mode messages per size (SURVEY §8d: >= 1000 for a stable p99)")
     ap.add_argument("--lat-gap-us", type=int, default=1000)
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--tp-n", type=int, default=200,
