@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 LADDER = [4096, 16384, 40960, 65536, 409600, 1 << 20, 4096000, 4 << 20, 16 << 20, 40960000]
+# the rest of the reference ladder (examples/benchmark/node/src/main.rs:11-21): sizes the
+# reference sends inline (< 4096 B, DataMessage::Vec); a device node sends them in slots too
+LADDER_SMALL = [0, 8, 64, 512, 2048]
 
 
 def parse():
@@ -521,8 +524,11 @@ def main():
             device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
             ladder_bufs[size] = b
         stream.sync()
+        for size in LADDER_SMALL:  # prefixes of the 4 KB payload
+            ladder_bufs[size] = ladder_bufs[4096]
+        sizes = LADDER_SMALL + LADDER
         # every size once through the path untimed first (its slot, the sink's mapping of it)
-        for size in LADDER:
+        for size in sizes:
             for _ in range(2):
                 node.send_output_device_bytes("throughput", ladder_bufs[size].ptr, size,
                                               {"seq": seq})
@@ -530,7 +536,7 @@ def main():
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
         wait_ack(seq)
         seq += 1
-        for size in LADDER:
+        for size in sizes:
             for _ in range(args.lat_n):
                 node.send_output_device_bytes("latency", ladder_bufs[size].ptr, size,
                                               {"seq": seq, "t_start": time.time_ns()})
@@ -539,13 +545,13 @@ def main():
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
         wait_ack(seq)
         seq += 1
-        for b in ladder_bufs.values():
+        for b in {id(b): b for b in ladder_bufs.values()}.values():
             b.free()
 
     # ---- throughput ladder (reference throughput mode: back-to-back messages per size) ----
     tp_ladder = {}
     if not args.no_ladder and args.tp_n > 0 and args.workload == "c2":
-        for size in LADDER:
+        for size in [z for z in LADDER_SMALL if z] + LADDER:
             nb = max(1, min(16, (640 << 20) // size))
             bufs = [device.DeviceBuffer(size) for _ in range(nb)]
             for b in bufs:
