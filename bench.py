@@ -133,11 +133,11 @@ def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
 
 
 def aql_kernel_name(workload: str, body: int) -> str:
-    """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*:
-    8 loads in flight per lane for 8-32 MB bodies, else 4; one segment at offset 0 -> pack1)."""
+    """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*: 4
+    loads in flight per lane unless DORA_GPU_PACK_VARIANT says u8; one segment at offset 0 ->
+    pack1)."""
     v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
-    u = 8 if v.startswith("u8") else 4 if v.startswith("u4") else (
-        8 if (8 << 20) <= body < (32 << 20) else 4)
+    u = 8 if v.startswith("u8") else 4
     return f"dora_aql_pack{'1' if workload == 'c2' else ''}_u{u} (AQL)"
 
 

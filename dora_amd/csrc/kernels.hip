@@ -145,6 +145,13 @@ uint64_t xseg_elems(const Segment& s) {
   return s.op == SEG_REBASE32 ? s.len / 4 : s.op == SEG_REBASE64 ? s.len / 8 : s.len;
 }
 
+// Loads in flight per lane: 4 at every size.  r01's isolated-pack probes preferred 8 loads over
+// 32 KiB chunks for 8-32 MB bodies; under the node's overlapping AQL packs (line-aligned chunks,
+// no release fence) 4 loads over 8 KiB chunks are faster there: C3 4.70-4.91 -> 4.56 us per
+// cloud, a flat 13 MB pack 4.81-4.91 -> 4.33-4.37 us, 16 MB unchanged
+// (profiles/r02_u4_mid_ab.jsonl, r02_c3_final_knobs_ab.jsonl).
+int default_unroll(uint64_t) { return 4; }
+
 uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
   if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
@@ -153,7 +160,8 @@ uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   }
   // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
   // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
-  // 8-32 MB prefers 32 KiB x 8 loads; below that ~2k workgroups of >= 8 KiB.
+  // 8-32 MB preferred 32 KiB x 8 loads in isolation (the 8-load variant's chunk, kept for the
+  // tuning knob); below that ~2k workgroups of >= 8 KiB.
   constexpr uint64_t kGrain = 8192;
   if (body_bytes >= (32u << 20)) return kGrain;
   if (unroll == 8) return 32768;
@@ -283,7 +291,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     const size_t m = std::min<size_t>(kMaxSegs, n - i);
     for (size_t k = 0; k < m; ++k) body += segs[i + k].len;
     Variant var = pack_variant();
-    if (var.unroll == 0) var.unroll = (body >= (8u << 20) && body < (32u << 20)) ? 8 : 4;
+    if (var.unroll == 0) var.unroll = default_unroll(body);
     a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
     uint64_t chunks = 0;
     for (size_t k = 0; k < m; ++k) {
@@ -425,7 +433,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
     body += segs[k].len;
   }
   Variant var = pack_variant();
-  if (var.unroll == 0) var.unroll = (body >= (8u << 20) && body < (32u << 20)) ? 8 : 4;
+  if (var.unroll == 0) var.unroll = default_unroll(body);
   a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
   uint64_t chunks = 0;
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
@@ -460,7 +468,7 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
     return fail(DORA_ERR_INVALID, "AQL single-segment pack: segment at offset %llu",
                 (unsigned long long)sg.dst_off);
   Variant var = pack_variant();
-  if (var.unroll == 0) var.unroll = (sg.len >= (8u << 20) && sg.len < (32u << 20)) ? 8 : 4;
+  if (var.unroll == 0) var.unroll = default_unroll(sg.len);
   const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, var.unroll);
   const uint64_t chunks =
       segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, sg.len, chunk_bytes);
