@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "common.h"
+#include "subprof.h"
 
 extern "C" const char dora_aql_code_object[];
 extern "C" const char dora_aql_code_object_end[];
@@ -341,6 +342,7 @@ void aql_forget_flags(int device, const void* base, size_t size) {
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
+  SubSpan sp_all(SP_AQL_PACK);
   std::lock_guard<std::mutex> g(a->mu);
   // the argument slot of the dispatch kRingSlots back must have completed
   const uint64_t r = a->next % kRingSlots;
@@ -355,6 +357,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
       }
     }
   }
+  SubSpan sp_args(SP_AQL_ARGS);
   uint8_t args[kSlotBytes];
   uint32_t grid = 0;
   int unroll = 4;
@@ -397,6 +400,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
   // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
   // the barrier; profiles/r02_aql_big_ab.jsonl).  Smaller packs overlap freely on all queues.
+  sp_args.stop();
+  SubSpan sp_disp(SP_AQL_DISPATCH);
   static const uint64_t barrier_bytes = [] {
     const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
     return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;

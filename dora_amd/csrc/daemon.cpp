@@ -34,6 +34,7 @@
 #include "interdaemon.h"
 #include "dora_gpu.h"
 #include "shm.h"
+#include "subprof.h"
 #include "trace.h"
 #include "wire.h"
 
@@ -384,6 +385,7 @@ class Daemon {
   }
 
   void handle(int i, uint32_t kind, const std::vector<uint8_t>& payload) {
+    SubSpan sp(SP_DAEMON_ROUTE);
     RBuf r(payload);
     switch (kind) {
       case REQ_SUBSCRIBE:
@@ -458,10 +460,10 @@ class Daemon {
       for (const Receiver& rc : it->second) {
         DNode& rn = nodes_[rc.node];
         if (!rn.subscribed || rn.done || !rn.open_inputs.count(rc.input)) continue;
-        ev_buf_.b.clear();
+        ev_buf_.clear();
         ev_buf_.str(rc.input);
         ev_buf_.raw(tail, tail_len);
-        push_event_raw(rc.node, EV_INPUT, ev_buf_.b.data(), ev_buf_.b.size());
+        push_event_raw(rc.node, EV_INPUT, ev_buf_.data(), ev_buf_.size());
         if (ti) {
           trace(TP_ROUTED, data.ipc.token);
           ti->add(rc.node);
@@ -515,12 +517,12 @@ class Daemon {
       w.raw(uid, kBcastIdBytes);
       w.u32(nranks);
       w.u32(k + 1);
-      push_event(members[k].node, EV_BCAST_JOIN, std::move(w.b));
+      push_event(members[k].node, EV_BCAST_JOIN, w.take());
     }
     WBuf a;
     a.str(output);
     a.u32(nranks);
-    push_drop_record(i, DROP_BCAST_GROUP, std::move(a.b));
+    push_drop_record(i, DROP_BCAST_GROUP, a.take());
   }
 
   void check_drop_token(const DropToken& t) {
@@ -550,7 +552,7 @@ class Daemon {
       if (!rn.open_inputs.erase(rc.input)) continue;
       WBuf w;
       w.str(rc.input);
-      push_event(rc.node, EV_INPUT_CLOSED, std::move(w.b));
+      push_event(rc.node, EV_INPUT_CLOSED, w.take());
       if (rn.open_inputs.empty() && !rn.all_closed_sent) {
         rn.all_closed_sent = true;
         push_event(rc.node, EV_ALL_INPUTS_CLOSED, {});

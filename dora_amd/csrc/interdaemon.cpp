@@ -45,7 +45,7 @@ void encode_ide(const InterDaemonEvent& e, std::vector<uint8_t>& out) {
     w.u32(static_cast<uint32_t>(e.outputs.size()));
     for (const auto& o : e.outputs) w.str(o);
   }
-  out.swap(w.b);
+  out = w.take();
 }
 
 InterDaemonEvent decode_ide(const uint8_t* p, size_t n) {

@@ -154,10 +154,13 @@ int default_unroll(uint64_t) { return 4; }
 
 uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
-  if (const char* e = std::getenv("DORA_GPU_PACK_CHUNK")) {
-    uint64_t v = std::strtoull(e, nullptr, 10);
-    if (v >= kLine && v % kLine == 0 && v <= (1u << 30)) return static_cast<uint32_t>(v);
-  }
+  // read once: getenv scans the environment (~0.1 us per send on the AQL path)
+  static const uint32_t env_chunk = [] {
+    const char* e = std::getenv("DORA_GPU_PACK_CHUNK");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v >= kLine && v % kLine == 0 && v <= (1u << 30) ? static_cast<uint32_t>(v) : 0u;
+  }();
+  if (env_chunk) return env_chunk;
   // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
   // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
   // 8-32 MB preferred 32 KiB x 8 loads in isolation (the 8-load variant's chunk, kept for the

@@ -14,7 +14,9 @@
 //   is reported when the last reference to the input data is released, after the node's stream
 //   has drained, so the owner can reuse the slot.
 #include <hip/hip_runtime_api.h>
+#include <pthread.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -40,6 +42,7 @@
 #include "plan.h"
 #include "shm.h"
 #include "stdout_capture.h"
+#include "subprof.h"
 #include "trace.h"
 #include "wire.h"
 
@@ -108,6 +111,20 @@ struct Slot {
 // Async sends (default): the sender records the slot's interprocess event after the pack and
 // sends at once; the receiver waits on that event before handing the input out.  Sync sends
 // synchronise the node stream before the descriptor leaves (DORA_GPU_SEND_MODE=sync).
+// getpid() is a system call on current glibc; the descriptor path asks for it per message.
+// Cached per process, refreshed in a forked child.
+int self_pid() {
+  static std::atomic<int> pid{0};
+  static std::once_flag once;
+  std::call_once(once, [] { pthread_atfork(nullptr, nullptr, [] { pid.store(0); }); });
+  int p = pid.load(std::memory_order_relaxed);
+  if (!p) {
+    p = static_cast<int>(getpid());
+    pid.store(p, std::memory_order_relaxed);
+  }
+  return p;
+}
+
 bool async_sends() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_SEND_MODE");
@@ -529,10 +546,12 @@ struct InputData {
     }
     if (has_token || local) {
       // consumer reads on the node stream must be complete before the memory is reused
+      SubSpan sq(SP_STREAM_QUERY);
       if (core->stream && hipStreamQuery(core->stream) != hipSuccess)
         (void)hipStreamSynchronize(core->stream);
     }
     if (has_token) {
+      SubSpan sp(SP_RECV_RELEASE);
       core->report_drop_token(token);
       trace(TP_RELEASED, token);
     }
@@ -580,12 +599,16 @@ struct dora_node {
   std::string id;
   std::set<std::string> outputs;
   std::map<std::string, uint32_t> queue_size;
+  size_t min_queue_size = 0;  // smallest value of queue_size
   std::deque<dora::Slot*> cache;
   // samples sent, by drop token (map nodes from a pool: no malloc per send)
   std::pmr::unsynchronized_pool_resource sent_pool;
   std::pmr::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out{&sent_pool};
   dora::WBuf send_buf;                 // request encoding scratch of send_sample, reused
   std::vector<uint8_t> ti_buf;         // type-info scratch of pack_and_send, reused
+  dora_plan bytes_plan;                // send_output_bytes: the one-buffer plan, re-pointed
+  std::vector<uint8_t> bytes_ti;       // ... and its type info for a sample of bytes_ti_len
+  uint64_t bytes_ti_len = 0;
   std::deque<std::unique_ptr<dora_event>> queue;
   bool ended = false;
   // profiling of the pack kernel on the node stream
@@ -734,6 +757,9 @@ void on_token(dora_node* n, const DropToken& t) {
   if (it == n->sent_out.end()) return;  // "received unknown finished drop token"
   Slot* s = it->second;
   n->sent_out.erase(it);
+  // the slot's fill flag line was last written by the GPU: start pulling it in now, so the
+  // last-fill check of its reuse (allocate_slot, oldest first) finds it in cache
+  if (s->flag >= 0) _mm_prefetch(reinterpret_cast<const char*>(n->core->flag_host(s->flag)), _MM_HINT_T0);
   add_to_cache(n, s);
 }
 
@@ -757,16 +783,24 @@ uint64_t slot_bytes(uint64_t len) {
 }
 
 int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
-  // best fit among cached slots, iterating newest-first like `.rev()...min_by_key`
+  // best fit among cached slots (mod.rs:321-346 `.rev()...min_by_key`); among slots of equal
+  // capacity the oldest returned one, whose last fill has had the longest to complete and whose
+  // flag line on_token has prefetched (the reference takes the newest; any fit is equivalent)
   int best = -1;
-  for (int i = static_cast<int>(n->cache.size()) - 1; i >= 0; --i) {
+  for (int i = 0; i < static_cast<int>(n->cache.size()); ++i) {
     Slot* s = n->cache[static_cast<size_t>(i)];
-    if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) best = i;
+    if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) {
+      best = i;
+      if (s->cap == len) break;  // an exact fit: no later slot fits better
+    }
   }
   if (best >= 0) {
     Slot* s = n->cache[static_cast<size_t>(best)];
     n->cache.erase(n->cache.begin() + best);
-    if (wait_slot_idle(n, s)) {
+    SubSpan sp_flag(SP_SLOT_FLAG);
+    const bool idle = wait_slot_idle(n, s);
+    sp_flag.stop();
+    if (idle) {
       *out = s;
       ++n->cache_hits;
       return DORA_OK;
@@ -871,6 +905,7 @@ int post_bcast_receive(NodeCore* c, InputData* in, const std::string& input) {
 }
 
 void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
+  SubSpan sp(SP_RECV_ENCODE);
   auto ev = std::make_unique<dora_event>();
   RBuf r(p);
   switch (kind) {
@@ -904,7 +939,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
             ev->error = dora_gpu_last_error();
             in->ptr = nullptr;
           }
-        } else if (d.ipc.owner_pid == getpid()) {
+        } else if (d.ipc.owner_pid == self_pid()) {
           std::lock_guard<std::mutex> g(own_slots().mu);
           auto it = own_slots().ptrs.find(d.ipc.slot_id);
           if (it != own_slots().ptrs.end()) base = it->second;
@@ -982,6 +1017,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
 // local receive slot with one peer copy and return the producer's token at once.
 void finish_input(dora_node* n, dora_event* ev) {
   if (!ev->pending) return;
+  SubSpan sp(SP_RECV_FINISH);
   ev->pending = false;
   InputData* in = ev->data.get();
   const DeviceIpc& d = ev->ipc;
@@ -1141,6 +1177,10 @@ int ensure_local(InputData* in) {
 
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
 void drop_oldest_inputs(dora_node* n) {
+  // no input can exceed its queue size while the whole queue holds no more events than the
+  // smallest one (the common case of a receiver keeping up): nothing to count
+  if (n->queue_size.empty() || n->queue.size() <= n->min_queue_size) return;
+  SubSpan sp(SP_RECV_DROPOLD);
   std::map<std::string, uint32_t> remaining = n->queue_size;
   for (auto it = n->queue.rbegin(); it != n->queue.rend(); ++it) {
     dora_event* e = it->get();
@@ -1164,6 +1204,7 @@ void drop_oldest_inputs(dora_node* n) {
 void drain_events(dora_node* n) {
   uint32_t kind;
   std::vector<uint8_t>& p = n->ev_buf;  // reused across events
+  SubSpan sp(SP_RECV_DRAIN);
   bool got = false;
   while (n->core->ev.try_pop(&kind, &p)) {
     encode_event(n, kind, p);
@@ -1187,7 +1228,11 @@ void put_metadata(WBuf& w, const std::vector<uint8_t>& ti, const uint8_t* params
 int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
                 const uint8_t* params, size_t params_len, dora_sample* sample,
                 DropToken* token_out = nullptr, uint64_t ts_override = 0) {
-  handle_finished_drop_tokens(n);
+  {
+    SubSpan sp(SP_SEND_TOKENS);
+    handle_finished_drop_tokens(n);
+  }
+  SubSpan sp_lookup(SP_SEND_LOOKUP);
   if (!n->outputs.count(output_id)) {
     delete sample;  // the sample is consumed either way
     return fail(DORA_ERR_NOT_FOUND,
@@ -1197,6 +1242,8 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
   }
   // Metadata::from_parameters(clock.new_timestamp(), ..) mod.rs:258; a proxy of a remote
   // node keeps the producer's timestamp (the inter-daemon message's metadata)
+  sp_lookup.stop();
+  SubSpan sp_req(SP_SEND_REQUEST);
   const uint64_t ts = ts_override ? ts_override : now_ns();
   DataMsg d;
   Slot* slot = nullptr;
@@ -1206,7 +1253,7 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.kind = DATA_DEVICE_IPC;
       std::memcpy(d.ipc.handle, &slot->handle, 64);
       d.ipc.device = n->core->device;
-      d.ipc.owner_pid = getpid();
+      d.ipc.owner_pid = self_pid();
       d.ipc.slot_id = slot->id;
       d.ipc.offset = 0;
       d.ipc.len = sample->len;
@@ -1247,15 +1294,17 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     delete sample;
   }
   WBuf& w = n->send_buf;
-  w.b.clear();
+  w.clear();
   w.str(output_id);
   put_metadata(w, ti, params, params_len, ts);
   w.data(d);
-  int rc = n->core->request(REQ_SEND_MESSAGE, w.b);
+  int rc = n->core->request(REQ_SEND_MESSAGE, w.data(), w.size());
+  sp_req.stop();
   if (rc != DORA_OK) {
     if (slot) add_to_cache(n, slot);
     return rc;
   }
+  SubSpan sp_track(SP_SEND_TRACK);
   if (slot) {
     n->sent_out[d.ipc.token] = slot;
     if (token_out) *token_out = d.ipc.token;
@@ -1282,8 +1331,10 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
     *out = s;
     return DORA_OK;
   }
+  SubSpan sp_new(SP_SAMPLE_NEW);
   auto* s = new dora_sample();
   s->len = len;
+  sp_new.stop();
   if (len > 0) {
     if (!n->aql_ready) {
       // the first non-empty sample of this node sets up the process's AQL queues and loads the
@@ -1292,12 +1343,15 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
       n->aql_ready = true;
       (void)aql_queue(n->core->device);
     }
+    SubSpan sp_tok(SP_ALLOC_TOKENS);
     handle_finished_drop_tokens(n);
+    sp_tok.stop();
     // Async sends run ahead of the GPU; bound the samples in flight so the sender waits for a
     // returned slot instead of hipMalloc-ing new ones (a device slot costs far more to create
     // than a shm region).
     // After `slot_wait_ns` without a returned token the slot is allocated anyway, as the
     // reference would (a receiver may legitimately hold many inputs).
+    SubSpan sp_wait(SP_ALLOC_WAIT);
     const uint64_t t0 = mono_ns();
     while (async_sends() && n->sent_out.size() >= max_in_flight(len) &&
            mono_ns() - t0 < slot_wait_ns()) {
@@ -1305,7 +1359,9 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
       handle_finished_drop_tokens(n);
       if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
     }
+    sp_wait.stop();
     s->ext_len = std::max(len, ext_len);
+    SubSpan sp_slot(SP_ALLOC_SLOT);
     int rc = allocate_slot(n, s->ext_len, &s->slot);
     if (rc != DORA_OK) {
       delete s;
@@ -1414,7 +1470,10 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   if (sp && !st && !t_start && !t_stop && dev == ARROW_DEVICE_ROCM &&
       nseg <= aql_max_segments() && std::max(s->len, s->ext_len) < aql_max_bytes() &&
       std::all_of(segs, segs + nseg, [](const Segment& g) { return g.op == SEG_COPY; }) &&
-      hipStreamQuery(n->core->stream) != hipErrorNotReady) {
+      [&] {
+        SubSpan sq(SP_STREAM_QUERY);
+        return hipStreamQuery(n->core->stream) != hipErrorNotReady;
+      }()) {
     // host-bound size: one raw AQL packet instead of hipLaunchKernel (aql.h)
     if (AqlQueue* q = aql_queue(n->core->device)) {
       const std::atomic<uint64_t>* fh = n->core->flag_host(s->slot->flag);
@@ -1480,11 +1539,11 @@ int forward_in_place(dora_node* n, const char* output_id, const dora_event* ev,
   d.ipc.flag_node = d.ipc.flag_index = 0;
   d.ipc.epoch = 0;
   WBuf& w = n->send_buf;
-  w.b.clear();
+  w.clear();
   w.str(output_id);
   put_metadata(w, ev->meta.type_info, params, params_len, now_ns());
   w.data(d);
-  int rc = n->core->request(REQ_SEND_MESSAGE, w.b);
+  int rc = n->core->request(REQ_SEND_MESSAGE, w.data(), w.size());
   if (rc != DORA_OK) return rc;
   n->forwarded[d.ipc.token] = ev->data;
   ++n->zero_copy_forwards;
@@ -1561,7 +1620,7 @@ void form_bcast_groups(dora_node* n) {
     WBuf w;
     w.str(o);
     w.raw(uid, sizeof(uid));
-    if (c->request(REQ_BCAST_GROUP, w.b) != DORA_OK) return;
+    if (c->request(REQ_BCAST_GROUP, w.data(), w.size()) != DORA_OK) return;
     uint32_t nranks = 0;
     bool answered = false;
     const uint64_t t0 = mono_ns();
@@ -1643,13 +1702,13 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     }
     t2 = t3 = mono_ns();
   }
-  std::vector<uint8_t>& ti = n->ti_buf;
-  if (ti_pre) {
-    ti.assign(ti_pre->begin(), ti_pre->end());
-  } else {
-    ti.clear();
-    serialize_type_info(plan->root, ti);
+  SubSpan sp_ti(SP_SEND_TI);
+  if (!ti_pre) {
+    n->ti_buf.clear();
+    serialize_type_info(plan->root, n->ti_buf);
   }
+  const std::vector<uint8_t>& ti = ti_pre ? *ti_pre : n->ti_buf;
+  sp_ti.stop();
   DropToken tok{};
   const bool traced = trace_enabled() && s->slot;
   rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
@@ -1764,6 +1823,8 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     auto eq = kv.find('=');
     n->queue_size[kv.substr(0, eq)] = static_cast<uint32_t>(std::stoul(kv.substr(eq + 1)));
   }
+  n->min_queue_size = SIZE_MAX;
+  for (auto& kv : n->queue_size) n->min_queue_size = std::min<size_t>(n->min_queue_size, kv.second);
   const char* prof = std::getenv("DORA_GPU_PROFILE_PACK");
   if (prof && *prof && *prof != '0' && device >= 0)
     n->profile = dora::ensure_timing(n) == DORA_OK;
@@ -1830,7 +1891,7 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   dora::WBuf w;
   w.u32(static_cast<uint32_t>(outs.size()));
   for (auto& o : outs) w.str(o);
-  (void)n->core->request(dora::REQ_CLOSE_OUTPUTS, w.b);
+  (void)n->core->request(dora::REQ_CLOSE_OUTPUTS, w.data(), w.size());
   n->queue.clear();  // releases undelivered inputs (tokens reported)
   uint64_t t0 = dora::mono_ns();
   while (!n->sent_out.empty() || !n->forwarded.empty()) {
@@ -1993,18 +2054,29 @@ int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void*
                                 size_t params_len) {
   if (!n || !output_id || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
-  dora_plan plan;
-  plan.dev = device_type;
-  plan.size = len;
-  {
+  dora::SubSpan sp(dora::SP_SEND_PLAN);
+  // one UInt8 buffer: the plan and its type info are built once per node and re-pointed per send
+  dora_plan& plan = n->bytes_plan;
+  if (n->bytes_ti.empty()) {
     ArrowSchema u8{};
     u8.format = "C";
     dora::serialize_schema(&u8, true, plan.root.schema);
+    plan.root.bufs.assign(1, {0, 0});
   }
+  plan.dev = device_type;
+  plan.size = len;
   plan.root.len = len;
-  plan.root.bufs.push_back({0, len});
+  plan.root.bufs[0] = {0, len};
+  plan.segs.clear();
   if (len) plan.segs.push_back({data, 0, len});
-  return dora::pack_and_send(n, output_id, &plan, params, params_len);
+  // the type info depends on len only through the buffer length: re-serialize when it changes
+  if (n->bytes_ti.empty() || n->bytes_ti_len != len) {
+    n->bytes_ti.clear();
+    dora::serialize_type_info(plan.root, n->bytes_ti);
+    n->bytes_ti_len = len;
+  }
+  sp.stop();
+  return dora::pack_and_send(n, output_id, &plan, params, params_len, &n->bytes_ti);
   DORA_GUARD_END
 }
 
@@ -2025,7 +2097,7 @@ int dora_node_close_outputs(dora_node* n, const char* const* ids, size_t count) 
     n->outputs.erase(ids[i]);
     w.str(ids[i]);
   }
-  return n->core->request(dora::REQ_CLOSE_OUTPUTS, w.b);
+  return n->core->request(dora::REQ_CLOSE_OUTPUTS, w.data(), w.size());
   DORA_GUARD_END
 }
 

@@ -54,9 +54,9 @@ void send_batch(StdoutCapture* c, const std::string& text) {
   m.metadata(md);
   WBuf w;
   w.str(c->output);
-  w.bytes(m.b);
+  w.bytes(m.data(), m.size());
   w.data(d);
-  (void)c->request(REQ_SEND_MESSAGE, w.b);
+  (void)c->request(REQ_SEND_MESSAGE, w.take());
 }
 
 bool tracing_output(const std::string& s) {

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "shm.h"
+#include "subprof.h"
 
 namespace dora {
 namespace {
@@ -75,5 +76,53 @@ void trace_at(TracePoint p, const DropToken& t, uint64_t t_ns) {
 void trace_set_name(const std::string& who) { tracer().who = who; }
 
 void trace_flush() { tracer().flush(); }
+
+namespace {
+
+const char* const kSubNames[SP_COUNT] = {
+    "send_plan",    "alloc_tokens", "alloc_wait",   "alloc_slot",    "stream_query",
+    "aql_pack",     "aql_args",     "aql_dispatch", "send_ti",       "send_tokens",
+    "send_lookup",  "send_request", "send_track",   "recv_drain",    "recv_encode",
+    "recv_dropold", "recv_finish",  "recv_release", "daemon_route",  "slot_flag",
+    "sample_new"};
+
+struct SubProf {
+  const bool on = g_subprof_on;
+  std::atomic<uint64_t> ticks[SP_COUNT] = {};
+  std::atomic<uint64_t> calls[SP_COUNT] = {};
+  uint64_t tsc0 = __rdtsc(), ns0 = mono_ns();
+  ~SubProf() {
+    if (!on) return;
+    const double ns_per_tick = double(mono_ns() - ns0) / double(__rdtsc() - tsc0);
+    std::fprintf(stderr, "{\"subphases\": {");
+    bool first = true;
+    for (int k = 0; k < SP_COUNT; ++k) {
+      const uint64_t c = calls[k].load();
+      if (!c) continue;
+      std::fprintf(stderr, "%s\"%s\": [%.1f, %llu]", first ? "" : ", ", kSubNames[k],
+                   double(ticks[k].load()) * ns_per_tick / double(c), (unsigned long long)c);
+      first = false;
+    }
+    std::fprintf(stderr, "}, \"pid\": %d}\n", int(getpid()));
+  }
+};
+
+SubProf& subprof() {
+  static SubProf p;
+  return p;
+}
+
+}  // namespace
+
+const bool g_subprof_on = [] {
+  const char* e = std::getenv("DORA_GPU_SUBPHASES");
+  return e && *e && *e != '0';
+}();
+
+void subprof_add(int phase, uint64_t ticks) {
+  SubProf& p = subprof();
+  p.ticks[phase].fetch_add(ticks, std::memory_order_relaxed);
+  p.calls[phase].fetch_add(1, std::memory_order_relaxed);
+}
 
 }  // namespace dora

@@ -4,6 +4,7 @@
 // (node_to_daemon.rs:9-69, daemon_to_node.rs:48-77).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -84,17 +85,28 @@ struct Metadata {
   std::vector<uint8_t> parameters;  // BTreeMap<String, Parameter> encoding (node.cpp)
 };
 
+// Encoder.  Tracks its own length over storage that only grows: a send encodes ~25 fields, and
+// std::vector bookkeeping per field cost ~190 ns per message against ~20 ns for plain copies.
 class WBuf {
  public:
-  std::vector<uint8_t> b;
-  void u8(uint8_t v) { b.push_back(v); }
+  void clear() { n_ = 0; }
+  const uint8_t* data() const { return buf_.data(); }
+  size_t size() const { return n_; }
+  // The encoded bytes as a vector (the storage moves out; the buffer is empty afterwards).
+  std::vector<uint8_t> take() {
+    buf_.resize(n_);
+    n_ = 0;
+    return std::move(buf_);
+  }
+  void u8(uint8_t v) { raw(&v, 1); }
   void u16(uint16_t v) { raw(&v, 2); }
   void u32(uint32_t v) { raw(&v, 4); }
   void u64(uint64_t v) { raw(&v, 8); }
   void i32(int32_t v) { raw(&v, 4); }
   void raw(const void* p, size_t n) {
-    const auto* c = static_cast<const uint8_t*>(p);
-    b.insert(b.end(), c, c + n);
+    if (buf_.size() - n_ < n) buf_.resize(std::max(2 * buf_.size(), n_ + n + 256));
+    if (n) std::memcpy(buf_.data() + n_, p, n);
+    n_ += n;
   }
   void bytes(const uint8_t* p, size_t n) {
     u64(n);
@@ -102,6 +114,7 @@ class WBuf {
   }
   void bytes(const std::vector<uint8_t>& v) { bytes(v.data(), v.size()); }
   void str(const std::string& s) { bytes(reinterpret_cast<const uint8_t*>(s.data()), s.size()); }
+  void str(const char* s) { bytes(reinterpret_cast<const uint8_t*>(s), std::strlen(s)); }
   void token(const DropToken& t) { raw(t.b, 16); }
   void data(const DataMsg& d) {
     u8(d.kind);
@@ -131,6 +144,10 @@ class WBuf {
     bytes(m.type_info);
     bytes(m.parameters);
   }
+
+ private:
+  std::vector<uint8_t> buf_;
+  size_t n_ = 0;
 };
 
 class RBuf {

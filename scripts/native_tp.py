@@ -44,6 +44,14 @@ def main():
                     dstat = json.loads(line)
                 except ValueError:
                     pass
+        sub = {}
+        for who in ("source", "sink1", "_daemon"):
+            for line in (df.log(who) or "").splitlines():
+                if line.startswith('{"subphases"'):
+                    try:
+                        sub[who] = json.loads(line)["subphases"]
+                    except ValueError:
+                        pass
         print(json.dumps({"size": size, "n": a.n, "GBps": r.get("tp_delivered_GBps"),
                           "us_per_msg": round(size / (r["tp_delivered_GBps"] * 1e3), 3)
                           if r.get("tp_delivered_GBps") else None,
@@ -55,6 +63,7 @@ def main():
                               "sink_next_event": sink.get("next_event_us"),
                               "sink_free": sink.get("free_us"),
                               "daemon_per_routed": dstat.get("busy_us_per_routed")},
+                          "subphases_ns": sub or None,
                           "exit_codes": codes, "env": env}), flush=True)
 
 
