@@ -290,13 +290,21 @@ SINK_ENV = {k[len("DORA_BENCH_SINK_"):]: v for k, v in os.environ.items()
             if k.startswith("DORA_BENCH_SINK_DORA_")}
 
 
-def run_native_ladder(launcher, gpu, n=1000, timeout=120.0):
+def native_ladder_msgs(size):
+    """Messages per size of the native ladder: >= ~20 ms of back-to-back traffic, so one host
+    hiccup does not set the rate (1000 x 4 KB took ~1 ms and varied 1.0-1.7 us per message)."""
+    return 20000 if size <= 4096000 else 3000 if size <= (16 << 20) else 1000
+
+
+def run_native_ladder(launcher, gpu, n=None, timeout=120.0):
     """Throughput mode of the native benchmark node (dora-gpu-bench-source -> -sink, one GPU,
     zero-copy edge) per size: the data plane through its C ABI, as a Rust node would bind it,
     without the Python node's per-send cost.  Reported, never raised."""
     from dora_amd.dataflow import Dataflow
     out = {}
+    n_fixed = n
     for size in NATIVE_SIZES:
+        n = n_fixed or native_ladder_msgs(size)
         tmp = tempfile.mkdtemp(prefix="dora-native-")
         try:
             desc = c4_descriptor(2, tmp, "kernel", tp_n=n, gpu=lambda g: gpu)

@@ -315,9 +315,19 @@ struct NodeCore {
   std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>> flag_pending;
   std::vector<uint8_t> fill_unsignalled;  // per fill stream: work not covered by a fill flag
 
+  // One entry per fill flag with the latest epoch ordered on it (a flag's epochs only grow, so
+  // waiting for the latest covers the earlier ones).  Matching by pointer reads no flag: the
+  // flags are host lines the GPU writes, and pruning by loading them cost a cache miss each
+  // (64 per prune, ~0.4 us per send amortised over the two lists).  The list stays as long as
+  // the node has slots with flags; only past 256 entries are completed ones pruned.
   static void note(std::vector<std::pair<const std::atomic<uint64_t>*, uint64_t>>& v,
                    const std::atomic<uint64_t>* f, uint64_t epoch) {
-    if (v.size() >= 64) {
+    for (auto& x : v)
+      if (x.first == f) {
+        x.second = std::max(x.second, epoch);
+        return;
+      }
+    if (v.size() >= 256) {
       size_t k = 0;
       for (auto& x : v)
         if (x.first->load(std::memory_order_acquire) < x.second) v[k++] = x;
