@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--lat-gap-us", type=int, default=1000)
     ap.add_argument("--no-ladder", action="store_true")
     ap.add_argument("--tp-n", type=int, default=200,
-                    help="throughput ladder: back-to-back messages per size (0: skip)")
+                    help="throughput ladder: back-to-back messages per size, at least 2000 up "
+                         "to 4 MiB (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
     ap.add_argument("--c3-lists", type=int, default=0,
@@ -565,15 +566,18 @@ def main():
             for b in bufs:
                 device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
             stream.sync()
-            for k in range(8):  # warm the slot cache for this size
+            for k in range(24):  # warm the slot cache for this size (2x the in-flight cap)
                 node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, {"seq": seq})
                 seq += 1
             node.send_output("throughput", b"", {"seq": seq, "ack": True})
             wait_ack(seq)
             seq += 1
             d0 = node.dataflow_counters("sink")["dropped_inputs"]
+            # small sizes run ~1-2 us per message: >= 2000 of them, so a host hiccup does not
+            # set the rate of a ~0.3 ms burst
+            tp_n = args.tp_n if size > (4 << 20) else max(args.tp_n, 2000)
             t_a = time.perf_counter()
-            for k in range(args.tp_n):
+            for k in range(tp_n):
                 node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, {"seq": seq})
                 seq += 1
             node.send_output("throughput", b"", {"seq": seq, "ack": True})
@@ -583,7 +587,7 @@ def main():
             # the sink's queue (queue_size 10, the reference default) may drop inputs when it
             # falls behind: only delivered messages count
             dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
-            got = args.tp_n - dropped
+            got = tp_n - dropped
             tp_ladder[str(size)] = {"GBps": round(got * size / dt / 1e9, 2),
                                     "msgs_per_s": round(got / dt, 1),
                                     "us_per_msg": round(dt / got * 1e6, 2),

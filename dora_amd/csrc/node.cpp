@@ -94,7 +94,11 @@ constexpr uint64_t kDropWaitNs = 10000000000;  // 10 s per token on drop (mod.rs
 
 struct Slot {
   void* ptr = nullptr;
-  uint64_t cap = 0;  // requested length (cache best-fit key, like Shmem::len)
+  // bytes the slot holds (its whole 2 MiB-grain allocation): the cache's best-fit key.  The
+  // reference keys on the requested length (Shmem::len); a slot's full capacity lets a 4 MiB
+  // sample reuse a slot first made for 4,096,000 B (the ladder's next size created fresh slots,
+  // hipMalloc + export + the receiver's mapping, for ~20 of its sends).
+  uint64_t cap = 0;
   uint64_t id = 0;
   hipIpcMemHandle_t handle;
   int flag = -1;              // FillFlag index in the node's region entry (async sends)
@@ -797,11 +801,12 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   // capacity the oldest returned one, whose last fill has had the longest to complete and whose
   // flag line on_token has prefetched (the reference takes the newest; any fit is equivalent)
   int best = -1;
+  const uint64_t need = slot_bytes(len);  // the smallest capacity a slot can have
   for (int i = 0; i < static_cast<int>(n->cache.size()); ++i) {
     Slot* s = n->cache[static_cast<size_t>(i)];
     if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) {
       best = i;
-      if (s->cap == len) break;  // an exact fit: no later slot fits better
+      if (s->cap == need) break;  // an exact fit: no later slot fits better
     }
   }
   if (best >= 0) {
@@ -822,7 +827,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
     own_slots().ptrs.erase(s->id);
   }
   auto* s = new Slot();
-  s->cap = len;
+  s->cap = slot_bytes(len);
   s->id = own_slots().next_id.fetch_add(1);
   hipError_t e = hipMalloc(&s->ptr, slot_bytes(len));
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);

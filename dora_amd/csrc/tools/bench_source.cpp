@@ -15,6 +15,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -64,6 +65,7 @@ std::vector<uint64_t> env_sizes(const char* k) {
 struct Source {
   void* ptr = nullptr;
   uint64_t csum = 0;
+  std::vector<void*> extra;  // DORA_BENCH_TP_SOURCES - 1 more copies the throughput mode rotates over
 };
 
 }  // namespace
@@ -85,6 +87,9 @@ int main() {
   dora_stream_t st = dora_node_stream(node);
   int errors = 0;
 
+  // throughput mode: rotating source copies, so the sources of a burst are not all served from the
+  // Infinity Cache (one resident source per size by default, as the reference node sends one Vec)
+  const long tp_sources = std::max(1L, env_long("DORA_BENCH_TP_SOURCES", 1));
   std::map<uint64_t, Source> src;
   std::vector<uint64_t> all = lat_sizes;
   if (tp_size) all.push_back(tp_size);
@@ -97,15 +102,25 @@ int main() {
                    dora_gpu_last_error());
       return 1;
     }
+    for (long k = 1; s == tp_size && k < tp_sources; ++k) {
+      void* p = nullptr;
+      if (dora_gpu_malloc(&p, s) != 0 || dora_gpu_fill_splitmix(p, s, 0xD05A + s, st) != 0) {
+        std::fprintf(stderr, "source: payload copy: %s\n", dora_gpu_last_error());
+        return 1;
+      }
+      x.extra.push_back(p);
+    }
   }
+  dora_gpu_stream_sync(st);
 
   int64_t seq = 0;
   // throughput-mode messages carry default parameters, like the reference node's
   // send_output_raw(.., Default::default(), ..): latency comes from the metadata timestamp
   auto send_plain = [&](const char* output, uint64_t size) {
-    ++seq;
-    if (dora_node_send_output_bytes(node, output, src[size].ptr, size, ARROW_DEVICE_ROCM, nullptr,
-                                    0) != 0) {
+    const Source& x = src[size];
+    const size_t k = static_cast<size_t>(seq++ % tp_sources);
+    const void* p = k == 0 ? x.ptr : x.extra[k - 1];
+    if (dora_node_send_output_bytes(node, output, p, size, ARROW_DEVICE_ROCM, nullptr, 0) != 0) {
       std::fprintf(stderr, "source: send failed: %s\n", dora_gpu_last_error());
       ++errors;
     }
@@ -214,7 +229,10 @@ int main() {
                (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str(),
                tp_n > 0 ? (tp_s * 1e9 - double(idle1 - idle0)) / 1e3 / double(tp_n) : 0.0);
   if (f != stdout) std::fclose(f);
-  for (auto& kv : src) dora_gpu_free(kv.second.ptr);
+  for (auto& kv : src) {
+    dora_gpu_free(kv.second.ptr);
+    for (void* p : kv.second.extra) dora_gpu_free(p);
+  }
   dora_node_free(node);
   return errors || !ok ? 1 : 0;
 }
