@@ -318,8 +318,14 @@ def run_native_ladder(launcher, gpu, n=None, timeout=120.0):
             finally:
                 df.stop()
             r = _load(os.path.join(tmp, "source.json")) or {}
+            sk = _load(os.path.join(tmp, "sink1.json")) or {}
             gbps = r.get("tp_delivered_GBps")
-            out[str(size)] = {"GBps": gbps, "msgs": n,
+            # the source counts messages sent; only delivered ones count (the sink's queue,
+            # queue_size 10, drops its oldest inputs when it falls behind — any phase)
+            dropped = sk.get("dropped_inputs", 0) or 0
+            if gbps and dropped:
+                gbps = round(gbps * (n - min(dropped, n - 1)) / n, 3)
+            out[str(size)] = {"GBps": gbps, "msgs": n, "sink_dropped": dropped,
                               "us_per_msg": round(size / (gbps * 1e3), 3) if gbps else None,
                               "hbm_frac_2S": round(2 * gbps / HBM_PEAK_GBPS, 4) if gbps else None,
                               "send_phase_us": r.get("send_phase_us"), "ok": r.get("ok"),

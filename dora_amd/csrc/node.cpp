@@ -143,15 +143,19 @@ constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
 // Samples a sender may have in flight (sent, token not back) before it waits for a returned
 // slot.  Below 8 MiB a message's life is dominated by the dispatch-to-fill-flag latency
 // (~5-8 us for a 4 KB-4 MB pack over the AQL queues, scripts/trace_report.py), so the pipeline
-// depth sets the rate: 12 there, 8 for larger samples, which are HBM-bound and lose to more
-// concurrent packs (C3, 13 MB: -20 % at 12).  DORA_GPU_MAX_IN_FLIGHT sets both.
+// depth sets the rate: 11 there, 8 for larger samples, which are HBM-bound and lose to more
+// concurrent packs (C3, 13 MB: -20 % at 12).  11 = the reference's default queue_size (10) + the
+// input a receiver holds: a receiver that pauses (a checksum, a host hiccup) then finds at most
+// 10 ready inputs queued and drops none (12 dropped one per pause; in-flight 12 vs 16-24 made
+// no difference to the 4 MB rate, profiles/r02_sweep_4mb_*.jsonl).  DORA_GPU_MAX_IN_FLIGHT sets
+// both.
 size_t max_in_flight(uint64_t len) {
   static const long env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
     return e ? std::atol(e) : 0L;
   }();
   if (env > 0) return static_cast<size_t>(env);
-  return len < kSmallInFlightBytes ? 12 : 8;
+  return len < kSmallInFlightBytes ? 11 : 8;
 }
 
 // Streams the sends of a node spread their fills over (DORA_GPU_FILL_STREAMS, default 3).  A
@@ -1190,6 +1194,20 @@ int ensure_local(InputData* in) {
   return DORA_OK;
 }
 
+// An input whose producer's fill is still running.  In the reference the sample is filled before
+// the message leaves the sender (send_output returns after the copy), so such an input would not
+// be queued here yet: the queue_size policy neither counts nor drops it.  Without this, an
+// async sender with more samples in flight than a receiver's queue_size (12 vs the default 10)
+// made the receiver drop inputs whenever it waited on the GPU: 20-25 % of a 1-4 MB burst from
+// the Python node (scripts/py_tp.py), inputs the reference would have delivered.
+bool fill_in_transit(dora_node* n, const dora_event* e) {
+  if (!e->pending || e->ipc.fill != FILL_FLAG) return false;
+  RegionHdr* h = n->core->region->hdr();
+  if (e->ipc.flag_node >= h->n_nodes || e->ipc.flag_index >= kFillFlags) return false;
+  return h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch.load(std::memory_order_acquire) <
+         e->ipc.epoch;
+}
+
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
 void drop_oldest_inputs(dora_node* n) {
   // no input can exceed its queue size while the whole queue holds no more events than the
@@ -1202,6 +1220,7 @@ void drop_oldest_inputs(dora_node* n) {
     if (!e || e->type != DORA_EVENT_INPUT) continue;
     auto q = remaining.find(e->id);
     if (q == remaining.end()) continue;
+    if (fill_in_transit(n, e)) continue;
     if (q->second == 0) {
       it->reset();  // releases the InputData -> drop token reported
       ++n->dropped_inputs;

@@ -63,6 +63,7 @@ def main():
                               "sink_next_event": sink.get("next_event_us"),
                               "sink_free": sink.get("free_us"),
                               "daemon_per_routed": dstat.get("busy_us_per_routed")},
+                          "sink_dropped": sink.get("dropped_inputs"),
                           "subphases_ns": sub or None,
                           "exit_codes": codes, "env": env}), flush=True)
 

@@ -459,6 +459,9 @@ def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
         node = Node("node", dataflow=df.shm, device=0)
         for k in range(n_msgs):
             node.send_output_device_bytes("data", bufs[k].ptr, size, {"seq": k})
+        # every fill complete before the receiver drains: the burst is fully "sent" in the
+        # reference's sense (an input whose fill still runs is not queued for the policy yet)
+        node.sync()
         sent.set()
         t_close = time.time()
         node_stats = node.stats()
@@ -476,6 +479,45 @@ def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
     assert got[0][2] == n_msgs - 2
     assert node_stats["slots_created"] + node_stats["cache_hits"] == n_msgs
     assert close_s < 5.0, close_s
+
+
+def test_default_queue_keeps_up_with_async_burst(launcher, tmp_path):
+    """A receiver with the reference's default queue_size (10) that keeps up with a back-to-back
+    burst drops nothing, although the sender keeps up to 12 samples in flight: inputs whose
+    fill is still running are not yet queued for the drop policy (the reference fills before
+    the message leaves the sender).  Every input is verified bit-exact."""
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    res = str(tmp_path / "sink.json")
+    n_msgs, size, nsrc = 2000, 4096000, 16
+    bufs, sums = _distinct_sources(nsrc, size)
+    warm = 40  # slots created and mapped (milliseconds each) before the burst
+    with Dataflow(_bench_desc(res, queue_size=10), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        for k in range(warm):
+            node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size, {"seq": k})
+        node.send_output("data", b"", {"seq": warm, "ack": True})
+        node.wait_input("ack", "seq", warm, 60.0)
+        d0 = node.dataflow_counters("sink")["dropped_inputs"]
+        for k in range(n_msgs):
+            meta = {"seq": warm + 1 + k}
+            if k % 50 == 0:
+                meta.update({"csum": sums[k % nsrc], "verify": True})
+            node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size, meta)
+        node.send_output("data", b"", {"seq": warm + 1 + n_msgs, "ack": True})
+        node.wait_input("ack", "seq", warm + 1 + n_msgs, 60.0)
+        dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    for b in bufs:
+        b.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert dropped == 0, (dropped, out["dropped_inputs"])
+    assert sum(s["verified"] for s in out["series"]) == n_msgs // 50
+    assert sum(s["mismatches"] for s in out["series"]) == 0
 
 
 def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
