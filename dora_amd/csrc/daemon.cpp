@@ -166,6 +166,7 @@ class Daemon {
     uint64_t idle_since = mono_ns();
     uint64_t idle_from = 0;
     uint64_t last_liveness = 0;
+    AdaptiveSpin spin;  // spins through short idle gaps instead of sleeping (shm.h)
     std::vector<uint8_t> payload;
     RegionHdr* h = region_->hdr();
     bool placed = false;
@@ -210,13 +211,16 @@ class Daemon {
         last_liveness = now;
       }
       if (work) {
-        if (idle_from) add_idle_ns(now - idle_from);  // the spin/sleep that preceded this work
+        if (idle_from) {  // the spin/sleep that preceded this work
+          add_idle_ns(now - idle_from);
+          spin.observe(now - idle_from);
+        }
         idle_from = 0;
         idle_since = now;
         continue;
       }
       if (!idle_from) idle_from = now;
-      if (int64_t(now - idle_since) / 1000 < spin_budget_us()) {
+      if (int64_t(now - idle_since) / 1000 < spin.budget_us()) {
         __builtin_ia32_pause();
         continue;
       }

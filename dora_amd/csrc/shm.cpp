@@ -139,6 +139,28 @@ int64_t spin_budget_us() {
   return v;
 }
 
+int64_t spin_max_us() {
+  static int64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_SPIN_MAX_US");
+    return e ? std::atoll(e) : int64_t(5000);
+  }();
+  return v;
+}
+
+int64_t AdaptiveSpin::budget_us() const {
+  const int64_t base = spin_budget_us(), cap = spin_max_us();
+  const int64_t want = int64_t(2 * mean_ns_ / 1000);
+  return want <= cap && want > base ? want : base;
+}
+
+void AdaptiveSpin::observe(uint64_t idle_ns) {
+  // running mean over ~8 gaps; the first gap seeds it.  Gaps are clamped to 4 x the cap so that
+  // one long pause (start-up, a stalled producer) is forgotten within ~16 messages.
+  const uint64_t lim = uint64_t(std::max<int64_t>(spin_max_us(), 0)) * 4000;
+  if (idle_ns > lim) idle_ns = lim;
+  mean_ns_ =mean_ns_ ? mean_ns_ - mean_ns_ / 8 + idle_ns / 8 : idle_ns;
+}
+
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us) {
   timespec ts, *tp = nullptr;
   if (timeout_us >= 0) {
@@ -343,14 +365,19 @@ bool RingReader::try_pop(uint32_t* kind, std::vector<uint8_t>* payload) {
 
 bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag) {
   const uint64_t t0 = mono_ns();
-  const int64_t spin = spin_budget_us();
+  const int64_t spin = spin_.budget_us();
   struct Idle {
     uint64_t t0;
     bool was_empty;
+    AdaptiveSpin* spin;
+    bool got = false;
     ~Idle() {
-      if (was_empty) add_idle_ns(mono_ns() - t0);
+      if (!was_empty) return;
+      const uint64_t d = mono_ns() - t0;
+      add_idle_ns(d);
+      if (got) spin->observe(d);
     }
-  } idle{t0, empty()};
+  } idle{t0, empty(), &spin_};
   while (empty()) {
     const int64_t el = int64_t(mono_ns() - t0) / 1000;
     if (timeout_us >= 0 && el >= timeout_us) return false;
@@ -368,6 +395,7 @@ bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_fla
     }
     h_->waiters.fetch_sub(1, std::memory_order_seq_cst);
   }
+  idle.got = true;
   return true;
 }
 

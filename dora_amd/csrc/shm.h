@@ -126,6 +126,24 @@ class RingWriter {
   RingHdr* h_ = nullptr;
 };
 
+// How long a waiter spins before it sleeps on a futex.  A futex wake-up on a shared host can take
+// milliseconds (the woken thread waits for a CPU a neighbour holds): on one MI355X box the
+// latency ladder's p99 (1000 messages 1 ms apart per size) was 0.2-3.2 ms with every waiter
+// sleeping after 200 us of spinning, and 4-73 us when they spun through the gap
+// (profiles/r02_lat_tail_ab.jsonl).  So a waiter spins through its recent idle gaps when they
+// are short: budget = max(base, 2 x the running mean of the idle gaps that ended with data) while
+// that is within the cap, else the base.  A stream slower than the cap allows (e.g. 30 Hz
+// cameras) costs no more CPU than before; streams at >= ~400 Hz keep their waiters on-CPU.
+// DORA_GPU_SPIN_US = the base (200), DORA_GPU_SPIN_MAX_US = the cap (5000; 0: fixed base).
+class AdaptiveSpin {
+ public:
+  int64_t budget_us() const;
+  void observe(uint64_t idle_ns);  // an idle gap that ended because data arrived
+
+ private:
+  uint64_t mean_ns_ = 0;
+};
+
 class RingReader {
  public:
   RingReader() = default;
@@ -140,13 +158,15 @@ class RingReader {
  private:
   Region* r_ = nullptr;
   RingHdr* h_ = nullptr;
+  AdaptiveSpin spin_;
 };
 
 // futex helpers on shared (non-private) words
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us);
 void futex_wake(std::atomic<uint32_t>* w);
-int64_t spin_budget_us();
-uint64_t now_ns();           // CLOCK_REALTIME (timestamps that cross processes)
+int64_t spin_budget_us();      // the base budget (DORA_GPU_SPIN_US)
+int64_t spin_max_us();         // the adaptive cap (DORA_GPU_SPIN_MAX_US)
+uint64_t now_ns();          // CLOCK_REALTIME (timestamps that cross processes)
 uint64_t mono_ns();          // CLOCK_MONOTONIC
 // Restrict the calling thread (and threads it starts later) to the CPUs of NUMA node `numa`
 // within its current affinity; false when that would leave none or changes nothing.
