@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--n", type=int, default=5000)
     ap.add_argument("--sources", type=int, default=16)
     ap.add_argument("--no-params", action="store_true", help="send without parameters")
+    ap.add_argument("--align", type=int, default=0,
+                    help="allocate each source rounded up to this many bytes (0: exact size)")
     a = ap.parse_args()
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
@@ -42,7 +44,9 @@ def main():
     seq = 0
     out = []
     for size in [int(x) for x in a.sizes.split(",")]:
-        bufs = [device.DeviceBuffer(size) for _ in range(a.sources)]
+        alloc = -(-size // a.align) * a.align if a.align else size
+        bufs = [device.DeviceBuffer(alloc) for _ in range(a.sources)]
+        src_mod = sorted({b.ptr % (2 << 20) for b in bufs})
         for b in bufs:
             device.fill_splitmix(b.ptr, size, 1, stream)
         stream.sync()
@@ -70,7 +74,8 @@ def main():
         got = a.n - dropped
         out.append({"size": size, "n": a.n, "dropped": dropped,
                     "us_per_delivered_msg": round(dt / got * 1e6, 3),
-                    "hbm_frac_2S": round(2 * got * size / dt / 8e12, 4)})
+                    "hbm_frac_2S": round(2 * got * size / dt / 8e12, 4),
+                    "src_mod_2MiB": src_mod[:8]})
         for b in bufs:
             b.free()
     node.close()
