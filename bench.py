@@ -297,21 +297,35 @@ def native_ladder_msgs(size):
     return 20000 if size <= 4096000 else 3000 if size <= (16 << 20) else 1000
 
 
-def run_native_ladder(launcher, gpu, n=None, timeout=120.0):
+# Resident sources of the native ladder's throughput mode: the reference node sends one buffer
+# per size over and over (examples/benchmark/node/src/main.rs:28-36,59-69), and a 4 or 16 MB
+# source read that way stays in the GPU's L2s (8 x 4 MB, each XCD reads its 1/8 of the source):
+# only the sample writes reach HBM.  The HBM-resident ladder rotates copies past the L2s and,
+# from 16 MB, past the 256 MB Infinity Cache (640 MB of sources, at most 64 copies).
+NATIVE_RESIDENT_SIZES = [1 << 20, 4096000, 16 << 20]
+
+
+def native_sources(size, resident=False):
+    return 1 if resident else max(1, min(64, (640 << 20) // max(size, 1)))
+
+
+def run_native_ladder(launcher, gpu, n=None, timeout=120.0, resident=False):
     """Throughput mode of the native benchmark node (dora-gpu-bench-source -> -sink, one GPU,
     zero-copy edge) per size: the data plane through its C ABI, as a Rust node would bind it,
-    without the Python node's per-send cost.  Reported, never raised."""
+    without the Python node's per-send cost.  Sources rotate past the caches unless `resident`
+    (the reference's one buffer per size).  Reported, never raised."""
     from dora_amd.dataflow import Dataflow
     out = {}
     n_fixed = n
-    for size in NATIVE_SIZES:
+    for size in (NATIVE_RESIDENT_SIZES if resident else NATIVE_SIZES):
         n = n_fixed or native_ladder_msgs(size)
         tmp = tempfile.mkdtemp(prefix="dora-native-")
         try:
             desc = c4_descriptor(2, tmp, "kernel", tp_n=n, gpu=lambda g: gpu)
             desc["nodes"][0]["env"].update({
                 "DORA_BENCH_TP_SIZE": str(size), "DORA_BENCH_LAT_SIZES": str(size),
-                "DORA_BENCH_LAT_N": "5", "DORA_BENCH_LAT_GAP_US": "1000"})
+                "DORA_BENCH_LAT_N": "5", "DORA_BENCH_LAT_GAP_US": "1000",
+                "DORA_BENCH_TP_SOURCES": str(native_sources(size, resident))})
             df = Dataflow(desc, launcher=launcher).start()
             try:
                 codes = df.wait(timeout)
@@ -328,6 +342,7 @@ def run_native_ladder(launcher, gpu, n=None, timeout=120.0):
             out[str(size)] = {"GBps": gbps, "msgs": n, "sink_dropped": dropped,
                               "us_per_msg": round(size / (gbps * 1e3), 3) if gbps else None,
                               "hbm_frac_2S": round(2 * gbps / HBM_PEAK_GBPS, 4) if gbps else None,
+                              "sources": native_sources(size, resident),
                               "send_phase_us": r.get("send_phase_us"), "ok": r.get("ok"),
                               "exit_codes": codes}
         except Exception as e:  # noqa: BLE001 — reported in the JSON line
@@ -437,10 +452,11 @@ def main():
     # The native ladder runs before this process opens the GPU: afterwards this process keeps
     # its HIP and AQL hardware queues, and the ladder's nodes then ran >= 16 MB ~1.4x slower
     # (DORA_BENCH_LADDER_LATE=1 keeps the old order for A/B).
-    native = None
+    native = native_res = None
     ladder_late = os.environ.get("DORA_BENCH_LADDER_LATE") == "1"
     if native_ladder and not ladder_late:
         native = run_native_ladder(launcher, local_rank)
+        native_res = run_native_ladder(launcher, local_rank, resident=True)
 
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
@@ -567,7 +583,7 @@ def main():
     tp_ladder = {}
     if not args.no_ladder and args.tp_n > 0 and args.workload == "c2":
         for size in [z for z in LADDER_SMALL if z] + LADDER:
-            nb = max(1, min(16, (640 << 20) // size))
+            nb = native_sources(size)  # rotated past the L2s / Infinity Cache, as the native ladder
             bufs = [device.DeviceBuffer(size) for _ in range(nb)]
             for b in bufs:
                 device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
@@ -704,6 +720,7 @@ def main():
             cross = run_cross_gpu(world, launcher, gpu=gpu_of)
         if native_ladder and ladder_late:
             native = run_native_ladder(launcher, local_rank)
+            native_res = run_native_ladder(launcher, local_rank, resident=True)
         launcher.close()
     barrier()
     value = total_bytes / t_max / 1e9
@@ -750,7 +767,10 @@ def main():
                    "sources_rotated": nsrc},
         "latency_us": lat,
         "throughput_per_size": tp_ladder,
+        # sources rotated past the L2s / Infinity Cache: every byte read and written in HBM
         "throughput_per_size_native": native,
+        # the reference's one source buffer per size (L2-resident reads up to 16 MB)
+        "throughput_per_size_native_resident_source": native_res,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "vs_box_copy": (round(achieved / (copy_cal["TBps_2S"] * 1e3), 3)

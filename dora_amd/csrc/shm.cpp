@@ -154,11 +154,14 @@ int64_t AdaptiveSpin::budget_us() const {
 }
 
 void AdaptiveSpin::observe(uint64_t idle_ns) {
-  // running mean over ~8 gaps; the first gap seeds it.  Gaps are clamped to 4 x the cap so that
-  // one long pause (start-up, a stalled producer) is forgotten within ~16 messages.
+  // Fast down, slow up: a gap shorter than the mean replaces it (after a pause, the next short
+  // gap turns spinning back on at once — with a plain running mean the first ~16 messages of a
+  // 1 ms ladder after a 20 ms pause still slept, p99 4.2 ms at that size); a longer gap moves it
+  // 1/4 of the way (a 1 ms stream after a burst spins through its gaps from the 3rd message).
+  // Gaps are clamped to 4 x the cap.
   const uint64_t lim = uint64_t(std::max<int64_t>(spin_max_us(), 0)) * 4000;
   if (idle_ns > lim) idle_ns = lim;
-  mean_ns_ =mean_ns_ ? mean_ns_ - mean_ns_ / 8 + idle_ns / 8 : idle_ns;
+  mean_ns_ = idle_ns <= mean_ns_ || !mean_ns_ ? idle_ns : mean_ns_ + (idle_ns - mean_ns_) / 4;
 }
 
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us) {

@@ -131,8 +131,8 @@ class RingWriter {
 // latency ladder's p99 (1000 messages 1 ms apart per size) was 0.2-3.2 ms with every waiter
 // sleeping after 200 us of spinning, and 4-73 us when they spun through the gap
 // (profiles/r02_lat_tail_ab.jsonl).  So a waiter spins through its recent idle gaps when they
-// are short: budget = max(base, 2 x the running mean of the idle gaps that ended with data) while
-// that is within the cap, else the base.  A stream slower than the cap allows (e.g. 30 Hz
+// are short: budget = max(base, 2 x a fast-down / slow-up mean of the idle gaps that ended with
+// data) while that is within the cap, else the base.  A stream slower than the cap allows (e.g. 30 Hz
 // cameras) costs no more CPU than before; streams at >= ~400 Hz keep their waiters on-CPU.
 // DORA_GPU_SPIN_US = the base (200), DORA_GPU_SPIN_MAX_US = the cap (5000; 0: fixed base).
 class AdaptiveSpin {

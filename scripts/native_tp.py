@@ -27,6 +27,7 @@ def main():
         tmp = tempfile.mkdtemp(prefix="dora-native-tp-")
         desc = bench.c4_descriptor(2, tmp, "kernel", tp_n=a.n, gpu=lambda g: 0, env=env)
         src = desc["nodes"][0]
+        src["env"].update(env)  # c4_descriptor gives `env` to the sinks only
         src["env"].update({"DORA_BENCH_TP_SIZE": str(size), "DORA_BENCH_LAT_SIZES": str(size),
                            "DORA_BENCH_LAT_N": "5", "DORA_BENCH_LAT_GAP_US": "1000"})
         df = Dataflow(desc).start()
