@@ -551,6 +551,57 @@ def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
     assert stats["slots_created"] + stats["cache_hits"] == n_msgs
 
 
+class _StreamHandle:
+    def __init__(self, h):
+        self.handle = h
+
+
+def test_rewritten_source_each_send_bit_exact(launcher, tmp_path):
+    """One device source rewritten before every send (on the node stream, as
+    dora_node_stream's contract says) and sent on the AQL path each time: every delivered sample
+    must carry the bytes of its own rewrite.  The pack's workgroups may run on XCDs whose L2s
+    still hold the buffer's lines from the previous pack; the dispatch's acquire fence (or
+    coherent loads) must keep them from being served."""
+    from dora_amd import device
+    from dora_amd._lib import call
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    n_msgs, size = 200, 256 << 10
+    s = device.Stream()
+    scratch = device.DeviceBuffer(size)
+    sums = []
+    for k in range(n_msgs):
+        device.fill_splitmix(scratch.ptr, size, 0xC0FFEE00 + k, s)
+        sums.append(to_i64(device.csum64(scratch.ptr, size, s)))
+    scratch.free()
+    assert len(set(sums)) == n_msgs
+    src = device.DeviceBuffer(size)
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        for k in range(n_msgs):
+            # dora_node_stream orders every fill launched so far (the previous pack still reading
+            # `src`) before the work queued on it next: the rewrite
+            ns = _StreamHandle(node.stream)
+            device.fill_splitmix(src.ptr, size, 0xC0FFEE00 + k, ns)
+            call("dora_gpu_stream_sync", ns.handle)  # node stream idle: the send takes AQL
+            node.send_output_device_bytes("data", src.ptr, size,
+                                          {"seq": k, "csum": sums[k], "verify": True})
+        paths = node.fill_paths()
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    src.free()
+    s.close()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(x["mismatches"] for x in out["series"]) == 0, out
+    assert sum(x["verified"] for x in out["series"]) == n_msgs
+    assert paths["aql"] >= n_msgs, paths
+
+
 def test_output_without_receivers_recycles_safely(launcher, tmp_path):
     """Sends on an output nobody subscribes to get their drop token back at once (the daemon's
     check_drop_token with no pending receiver), long before their packs finish.  The recycled
