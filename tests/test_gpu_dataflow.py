@@ -602,6 +602,46 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path):
     assert paths["aql"] >= n_msgs, paths
 
 
+def test_host_source_reused_right_after_send_bit_exact(launcher, tmp_path):
+    """send_output_raw semantics for host data (examples/benchmark/node/src/main.rs:46-48: the
+    closure copies `data` before send returns): one host buffer overwritten with the next payload
+    as soon as each send returns, through the C ABI as a Rust node would call it.  Every
+    delivered sample must hold the payload of its own send."""
+    import ctypes
+    from dora_amd import device
+    from dora_amd._lib import ARROW_DEVICE_CPU
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node, _fast
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    n_msgs, size = 120, 1 << 20
+    payloads = [os.urandom(size) for _ in range(n_msgs)]
+    s = device.Stream()
+    sums = []
+    for p in payloads:
+        b = device.DeviceBuffer.from_bytes(p, s)
+        sums.append(to_i64(device.csum64(b.ptr, size, s)))
+        b.free()
+    s.close()
+    buf = ctypes.create_string_buffer(size)
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        for k in range(n_msgs):
+            ctypes.memmove(buf, payloads[k], size)
+            rc = _fast.send_bytes(node.handle, "data", ctypes.addressof(buf), size,
+                                  ARROW_DEVICE_CPU, {"seq": k, "csum": sums[k], "verify": True})
+            assert rc == 0
+            ctypes.memset(buf, 0xA5, size)  # the caller reuses its buffer at once
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(x["mismatches"] for x in out["series"]) == 0, out
+    assert sum(x["verified"] for x in out["series"]) == n_msgs
+
+
 def test_output_without_receivers_recycles_safely(launcher, tmp_path):
     """Sends on an output nobody subscribes to get their drop token back at once (the daemon's
     check_drop_token with no pending receiver), long before their packs finish.  The recycled
