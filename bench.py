@@ -136,10 +136,13 @@ def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
 def aql_kernel_name(workload: str, body: int) -> str:
     """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*: 4
     loads in flight per lane unless DORA_GPU_PACK_VARIANT says u8; one segment at offset 0 ->
-    pack1)."""
+    pack1, with agent-coherent source loads (pack1c) unless DORA_GPU_AQL_COHERENT=0)."""
     v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
     u = 8 if v.startswith("u8") else 4
-    return f"dora_aql_pack{'1' if workload == 'c2' else ''}_u{u} (AQL)"
+    if workload != "c2":
+        return f"dora_aql_pack_u{u} (AQL)"
+    c = "c" if u == 4 and os.environ.get("DORA_GPU_AQL_COHERENT", "1") != "0" else ""
+    return f"dora_aql_pack1{c}_u{u} (AQL)"
 
 
 def pmc_traffic(msg_bytes: int):

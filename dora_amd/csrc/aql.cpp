@@ -65,8 +65,8 @@ struct AqlQueue {
   hsa_queue_t* qs[kMaxQueues] = {};
   uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
   int nq = 0;
-  uint64_t kobj[4] = {0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8
-  uint32_t group[4] = {0, 0, 0, 0}, priv[4] = {0, 0, 0, 0};
+  uint64_t kobj[5] = {0, 0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8, pack1c_u4
+  uint32_t group[5] = {0, 0, 0, 0, 0}, priv[5] = {0, 0, 0, 0, 0};
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
   uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
@@ -216,9 +216,9 @@ AqlQueue* create(int device) {
     delete a;
     return note("code object");
   }
-  const char* names[4] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
-                          "dora_aql_pack1_u8.kd"};
-  for (int k = 0; k < 4; ++k) {
+  const char* names[5] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
+                          "dora_aql_pack1_u8.kd", "dora_aql_pack1c_u4.kd"};
+  for (int k = 0; k < 5; ++k) {
     hsa_executable_symbol_t sym;
     uint32_t ka = 0;
     if (hsa_executable_get_symbol_by_name(exe, names[k], &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
@@ -430,7 +430,21 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   }
   hsa_queue_store_write_index_relaxed(q, idx + 1);
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  const int k = (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
+  // Single-segment packs read their source with agent-coherent loads (dora_aql_pack1c_u4: sc1,
+  // the scope LLVM's gfx942 memory model gives relaxed agent-scope atomic loads) and their packets
+  // carry no acquire fence (below): the fence's L2 invalidation is what kept a source line an
+  // earlier pack left in an L2 from being served after a writer on another XCD replaced it, and
+  // coherent loads never take such a line.  Their arguments are preloaded into SGPRs by the
+  // command processor, so no kernarg line can be stale either.  Interleaved A/B on one box, sources
+  // rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 -> 1.23-1.26 us per
+  // message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.  DORA_GPU_AQL_COHERENT=0:
+  // plain loads behind the acquire fence (A/B knob).
+  static const bool coherent = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_COHERENT");
+    return !(e && *e == '0');
+  }();
+  const bool coh = coherent && one && unroll == 4;
+  const int k = coh ? 4 : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
@@ -467,7 +481,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   }();
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                           (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
-                          (acquire << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                          ((coh ? uint32_t(HSA_FENCE_SCOPE_NONE) : acquire)
+                           << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),

@@ -23,7 +23,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u8(AqlPackA
 // no HDP flush per send (aql.cpp; profiles/r01_aql_preload_probe.jsonl: 0.15 vs 1.6 us host
 // time per dispatch at the same device time).  The chunk count is derived here as
 // build_aql_args derives it for one segment.
-template <int U>
+template <int U, int NT = 2>
 __device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t len,
                                       uint64_t* flag, uint32_t* done, uint64_t epoch,
                                       uint32_t chunk_bytes, uint32_t grid) {
@@ -41,7 +41,7 @@ __device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t
   a.edge_mask = 0;  // a tail unit past `len` may lie outside the destination: bytes one by one
   a.chunk_end[0] = static_cast<uint32_t>(nc);
   a.seg[0] = {src, 0, len};
-  dora::pack::pack_body<U, 2>(a, __builtin_amdgcn_workgroup_id_x(), grid);
+  dora::pack::pack_body<U, NT>(a, __builtin_amdgcn_workgroup_id_x(), grid);
 }
 
 extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u4(
@@ -54,4 +54,12 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u8(
     uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
     uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
   pack1<8>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
+}
+
+// As dora_aql_pack1_u4, reading the source with agent-coherent loads (pack_device.h kCoherent):
+// dispatched without the packet's acquire fence (aql.cpp, DORA_GPU_AQL_COHERENT).
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
+    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
+    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
+  pack1<4, dora::pack::kCoherent>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }

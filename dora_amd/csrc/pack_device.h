@@ -81,7 +81,25 @@ typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 // Memory policy NT: 0 plain, 1 non-temporal loads and stores, 2/3 non-temporal loads and stores
 // written through to device (sc1) / system (sc0 sc1) scope — no L2 write-back needed before a
-// fill signal.
+// fill signal.  4: as 2, and the source is read with agent-coherent loads (buffer_load sc1 nt),
+// which never return a line another XCD's writer has since replaced, so the dispatch needs no
+// acquire fence (its L2 invalidation) to see a source rewritten since an earlier pack read it.
+constexpr int kCoherent = 4;
+// raw buffer loads: cache policy bits sc1 (16) | nt (2); resource word 3 as for gfx9 raw buffers
+constexpr int kCoherentPolicy = 16 | 2;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const uint8_t* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ldc16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kCoherentPolicy);
+}
+// one source byte (heads, tails, stitched units)
+template <int NT>
+__device__ __forceinline__ uint8_t ld1(const uint8_t* p) {
+  if constexpr (NT == kCoherent) return __builtin_amdgcn_raw_buffer_load_b8(src_rsrc(p), 0, 0, kCoherentPolicy);
+  return *p;
+}
+
 template <int NT, bool DW = false>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
   if constexpr (DW) {  // p only 4-byte aligned
@@ -93,7 +111,7 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
 }
 template <int NT>
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT == 2) {
+  if constexpr (NT == 2 || NT == kCoherent) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
   } else if constexpr (NT == 3) {
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
@@ -133,12 +151,17 @@ __device__ __forceinline__ u32x4 funnel(u32x4 lo, u32x4 hi, uint32_t b) {
 template <int U, int NT, bool DW = false>
 __device__ __forceinline__ void copy_aligned(uint8_t* dp, const uint8_t* sp, uint64_t skip,
                                              uint64_t nunits) {
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t r;
+  if constexpr (NT == kCoherent) r = src_rsrc(sp);
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
-      if (i >= skip && i < nunits) v[u] = ld16<NT, DW>(sp + 16 * i);
+      if (i >= skip && i < nunits) {
+        if constexpr (NT == kCoherent) v[u] = ldc16(r, static_cast<uint32_t>(16 * i));
+        else v[u] = ld16<NT, DW>(sp + 16 * i);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -152,14 +175,21 @@ template <int U, int NT, int Q>
 __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, uint32_t b,
                                              uint64_t skip, uint64_t nunits) {
   // sbase = 16-aligned address holding the first source byte at byte 4Q+b.
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t r;
+  if constexpr (NT == kCoherent) r = src_rsrc(sbase);
   for (uint64_t base = threadIdx.x; base < nunits; base += kThreads * U) {
     u32x4 lo[U], hi[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + uint64_t(u) * kThreads;
       if (i >= skip && i < nunits) {
-        lo[u] = ld16<NT>(sbase + 16 * i);
-        hi[u] = ld16<NT>(sbase + 16 * i + 16);
+        if constexpr (NT == kCoherent) {
+          lo[u] = ldc16(r, static_cast<uint32_t>(16 * i));
+          hi[u] = ldc16(r, static_cast<uint32_t>(16 * i + 16));
+        } else {
+          lo[u] = ld16<NT>(sbase + 16 * i);
+          hi[u] = ld16<NT>(sbase + 16 * i + 16);
+        }
       }
     }
 #pragma unroll
@@ -172,11 +202,11 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
 
 // Byte `o` (sample offset) of a stitched boundary unit: from the segment that holds it, else
 // the byte the destination already has (padding stays as it was, arrow_utils.rs:48).
-template <class A>
+template <int NT, class A>
 __device__ __forceinline__ uint8_t unit_byte(const A& a, uint64_t o) {
   for (uint32_t k = 0; k < (a.nseg & ~kUnitChunks); ++k) {
     const PackSeg g = a.seg[k];
-    if (o - g.dst_off < g.len) return g.src[o - g.dst_off];  // unsigned: o in [dst_off, +len)
+    if (o - g.dst_off < g.len) return ld1<NT>(g.src + (o - g.dst_off));  // o in [dst_off, +len)
   }
   return a.dst[o];
 }
@@ -213,13 +243,13 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
     const uint32_t t = threadIdx.x;
     if (has_head && !st_head) {
       const uint64_t hend = a0 < d1 ? a0 : d1;
-      if (t < hend - d0) st1<NT>(dst + d0 + t, src[t]);
+      if (t < hend - d0) st1<NT>(dst + d0 + t, ld1<NT>(src + t));
     }
     if (has_tail && !st_tail) {
       const uint64_t t0 = a1 > a0 ? a1 : a0;
       if (t >= 64 && t - 64 < d1 - t0) {
         const uint64_t d = t0 + (t - 64);
-        st1<NT>(dst + d, src[d - d0]);
+        st1<NT>(dst + d, ld1<NT>(src + (d - d0)));
       }
     }
     if (st_head || st_tail) {  // uniform over the workgroup
@@ -230,8 +260,8 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
       // a unit shared with the previous segment is written by that segment (the lowest one
       // holding a byte of it); a tail unit always belongs to its segment
       const bool own_head = st_head && (s == 0 || args.seg[s - 1].dst_off + args.seg[s - 1].len <= H);
-      if (own_head && t < 16) ub[t] = unit_byte(args, H + t);
-      if (st_tail && t >= 64 && t < 80) ub[16 + (t - 64)] = unit_byte(args, T + (t - 64));
+      if (own_head && t < 16) ub[t] = unit_byte<NT>(args, H + t);
+      if (st_tail && t >= 64 && t < 80) ub[16 + (t - 64)] = unit_byte<NT>(args, T + (t - 64));
       __syncthreads();
       if (own_head && t == 0) st16<NT>(dst + H, unit[0]);
       if (st_tail && t == 64) st16<NT>(dst + T, unit[1]);
