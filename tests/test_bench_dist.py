@@ -119,3 +119,31 @@ def test_edge_rate_uses_the_throughput_burst():
     assert e["GBps"] == 1.0 and e["xgmi_frac"] == round(1.0 / bench.XGMI_LINK_GBPS, 4)
     old = {"pulls": 0, "series": [dict(sink["series"][0], burst_n=0)]}  # older sinks: whole series
     assert bench.edge_rates({"s": old})[0]["GBps"] == round(12 * 100 / (10 ** 9 + 2000), 3)
+
+
+def test_ladder_sources_rotate_past_the_caches():
+    """The throughput ladders read every byte from HBM: rotated copies cover > 256 MB (the
+    Infinity Cache) at 16 MB and up, > 32 MB (the eight L2s) from 1 MB, at most 64 copies; the
+    resident-source ladder is the reference node's one buffer per size."""
+    import bench
+    for size in (1 << 20, 4096000, 16 << 20, 40960000):
+        n = bench.native_sources(size)
+        assert 1 < n <= 64
+        assert n * size > 32 << 20
+        if size >= 16 << 20:
+            assert n * size > 256 << 20
+        assert bench.native_sources(size, resident=True) == 1
+    assert bench.native_sources(0) == 64 and bench.native_sources(4096) == 64
+
+
+def test_aql_kernel_name_follows_the_coherent_knob(monkeypatch):
+    import bench
+    monkeypatch.delenv("DORA_GPU_AQL_COHERENT", raising=False)
+    monkeypatch.delenv("DORA_GPU_PACK_VARIANT", raising=False)
+    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
+    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
+    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "0")
+    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u4 (AQL)"
+    monkeypatch.setenv("DORA_GPU_PACK_VARIANT", "u8nt")
+    monkeypatch.delenv("DORA_GPU_AQL_COHERENT")
+    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u8 (AQL)"
