@@ -139,9 +139,11 @@ def aql_kernel_name(workload: str, body: int) -> str:
     pack1, with agent-coherent source loads (pack1c) unless DORA_GPU_AQL_COHERENT=0)."""
     v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
     u = 8 if v.startswith("u8") else 4
+    coh = os.environ.get("DORA_GPU_AQL_COHERENT", "1")
     if workload != "c2":
-        return f"dora_aql_pack_u{u} (AQL)"
-    c = "c" if u == 4 and os.environ.get("DORA_GPU_AQL_COHERENT", "1") != "0" else ""
+        c = "c" if u == 4 and coh == "all" else ""
+        return f"dora_aql_pack{c}_u{u} (AQL)"
+    c = "c" if u == 4 and coh != "0" else ""
     return f"dora_aql_pack1{c}_u{u} (AQL)"
 
 

@@ -65,8 +65,9 @@ struct AqlQueue {
   hsa_queue_t* qs[kMaxQueues] = {};
   uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
   int nq = 0;
-  uint64_t kobj[5] = {0, 0, 0, 0, 0};  // u4, u8, pack1_u4, pack1_u8, pack1c_u4
-  uint32_t group[5] = {0, 0, 0, 0, 0}, priv[5] = {0, 0, 0, 0, 0};
+  // u4, u8, pack1_u4, pack1_u8, pack1c_u4, packc_u4
+  uint64_t kobj[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t group[6] = {0, 0, 0, 0, 0, 0}, priv[6] = {0, 0, 0, 0, 0, 0};
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
   uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
@@ -145,6 +146,21 @@ hsa_status_t on_cpu_pool(hsa_amd_memory_pool_t pool, void* p) {
   return HSA_STATUS_SUCCESS;
 }
 
+// DORA_GPU_AQL_COHERENT (aql_pack): single-segment packs read their sources with agent-coherent
+// loads and carry no acquire fence (default; 0 = plain loads behind the fence).  "all" does the
+// same for multi-segment packs, which then copy their arguments from the device ring into LDS
+// with coherent loads first: one dependent memory round trip at every workgroup's start made C3
+// slower, 4.50 -> 4.89-5.23 us per cloud (profiles/r02_coherent_c3_ab.jsonl), so it is a knob.
+int coherent_level() {
+  static const int v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_COHERENT");
+    if (e && *e == '0') return 0;
+    if (e && std::string(e) == "all") return 2;
+    return 1;
+  }();
+  return v;
+}
+
 // DORA_GPU_AQL_PRELOAD=0: single-segment packs use the device argument ring too.
 bool preload_enabled() {
   static const bool v = [] {
@@ -216,9 +232,9 @@ AqlQueue* create(int device) {
     delete a;
     return note("code object");
   }
-  const char* names[5] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
-                          "dora_aql_pack1_u8.kd", "dora_aql_pack1c_u4.kd"};
-  for (int k = 0; k < 5; ++k) {
+  const char* names[6] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
+                          "dora_aql_pack1_u8.kd", "dora_aql_pack1c_u4.kd", "dora_aql_packc_u4.kd"};
+  for (int k = 0; k < 6; ++k) {
     hsa_executable_symbol_t sym;
     uint32_t ka = 0;
     if (hsa_executable_get_symbol_by_name(exe, names[k], &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
@@ -231,7 +247,8 @@ AqlQueue* create(int device) {
         hsa_executable_symbol_get_info(
             sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &a->priv[k]) !=
             HSA_STATUS_SUCCESS ||
-        ka != (k < 2 ? aql_args_size() : size_t(kArgs1Bytes)) || ka > kSlotBytes) {
+        ka != (k < 2 ? aql_args_size() : k == 5 ? sizeof(void*) : size_t(kArgs1Bytes)) ||
+        ka > kSlotBytes) {
       delete a;
       return note("kernel symbol / argument size");  // no hidden arguments expected
     }
@@ -383,6 +400,9 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
       a->used_sigs.push_back(done);
     }
   }
+  // Coherent packs (see `coherent` below): multi-segment ones read their arguments from the
+  // device-ring slot through a pointer preloaded from the host ring.
+  const bool coh_multi = coherent_level() >= 2 && !one && unroll == 4 && a->hring;
   uint8_t* slot;
   if (one) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
@@ -395,6 +415,11 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     // are posted writes ordered before the doorbell
     __builtin_ia32_sfence();
     *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
+    if (coh_multi) {
+      uint8_t* const dev_slot = slot;
+      slot = a->hring + r * kHostSlotBytes;
+      std::memcpy(slot, &dev_slot, sizeof(dev_slot));
+    }
   }
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
@@ -439,12 +464,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 -> 1.23-1.26 us per
   // message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.  DORA_GPU_AQL_COHERENT=0:
   // plain loads behind the acquire fence (A/B knob).
-  static const bool coherent = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_COHERENT");
-    return !(e && *e == '0');
-  }();
-  const bool coh = coherent && one && unroll == 4;
-  const int k = coh ? 4 : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
+  const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi;
+  const int k = coh ? (one ? 4 : 5) : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;

@@ -63,3 +63,21 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
     uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
   pack1<4, dora::pack::kCoherent>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
+
+// Multi-segment packs without the packet's acquire fence: the one (preloaded) argument is the
+// device-ring slot holding the AqlPackArgs, which the workgroup copies into LDS with
+// agent-coherent loads — a kernarg s_load could be served a stale L2 or scalar-cache line of a
+// slot last used kRingSlots packs ago once no fence invalidates them — and the sources are read
+// coherently as in dora_aql_pack1c_u4 (aql.cpp, DORA_GPU_AQL_COHERENT).
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_packc_u4(const AqlPackArgs* ap) {
+  __shared__ AqlPackArgs a;
+  constexpr uint32_t kWords = sizeof(AqlPackArgs) / 4;
+  static_assert(sizeof(AqlPackArgs) % 4 == 0 && kWords <= kThreads, "arguments fit one pass");
+  if (threadIdx.x < kWords) {
+    const auto r = dora::pack::src_rsrc(reinterpret_cast<const uint8_t*>(ap));
+    reinterpret_cast<uint32_t*>(&a)[threadIdx.x] =
+        __builtin_amdgcn_raw_buffer_load_b32(r, threadIdx.x * 4, 0, dora::pack::kCoherentPolicy);
+  }
+  __syncthreads();
+  dora::pack::pack_body<4, dora::pack::kCoherent>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
+}

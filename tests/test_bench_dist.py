@@ -142,6 +142,9 @@ def test_aql_kernel_name_follows_the_coherent_knob(monkeypatch):
     monkeypatch.delenv("DORA_GPU_PACK_VARIANT", raising=False)
     assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
     assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
+    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "all")
+    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_packc_u4 (AQL)"
+    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
     monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "0")
     assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u4 (AQL)"
     monkeypatch.setenv("DORA_GPU_PACK_VARIANT", "u8nt")
