@@ -556,12 +556,15 @@ class _StreamHandle:
         self.handle = h
 
 
-def test_rewritten_source_each_send_bit_exact(launcher, tmp_path):
+@pytest.mark.parametrize("writer", ["kernel", "dma"])
+def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer):
     """One device source rewritten before every send (on the node stream, as
-    dora_node_stream's contract says) and sent on the AQL path each time: every delivered sample
-    must carry the bytes of its own rewrite.  The pack's workgroups may run on XCDs whose L2s
-    still hold the buffer's lines from the previous pack; the dispatch's acquire fence (or
-    coherent loads) must keep them from being served."""
+    dora_node_stream's contract says) — by a kernel, or by a host-to-device copy — and sent on
+    the AQL path each time: every delivered sample must carry the bytes of its own rewrite.  The
+    pack's workgroups may run on XCDs whose L2s still hold the buffer's lines from the previous
+    pack; its agent-coherent loads (or the dispatch's acquire fence) must keep them from being
+    served."""
+    import ctypes
     from dora_amd import device
     from dora_amd._lib import call
     from dora_amd.dataflow import Dataflow
@@ -571,10 +574,12 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path):
     n_msgs, size = 200, 256 << 10
     s = device.Stream()
     scratch = device.DeviceBuffer(size)
-    sums = []
+    sums, host = [], []
     for k in range(n_msgs):
         device.fill_splitmix(scratch.ptr, size, 0xC0FFEE00 + k, s)
         sums.append(to_i64(device.csum64(scratch.ptr, size, s)))
+        if writer == "dma":
+            host.append(scratch.to_bytes(stream=s))
     scratch.free()
     assert len(set(sums)) == n_msgs
     src = device.DeviceBuffer(size)
@@ -584,7 +589,11 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path):
             # dora_node_stream orders every fill launched so far (the previous pack still reading
             # `src`) before the work queued on it next: the rewrite
             ns = _StreamHandle(node.stream)
-            device.fill_splitmix(src.ptr, size, 0xC0FFEE00 + k, ns)
+            if writer == "kernel":
+                device.fill_splitmix(src.ptr, size, 0xC0FFEE00 + k, ns)
+            else:
+                hb = ctypes.create_string_buffer(host[k], size)
+                call("dora_gpu_memcpy_async", src.ptr, hb, size, ns.handle)
             call("dora_gpu_stream_sync", ns.handle)  # node stream idle: the send takes AQL
             node.send_output_device_bytes("data", src.ptr, size,
                                           {"seq": k, "csum": sums[k], "verify": True})
