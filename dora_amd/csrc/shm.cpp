@@ -368,24 +368,38 @@ bool RingReader::try_pop(uint32_t* kind, std::vector<uint8_t>* payload) {
 
 bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag) {
   const uint64_t t0 = mono_ns();
+  // One idle gap may span several calls that time out (a sender polling for drop tokens every
+  // 1 ms): the gap — for the spin budget and the adaptive mean — runs from the first of them,
+  // unless the caller did other work for a while in between.
+  if (empty()) {
+    if (!idle_from_ || t0 - last_return_ > 100000) idle_from_ = t0;
+  } else {
+    idle_from_ = 0;
+  }
+  const uint64_t gap0 = idle_from_ ? idle_from_ : t0;
   const int64_t spin = spin_.budget_us();
   struct Idle {
+    RingReader* r;
     uint64_t t0;
     bool was_empty;
-    AdaptiveSpin* spin;
     bool got = false;
     ~Idle() {
+      const uint64_t now = mono_ns();
+      r->last_return_ = now;
       if (!was_empty) return;
-      const uint64_t d = mono_ns() - t0;
-      add_idle_ns(d);
-      if (got) spin->observe(d);
+      add_idle_ns(now - t0);
+      if (got) {
+        r->spin_.observe(now - r->idle_from_);
+        r->idle_from_ = 0;
+      }
     }
-  } idle{t0, empty(), &spin_};
+  } idle{this, t0, empty()};
   while (empty()) {
-    const int64_t el = int64_t(mono_ns() - t0) / 1000;
+    const uint64_t now = mono_ns();
+    const int64_t el = int64_t(now - t0) / 1000;
     if (timeout_us >= 0 && el >= timeout_us) return false;
     if (abort_flag && abort_flag->load(std::memory_order_relaxed)) return false;
-    if (el < spin) {
+    if (int64_t(now - gap0) / 1000 < spin) {
       __builtin_ia32_pause();
       continue;
     }

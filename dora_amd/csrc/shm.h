@@ -159,6 +159,8 @@ class RingReader {
   Region* r_ = nullptr;
   RingHdr* h_ = nullptr;
   AdaptiveSpin spin_;
+  uint64_t idle_from_ = 0;    // start of the current idle gap (0: none)
+  uint64_t last_return_ = 0;  // when wait() last returned
 };
 
 // futex helpers on shared (non-private) words
