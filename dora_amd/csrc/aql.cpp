@@ -400,8 +400,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
       a->used_sigs.push_back(done);
     }
   }
-  // Coherent packs (see `coherent` below): multi-segment ones read their arguments from the
-  // device-ring slot through a pointer preloaded from the host ring.
+  // Coherent multi-segment packs (DORA_GPU_AQL_COHERENT=all, coherent_level): the kernel reads
+  // its arguments from the device-ring slot through a pointer preloaded from the host ring.
   const bool coh_multi = coherent_level() >= 2 && !one && unroll == 4 && a->hring;
   uint8_t* slot;
   if (one) {
