@@ -55,6 +55,9 @@ def parse():
                     help="throughput ladder: back-to-back messages per size, at least 2000 up "
                          "to 4 MiB (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 block the default C2 run reports beside the headline")
+    ap.add_argument("--c3-steps", type=int, default=20)
     ap.add_argument("--sources", type=int, default=0, help="rotating source buffers (0: auto)")
     ap.add_argument("--c3-lists", type=int, default=0,
                     help="c3 diagnosis: lists per cloud (15: every buffer at 0 mod 16)")
@@ -136,14 +139,14 @@ def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
 def aql_kernel_name(workload: str, body: int) -> str:
     """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*: 4
     loads in flight per lane unless DORA_GPU_PACK_VARIANT says u8; one segment at offset 0 ->
-    pack1, with agent-coherent source loads (pack1c) unless DORA_GPU_AQL_COHERENT=0)."""
+    pack1, with agent-coherent source loads (pack1c) when DORA_GPU_AQL_COHERENT=1)."""
     v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
     u = 8 if v.startswith("u8") else 4
-    coh = os.environ.get("DORA_GPU_AQL_COHERENT", "1")
+    coh = os.environ.get("DORA_GPU_AQL_COHERENT", "0")
     if workload != "c2":
         c = "c" if u == 4 and coh == "all" else ""
         return f"dora_aql_pack{c}_u{u} (AQL)"
-    c = "c" if u == 4 and coh != "0" else ""
+    c = "c" if u == 4 and coh in ("1", "all") else ""
     return f"dora_aql_pack1{c}_u{u} (AQL)"
 
 
@@ -429,6 +432,79 @@ def summarize_cross(name, src, sinks, codes, logs):
     return res
 
 
+C3_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden",
+                         "c3_cloud.json")
+
+
+def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
+    """BASELINE configs[2] beside the C2 headline: `send_output` of device-resident 1M-point
+    clouds (List<Struct<x,y,z:f32,intensity:u8>>, 16 lists, validity bitmaps; one multi-segment
+    AQL pack each), `steps` back-to-back sends from `nsrc` rotating clouds, device time from the
+    packs' own stamps.  Parity: the last 4 timed clouds are held by the sink and checksummed
+    against the CPU oracle's sample (tests/golden/c3_cloud.json, make_c3_golden.py), and so is
+    a reference pack of the same cloud made before the clock."""
+    from dora_amd import device
+    from dora_amd.arrow_utils import Plan
+    from dora_amd.device import DeviceArray
+    from dora_amd.verify import to_i64
+    from dora_amd.workloads import point_cloud
+    golden = json.load(open(C3_GOLDEN))
+    cloud = point_cloud()
+    srcs = [DeviceArray.from_pyarrow(cloud) for _ in range(nsrc)]
+    with Plan.of(srcs[0]) as p:
+        S = p.size
+        ref = device.DeviceBuffer(S)
+        p.pack(ref.ptr, S, stream)
+        stream.sync()
+    ref_csum = device.csum64(ref.ptr, S, stream)
+    ref.free()
+    want = golden["csum64"]
+    for k in range(2 * nsrc):  # slots of this size in the cache, the sink's mappings of them
+        node.send_output("throughput", srcs[k % nsrc], {"seq": seq})
+        seq += 1
+    node.send_output("throughput", b"", {"seq": seq, "ack": True})
+    wait_ack(seq)
+    seq += 1
+    late = min(4, steps)
+    before = node.stats()
+    node.sync()
+    node.region_begin()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        meta = {"seq": seq}
+        if k >= steps - late:
+            meta.update({"csum": to_i64(want), "verify_late": True})
+        if k == steps - 1:
+            meta["ack"] = True
+        node.send_output("throughput", srcs[k % nsrc], meta)
+        seq += 1
+    node.region_mark()
+    wait_ack(seq - 1)
+    node.sync()
+    elapsed = time.perf_counter() - t0
+    region = node.region_end()
+    after = node.stats()
+    for a in srcs:
+        a.close()
+    span_ms, packs = region["span_ms"], region["packs"]
+    achieved = 2.0 * S * packs / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
+    return seq, {
+        "workload": "C3 (BASELINE configs[2]): send_output of device-resident 1M-point clouds, "
+                    "List<Struct<x,y,z:f32,intensity:u8>> in 16 lists with validity bitmaps",
+        "value": round(steps * S / elapsed / 1e9, 3), "unit": "GB/s", "steps": steps,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "msg_bytes": S, "sources_rotated": nsrc,
+        "slots_created_in_region": after["slots_created"] - before["slots_created"],
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "kernel": aql_kernel_name("c3", S),
+                     "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
+                     "region_packs": packs, "algorithmic_bytes_per_launch": 2 * S},
+        "parity": {"oracle_sample_bytes": golden["sample_bytes"], "oracle_csum64": want,
+                   "reference_pack_matches_oracle": ref_csum == want and S == golden["sample_bytes"],
+                   "late_verified_msgs": late},
+    }
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -485,6 +561,11 @@ def main():
     from dora_amd.workloads import payload_seed
 
     node = Node("node", dataflow=df.shm, device=local_rank)
+    # the benchmark node never rewrites its sources: every send returns as soon as its pack is
+    # queued (DORA_SEND_ASYNC), so packs overlap; the default synchronous send is measured
+    # beside it (sync_send_headline)
+    sync_sends = os.environ.get("DORA_BENCH_SYNC_SENDS") == "1"
+    node.set_async_sends(not sync_sends)
     stream = device.Stream()
     if args.workload == "c2":
         S = args.size
@@ -702,6 +783,9 @@ def main():
     stats["fill_paths"] = node.fill_paths()
     # the timed region's packs, each from its own stamps (first workgroup start -> fill signal)
     intervals = node.pack_intervals() if region else []
+    c3 = None
+    if args.workload == "c2" and not args.no_c3 and world == 1 and args.c3_steps > 0:
+        seq, c3 = run_c3_block(node, stream, wait_ack, seq, steps=args.c3_steps)
     node.close()
     codes = df.wait(120)
     df.stop()
@@ -749,8 +833,9 @@ def main():
             lat[str(s["size"])] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
                                    "p50_incl_pack_us": s["full_p50_us"],
                                    "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
-    verified = sum(s["verified"] for s in sink.get("series", []))
-    mismatches = sum(s["mismatches"] for s in sink.get("series", []))
+    c2_series = [s for s in sink.get("series", []) if c3 is None or s["size"] != c3["msg_bytes"]]
+    verified = sum(s["verified"] for s in c2_series)
+    mismatches = sum(s["mismatches"] for s in c2_series)
     if args.workload == "c2":
         metric = f"node->node GB/s ({S:,} B UInt8 samples) + p50/p99 latency per msg size"
         workload = ("C2: examples/benchmark node->sink edge, device-resident UInt8 samples, "
@@ -811,6 +896,11 @@ def main():
         "sink_dropped_inputs": sink.get("dropped_inputs"),
         "node_stats": stats, "exit_codes": codes,
     }
+    if c3 is not None:
+        s3 = [x for x in sink.get("series", []) if x["size"] == c3["msg_bytes"]]
+        c3["parity"]["verified_msgs"] = sum(x["verified"] for x in s3)
+        c3["parity"]["mismatches"] = sum(x["mismatches"] for x in s3)
+        line["c3"] = c3
     if cross is not None:
         line["cross_gpu"] = cross
     if base is not None:

@@ -51,6 +51,8 @@ _SIGS = {
     "dora_gpu_last_error": (c_char_p, []),
     "dora_gpu_version": (c_char_p, []),
     "dora_gpu_busy_stats": (c_int, [POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_gpu_aql_dispatch_counts": (c_int, [c_int, POINTER(c_uint64), c_size_t, POINTER(c_size_t)]),
+    "dora_gpu_aql_kernel_name": (c_char_p, [c_size_t]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),
@@ -96,6 +98,10 @@ _SIGS = {
     "dora_gpu_schema_release": (None, [POINTER(ArrowSchema)]),
     "dora_gpu_csum64": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
     "dora_gpu_csum64_sync": (c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_uint64)]),
+    "dora_gpu_l2_touch": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
+    "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
+    "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_fill_splitmix": (c_int, [c_void_p, c_size_t, c_uint64, c_void_p]),
     # node API
     "dora_node_init": (c_int, [c_char_p, c_char_p, c_int, POINTER(c_void_p)]),
@@ -113,6 +119,12 @@ _SIGS = {
                                       POINTER(ArrowSchema), c_int32, c_char_p, c_size_t]),
     "dora_node_send_output_bytes": (c_int, [c_void_p, c_char_p, c_void_p, c_size_t, c_int32,
                                             c_char_p, c_size_t]),
+    "dora_node_send_output_ex": (c_int, [c_void_p, c_char_p, POINTER(ArrowArray),
+                                         POINTER(ArrowSchema), c_int32, c_char_p, c_size_t,
+                                         ctypes.c_uint32]),
+    "dora_node_send_output_bytes_ex": (c_int, [c_void_p, c_char_p, c_void_p, c_size_t, c_int32,
+                                               c_char_p, c_size_t, ctypes.c_uint32]),
+    "dora_node_set_async_sends": (c_int, [c_void_p, c_int]),
     "dora_node_close_outputs": (c_int, [c_void_p, POINTER(c_char_p), c_size_t]),
     "dora_node_next_event": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
     "dora_event_type": (c_int, [c_void_p]),

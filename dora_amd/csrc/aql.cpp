@@ -53,6 +53,13 @@ struct Use {
 
 constexpr int kMaxQueues = 8;
 
+// The kernels of the embedded code object, in AqlQueue::kobj order.
+constexpr int kKernels = 7;
+constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4",   "dora_aql_pack_u8",
+                                                "dora_aql_pack1_u4",  "dora_aql_pack1_u8",
+                                                "dora_aql_pack1c_u4", "dora_aql_packc_u4",
+                                                "dora_aql_pack1p_u4"};
+
 struct AqlQueue {
   std::mutex mu;
   hsa_agent_t gpu{};
@@ -65,9 +72,9 @@ struct AqlQueue {
   hsa_queue_t* qs[kMaxQueues] = {};
   uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
   int nq = 0;
-  // u4, u8, pack1_u4, pack1_u8, pack1c_u4, packc_u4
-  uint64_t kobj[6] = {0, 0, 0, 0, 0, 0};
-  uint32_t group[6] = {0, 0, 0, 0, 0, 0}, priv[6] = {0, 0, 0, 0, 0, 0};
+  // u4, u8, pack1_u4, pack1_u8, pack1c_u4, packc_u4, pack1p_u4 (kKernelNames)
+  uint64_t kobj[7] = {};
+  uint32_t group[7] = {}, priv[7] = {};
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
   uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
@@ -77,6 +84,11 @@ struct AqlQueue {
   bool profiling = false;
   std::vector<hsa_signal_t> free_sigs, used_sigs;
   uint64_t ts_freq = 0;
+  uint64_t dispatched[7] = {};  // packets per kernel (kKernelNames order)
+  // test tool (bar_alloc): the GPU's coarse-grained pool, host-accessible through the BAR
+  hsa_agent_t cpu{};
+  hsa_amd_memory_pool_t coarse{};
+  bool coarse_ok = false;
 };
 
 namespace {
@@ -132,6 +144,22 @@ hsa_status_t on_pool(hsa_amd_memory_pool_t pool, void* p) {
   return HSA_STATUS_SUCCESS;
 }
 
+hsa_status_t on_coarse_pool(hsa_amd_memory_pool_t pool, void* p) {
+  auto* out = static_cast<std::pair<hsa_amd_memory_pool_t, bool>*>(p);
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL || out->second) return HSA_STATUS_SUCCESS;
+  bool alloc = false;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if (alloc && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED)) {
+    out->first = pool;
+    out->second = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 hsa_status_t on_cpu_pool(hsa_amd_memory_pool_t pool, void* p) {
   Agents* f = static_cast<Agents*>(p);
   hsa_amd_segment_t seg;
@@ -146,17 +174,25 @@ hsa_status_t on_cpu_pool(hsa_amd_memory_pool_t pool, void* p) {
   return HSA_STATUS_SUCCESS;
 }
 
-// DORA_GPU_AQL_COHERENT (aql_pack): single-segment packs read their sources with agent-coherent
-// loads and carry no acquire fence (default; 0 = plain loads behind the fence).  "all" does the
-// same for multi-segment packs, which then copy their arguments from the device ring into LDS
-// with coherent loads first: one dependent memory round trip at every workgroup's start made C3
-// slower, 4.50 -> 4.89-5.23 us per cloud (profiles/r02_coherent_c3_ab.jsonl), so it is a knob.
+// DORA_GPU_AQL_COHERENT (aql_pack).  Default (0, r03): every pack reads its sources with
+// non-temporal loads behind the packet's agent-scope acquire fence.  "1": single-segment packs
+// read with agent-coherent loads (dora_aql_pack1c_u4) and carry no acquire fence (the r02
+// default; 4 MB -8 %, 1 MB -15 % per message, profiles/r02_coherent_ab.jsonl).  r03 could not
+// make a source rewritten between sends read stale without the fence — host BAR stores, SDMA
+// and blit copies, with the source's lines loaded into every L2 and into the L1s of the CUs of
+// 256 earlier packs, even with L1-cached loads (tests/test_gpu_fence.py) — so there is no
+// evidence the fence is needed, and none that it is not: it stays on by default, and "1" is for
+// senders that know their sources are fresh.  "all" does the same for multi-segment packs, which
+// then copy their arguments from the device ring into LDS with coherent loads first: one
+// dependent memory round trip at every workgroup's start made C3 slower, 4.50 -> 4.89-5.23 us
+// per cloud (profiles/r02_coherent_c3_ab.jsonl), so it is a knob.
 int coherent_level() {
   static const int v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_COHERENT");
-    if (e && *e == '0') return 0;
+    if (e && *e == '1') return 1;
     if (e && std::string(e) == "all") return 2;
-    return 1;
+    if (e && std::string(e) == "plain") return -1;
+    return 0;
   }();
   return v;
 }
@@ -232,12 +268,11 @@ AqlQueue* create(int device) {
     delete a;
     return note("code object");
   }
-  const char* names[6] = {"dora_aql_pack_u4.kd", "dora_aql_pack_u8.kd", "dora_aql_pack1_u4.kd",
-                          "dora_aql_pack1_u8.kd", "dora_aql_pack1c_u4.kd", "dora_aql_packc_u4.kd"};
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < kKernels; ++k) {
     hsa_executable_symbol_t sym;
     uint32_t ka = 0;
-    if (hsa_executable_get_symbol_by_name(exe, names[k], &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
+    const std::string sym_name = std::string(kKernelNames[k]) + ".kd";
+    if (hsa_executable_get_symbol_by_name(exe, sym_name.c_str(), &f.gpu, &sym) != HSA_STATUS_SUCCESS ||
         hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT,
                                        &a->kobj[k]) != HSA_STATUS_SUCCESS ||
         hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE,
@@ -297,6 +332,11 @@ AqlQueue* create(int device) {
     }
   }
   hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &a->ts_freq);
+  a->cpu = f.cpu;
+  std::pair<hsa_amd_memory_pool_t, bool> coarse{{}, false};
+  hsa_amd_agent_iterate_memory_pools(f.gpu, on_coarse_pool, &coarse);
+  a->coarse = coarse.first;
+  a->coarse_ok = coarse.second;
   return a;
 }
 
@@ -455,17 +495,16 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   }
   hsa_queue_store_write_index_relaxed(q, idx + 1);
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  // Single-segment packs read their source with agent-coherent loads (dora_aql_pack1c_u4: sc1,
-  // the scope LLVM's gfx942 memory model gives relaxed agent-scope atomic loads) and their packets
-  // carry no acquire fence (below): the fence's L2 invalidation is what kept a source line an
-  // earlier pack left in an L2 from being served after a writer on another XCD replaced it, and
-  // coherent loads never take such a line.  Their arguments are preloaded into SGPRs by the
-  // command processor, so no kernarg line can be stale either.  Interleaved A/B on one box, sources
-  // rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 -> 1.23-1.26 us per
-  // message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.  DORA_GPU_AQL_COHERENT=0:
-  // plain loads behind the acquire fence (A/B knob).
+  // DORA_GPU_AQL_COHERENT=1 (coherent_level): single-segment packs read their source with
+  // agent-coherent loads (dora_aql_pack1c_u4: sc1 nt, bypassing the CU's L1 like the default's nt
+  // loads) and their packets carry no acquire fence (below); their arguments are preloaded into
+  // SGPRs by the command processor, so no kernarg line can be stale either.  Interleaved A/B on
+  // one box, sources rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 ->
+  // 1.23-1.26 us per message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.
   const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi;
-  const int k = coh ? (one ? 4 : 5) : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
+  const int k = coh                                        ? (one ? 4 : 5)
+                : (one && coherent_level() < 0 && unroll == 4) ? 6
+                                                               : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
@@ -512,7 +551,53 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   u.flag = flag_host;
   u.epoch = sig.epoch;
   ++a->next;
+  ++a->dispatched[k];
   return DORA_OK;
+}
+
+int bar_alloc(int device, size_t bytes, void** out) {
+  AqlQueue* a = aql_queue(device);
+  if (!a || !a->coarse_ok) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue / coarse-grained pool");
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(a->coarse, bytes, 0, &p) != HSA_STATUS_SUCCESS)
+    return fail(DORA_ERR_HIP, "hsa_amd_memory_pool_allocate");
+  if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return fail(DORA_ERR_UNSUPPORTED, "host access to device memory (no large BAR)");
+  }
+  *out = p;
+  return DORA_OK;
+}
+
+int bar_write(int device, void* dst, const void* src, size_t bytes) {
+  AqlQueue* a = aql_queue(device);
+  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue");
+  std::memcpy(dst, src, bytes);
+  __builtin_ia32_sfence();
+  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
+  // a read-back of the last line: the posted writes have reached the memory
+  if (bytes) (void)*reinterpret_cast<volatile uint8_t*>(static_cast<uint8_t*>(dst) + bytes - 1);
+  return DORA_OK;
+}
+
+void bar_free(void* p) {
+  if (p) hsa_amd_memory_pool_free(p);
+}
+
+size_t aql_kernel_count() { return kKernels; }
+
+const char* aql_kernel_name(size_t k) { return k < size_t(kKernels) ? kKernelNames[k] : nullptr; }
+
+uint64_t aql_dispatched(int device, size_t k) {
+  if (k >= size_t(kKernels) || device < 0 || device >= 64) return 0;
+  AqlQueue* a;
+  {
+    std::lock_guard<std::mutex> g(g_queues_mu);
+    a = g_queues[device];
+  }
+  if (!a) return 0;
+  std::lock_guard<std::mutex> g(a->mu);
+  return a->dispatched[k];
 }
 
 int aql_profile_enable(AqlQueue* a, bool on) {

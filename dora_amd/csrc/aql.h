@@ -42,6 +42,19 @@ void aql_forget_flags(int device, const void* base, size_t size);
 // frees of device memory (dora_gpu_free, device array release) call this first.
 void aql_fence_all();
 
+// Diagnostics: the kernels of the AQL code object and the packets dispatched per kernel in
+// this process on `device` (dora_gpu_aql_dispatch_counts).
+size_t aql_kernel_count();
+const char* aql_kernel_name(size_t k);
+uint64_t aql_dispatched(int device, size_t k);
+
+// Test tool (tests/fence_probe.py): device memory of the GPU's coarse-grained pool that the host
+// writes directly through the BAR (bar_write: stores + HDP flush + read-back), i.e. behind every
+// XCD's L2 — the writer a pack without an acquire fence cannot see.
+int bar_alloc(int device, size_t bytes, void** out);
+int bar_write(int device, void* dst, const void* src, size_t bytes);
+void bar_free(void* p);
+
 // Segments one AQL dispatch takes.
 size_t aql_max_segments();
 

@@ -81,3 +81,11 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_packc_u4(const A
   __syncthreads();
   dora::pack::pack_body<4, dora::pack::kCoherent>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
 }
+
+// Test kernel: as dora_aql_pack1_u4 with PLAIN (L1-cached) source loads.  Selected only by
+// DORA_GPU_AQL_COHERENT=plain, for the acquire fence's negative control (tests/test_gpu_fence.py).
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1p_u4(
+    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
+    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
+  pack1<4, dora::pack::kPlainSrc>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
+}

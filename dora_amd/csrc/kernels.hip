@@ -227,6 +227,21 @@ __global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t* __restrict__ p,
   }
 }
 
+// Test tool (the acquire-fence negative control, tests/test_gpu_fence.py): every workgroup reads
+// all of [p, p + n) with plain cached loads, so that each XCD's L2 ends up holding the lines
+// (one workgroup per CU: 32 per XCD, dispatched round robin over the XCDs).  The reduction is
+// stored only under a condition the data never meets, so the loads cannot be elided.
+__global__ __launch_bounds__(kThreads) void l2_touch_kernel(const uint8_t* __restrict__ p,
+                                                            uint64_t n, uint32_t* __restrict__ sink) {
+  const uint64_t nu = n / 16;
+  uint32_t x = 0;
+  for (uint64_t i = threadIdx.x; i < nu; i += kThreads) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p + 16 * i);
+    x ^= w[0] ^ w[1] ^ w[2] ^ w[3];
+  }
+  if (x == 0x5EEDF00Du && n == 1) sink[blockIdx.x] = x;
+}
+
 unsigned grid_for(uint64_t items) {
   uint64_t g = (items + kThreads - 1) / kThreads;
   return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 4096)));
@@ -504,6 +519,17 @@ int launch_csum(const void* data, size_t len, uint64_t* out_dev, hipStream_t str
   return DORA_OK;
 }
 
+int launch_l2_touch(const void* p, size_t len, hipStream_t stream) {
+  if (len < 16) return DORA_OK;
+  int cus = 0, dev = 0;
+  DORA_HIP(hipGetDevice(&dev));
+  DORA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  hipLaunchKernelGGL(l2_touch_kernel, dim3(std::max(cus, 1)), dim3(kThreads), 0, stream,
+                     static_cast<const uint8_t*>(p), uint64_t(len), nullptr);
+  DORA_HIP(hipGetLastError());
+  return DORA_OK;
+}
+
 int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
   if (!len) return DORA_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
@@ -581,6 +607,11 @@ int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uin
   }
   (void)hipFree(d);
   return rc;
+}
+
+int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream) {
+  if (!data && len) return dora::fail(DORA_ERR_INVALID, "data is NULL");
+  return dora::launch_l2_touch(data, len, static_cast<hipStream_t>(stream));
 }
 
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream) {

@@ -28,6 +28,7 @@
 #include <memory>
 #include <memory_resource>
 #include <mutex>
+#include <thread>
 #include <set>
 #include <sstream>
 #include <string>
@@ -658,6 +659,9 @@ struct dora_node {
   uint64_t phase_ns[4] = {0, 0, 0, 0};
   uint64_t phase_count = 0;
   bool compact = false;                     // send_output uses compacting plans
+  // DORA_SEND_ASYNC for every send (DORA_GPU_SEND_ASYNC=1): device-source sends return before
+  // their pack has read the source
+  bool async_default = false;
   // Plans of recent device-array sends by plan_key (a sender re-sending the same buffers, e.g. a
   // ring of preallocated frames, plans each once): the plan and its serialized type info
   struct CachedPlan {
@@ -1686,8 +1690,43 @@ void form_bcast_groups(dora_node* n) {
   }
 }
 
+// What a synchronous send of a device source waits for: the pack has read the whole source.
+struct SourceWait {
+  uint8_t kind = FILL_DONE;  // FILL_FLAG: flag >= epoch; FILL_EVENT: event; FILL_BCAST: stream
+  const std::atomic<uint64_t>* flag = nullptr;
+  uint64_t epoch = 0;
+  hipEvent_t event = nullptr;
+};
+
+// The reference copies a source inside send_output (arrow_utils.rs:48, node/mod.rs:206-209), so
+// its caller may rewrite the source as soon as the call returns.  A device source is read by the
+// pack kernel after the call has queued it; without DORA_SEND_ASYNC the call waits for that pack
+// (spin, then yield; bounded) — after the descriptor has left, so receivers are not delayed.
+int wait_source_read(dora_node* n, const SourceWait& w) {
+  SubSpan sp(SP_SEND_SOURCE_WAIT);
+  if (w.kind == FILL_FLAG && w.flag) {
+    const uint64_t t0 = mono_ns();
+    uint32_t spins = 0;
+    while (w.flag->load(std::memory_order_acquire) < w.epoch) {
+      if (++spins < 4096) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      const uint64_t dt = mono_ns() - t0;
+      if (dt > 10000000000ull) return fail(DORA_ERR_TIMEOUT, "pack did not read its source in 10 s");
+      if (dt > 200000) std::this_thread::yield();
+    }
+  } else if (w.kind == FILL_EVENT && w.event) {
+    DORA_HIP(hipEventSynchronize(w.event));
+  } else if (w.kind == FILL_BCAST) {
+    DORA_HIP(hipStreamSynchronize(n->core->stream));
+  }
+  return DORA_OK;
+}
+
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
-                  size_t params_len, const std::vector<uint8_t>* ti_pre = nullptr) {
+                  size_t params_len, const std::vector<uint8_t>* ti_pre = nullptr,
+                  uint32_t flags = 0) {
   dora_sample* s = nullptr;
   const uint64_t t0 = mono_ns();
   int rc = alloc_sample(n, plan->size, &s, plan->fill_size());
@@ -1745,7 +1784,17 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   sp_ti.stop();
   DropToken tok{};
   const bool traced = trace_enabled() && s->slot;
+  SourceWait wait;
+  const bool sync_src = plan->dev == ARROW_DEVICE_ROCM && s->slot && plan->size &&
+                        !((flags & DORA_SEND_ASYNC) || n->async_default);
+  if (sync_src) {
+    wait.kind = n->bcast_out.count(output_id) ? uint8_t(FILL_BCAST) : s->fill;
+    wait.epoch = s->epoch;
+    if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
+    if (s->fill == FILL_EVENT) wait.event = s->slot->done;
+  }
   rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
+  if (rc == DORA_OK && sync_src) rc = wait_source_read(n, wait);
   const uint64_t t4 = mono_ns();
   if (traced && rc == DORA_OK) {
     const uint64_t off = now_ns() - mono_ns();  // mono -> realtime for the trace
@@ -1850,6 +1899,7 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   }
 
   auto* n = new dora_node();
+  if (const char* e = std::getenv("DORA_GPU_SEND_ASYNC")) n->async_default = *e == '1';
   n->core = core;
   n->id = node_id;
   for (auto& o : dora::split(e.outputs, ',')) n->outputs.insert(o);
@@ -2024,6 +2074,12 @@ int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint
 int dora_node_send_output(dora_node* n, const char* output_id, const struct ArrowArray* array,
                           const struct ArrowSchema* schema, ArrowDeviceType device_type,
                           const uint8_t* params, size_t params_len) {
+  return dora_node_send_output_ex(n, output_id, array, schema, device_type, params, params_len, 0);
+}
+
+int dora_node_send_output_ex(dora_node* n, const char* output_id, const struct ArrowArray* array,
+                             const struct ArrowSchema* schema, ArrowDeviceType device_type,
+                             const uint8_t* params, size_t params_len, uint32_t flags) {
   if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
   const bool device = device_type == ARROW_DEVICE_ROCM && n->core->device >= 0;
@@ -2040,7 +2096,7 @@ int dora_node_send_output(dora_node* n, const char* output_id, const struct Arro
       if (e.key == n->plan_key_buf) {
         e.last_use = ++n->plan_clock;
         ++n->plan_hits;
-        return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti);
+        return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti, flags);
       }
       keyed = false;  // a hash collision: plan this one afresh, uncached
     }
@@ -2075,17 +2131,17 @@ int dora_node_send_output(dora_node* n, const char* output_id, const struct Arro
     dora::serialize_type_info(plan->root, e.ti);
     e.last_use = ++n->plan_clock;
     n->plan_index[h] = slot;
-    return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti);
+    return dora::pack_and_send(n, output_id, e.plan, params, params_len, &e.ti, flags);
   }
-  rc = dora::pack_and_send(n, output_id, plan, params, params_len);
+  rc = dora::pack_and_send(n, output_id, plan, params, params_len, nullptr, flags);
   delete plan;
   return rc;
   DORA_GUARD_END
 }
 
-int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void* data, size_t len,
-                                ArrowDeviceType device_type, const uint8_t* params,
-                                size_t params_len) {
+int dora_node_send_output_bytes_ex(dora_node* n, const char* output_id, const void* data,
+                                   size_t len, ArrowDeviceType device_type, const uint8_t* params,
+                                   size_t params_len, uint32_t flags) {
   if (!n || !output_id || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
   dora::SubSpan sp(dora::SP_SEND_PLAN);
@@ -2110,8 +2166,21 @@ int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void*
     n->bytes_ti_len = len;
   }
   sp.stop();
-  return dora::pack_and_send(n, output_id, &plan, params, params_len, &n->bytes_ti);
+  return dora::pack_and_send(n, output_id, &plan, params, params_len, &n->bytes_ti, flags);
   DORA_GUARD_END
+}
+
+int dora_node_send_output_bytes(dora_node* n, const char* output_id, const void* data, size_t len,
+                                ArrowDeviceType device_type, const uint8_t* params,
+                                size_t params_len) {
+  return dora_node_send_output_bytes_ex(n, output_id, data, len, device_type, params, params_len,
+                                        0);
+}
+
+int dora_node_set_async_sends(dora_node* n, int enable) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  n->async_default = enable != 0;
+  return DORA_OK;
 }
 
 int dora_node_set_compact(dora_node* n, int enable) {

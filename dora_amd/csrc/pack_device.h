@@ -85,6 +85,10 @@ typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // which never return a line another XCD's writer has since replaced, so the dispatch needs no
 // acquire fence (its L2 invalidation) to see a source rewritten since an earlier pack read it.
 constexpr int kCoherent = 4;
+// 5: as 2, but the source is read with PLAIN loads (L1-cached).  Test kernel only: the acquire
+// fence's negative control (tests/test_gpu_fence.py) — every shipped kernel reads sources with
+// nt or sc1 loads, which bypass the CU's L1 (MI355X_MICROARCH.md § visibility).
+constexpr int kPlainSrc = 5;
 // raw buffer loads: cache policy bits sc1 (16) | nt (2); resource word 3 as for gfx9 raw buffers
 constexpr int kCoherentPolicy = 16 | 2;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const uint8_t* p) {
@@ -102,16 +106,17 @@ __device__ __forceinline__ uint8_t ld1(const uint8_t* p) {
 
 template <int NT, bool DW = false>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  constexpr bool nt = NT != 0 && NT != kPlainSrc;
   if constexpr (DW) {  // p only 4-byte aligned
-    if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(p));
+    if constexpr (nt) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(p));
     return *reinterpret_cast<const u32x4_a4*>(p);
   }
-  if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  if constexpr (nt) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
   return *reinterpret_cast<const u32x4*>(p);
 }
 template <int NT>
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT == 2 || NT == kCoherent) {
+  if constexpr (NT == 2 || NT == kCoherent || NT == kPlainSrc) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
   } else if constexpr (NT == 3) {
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");

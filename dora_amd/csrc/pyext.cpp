@@ -127,13 +127,25 @@ PyObject* py_encode_parameters(PyObject*, PyObject* const* args, Py_ssize_t narg
   return PyBytes_FromStringAndSize(t_params.data(), Py_ssize_t(t_params.size()));
 }
 
-// send_bytes(handle, output_id, data_ptr, len, device_type, metadata) -> status
+// Optional trailing `flags` argument (DORA_SEND_ASYNC) of send_bytes / send_array.
+bool send_flags(PyObject* const* args, Py_ssize_t nargs, uint32_t* flags) {
+  *flags = 0;
+  if (nargs < 7) return true;
+  const unsigned long f = PyLong_AsUnsignedLong(args[6]);
+  if (f == static_cast<unsigned long>(-1) && PyErr_Occurred()) return false;
+  *flags = static_cast<uint32_t>(f);
+  return true;
+}
+
+// send_bytes(handle, output_id, data_ptr, len, device_type, metadata[, flags]) -> status
 PyObject* py_send_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-  if (nargs != 6) {
+  if (nargs != 6 && nargs != 7) {
     PyErr_SetString(PyExc_TypeError,
-                    "send_bytes(handle, output_id, data_ptr, len, device_type, metadata)");
+                    "send_bytes(handle, output_id, data_ptr, len, device_type, metadata[, flags])");
     return nullptr;
   }
+  uint32_t flags = 0;
+  if (!send_flags(args, nargs, &flags)) return nullptr;
   void *h = nullptr, *data = nullptr;
   if (!as_ptr(args[0], &h) || !as_ptr(args[2], &data)) return nullptr;
   const char* oid = as_cstr(args[1]);
@@ -146,20 +158,23 @@ PyObject* py_send_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   if (!encode(args[5], params)) return nullptr;
   int rc;
   Py_BEGIN_ALLOW_THREADS
-  rc = dora_node_send_output_bytes(static_cast<dora_node*>(h), oid, data, len,
-                                   static_cast<ArrowDeviceType>(dev),
-                                   reinterpret_cast<const uint8_t*>(params.data()), params.size());
+  rc = dora_node_send_output_bytes_ex(static_cast<dora_node*>(h), oid, data, len,
+                                      static_cast<ArrowDeviceType>(dev),
+                                      reinterpret_cast<const uint8_t*>(params.data()),
+                                      params.size(), flags);
   Py_END_ALLOW_THREADS
   return PyLong_FromLong(rc);
 }
 
-// send_array(handle, output_id, array_addr, schema_addr, device_type, metadata) -> status
+// send_array(handle, output_id, array_addr, schema_addr, device_type, metadata[, flags])
 PyObject* py_send_array(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-  if (nargs != 6) {
-    PyErr_SetString(PyExc_TypeError,
-                    "send_array(handle, output_id, array_addr, schema_addr, device_type, metadata)");
+  if (nargs != 6 && nargs != 7) {
+    PyErr_SetString(PyExc_TypeError, "send_array(handle, output_id, array_addr, schema_addr, "
+                                     "device_type, metadata[, flags])");
     return nullptr;
   }
+  uint32_t flags = 0;
+  if (!send_flags(args, nargs, &flags)) return nullptr;
   void *h = nullptr, *arr = nullptr, *sch = nullptr;
   if (!as_ptr(args[0], &h) || !as_ptr(args[2], &arr) || !as_ptr(args[3], &sch)) return nullptr;
   const char* oid = as_cstr(args[1]);
@@ -170,11 +185,12 @@ PyObject* py_send_array(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   if (!encode(args[5], params)) return nullptr;
   int rc;
   Py_BEGIN_ALLOW_THREADS
-  rc = dora_node_send_output(static_cast<dora_node*>(h), oid,
-                             static_cast<const struct ArrowArray*>(arr),
-                             static_cast<const struct ArrowSchema*>(sch),
-                             static_cast<ArrowDeviceType>(dev),
-                             reinterpret_cast<const uint8_t*>(params.data()), params.size());
+  rc = dora_node_send_output_ex(static_cast<dora_node*>(h), oid,
+                                static_cast<const struct ArrowArray*>(arr),
+                                static_cast<const struct ArrowSchema*>(sch),
+                                static_cast<ArrowDeviceType>(dev),
+                                reinterpret_cast<const uint8_t*>(params.data()), params.size(),
+                                flags);
   Py_END_ALLOW_THREADS
   return PyLong_FromLong(rc);
 }

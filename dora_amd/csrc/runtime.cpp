@@ -85,6 +85,30 @@ int dora_gpu_busy_stats(uint64_t* idle_ns, uint64_t* fill_wait_ns) {
   return DORA_OK;
 }
 
+int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_t* n) {
+  const size_t k = dora::aql_kernel_count();
+  if (n) *n = k;
+  for (size_t i = 0; i < k && i < cap && counts; ++i) counts[i] = dora::aql_dispatched(device, i);
+  return DORA_OK;
+}
+
+int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
+  return dora::bar_alloc(device, bytes, out);
+}
+
+int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes) {
+  if ((!dst || !src) && bytes) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  return dora::bar_write(device, dst, src, bytes);
+}
+
+void dora_gpu_test_bar_free(void* ptr) { dora::bar_free(ptr); }
+
+const char* dora_gpu_aql_kernel_name(size_t k) {
+  const char* s = dora::aql_kernel_name(k);
+  return s ? s : "";
+}
+
 int dora_gpu_device_count(int* count) {
   if (!count) return dora::fail(DORA_ERR_INVALID, "count is NULL");
   DORA_HIP(hipGetDeviceCount(count));

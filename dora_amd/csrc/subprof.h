@@ -32,6 +32,7 @@ enum SubPhase : int {
   SP_DAEMON_ROUTE,    // daemon: one request handled
   SP_SLOT_FLAG,       // allocate_slot: the reused slot's last-fill check
   SP_SAMPLE_NEW,      // alloc_sample: the sample object
+  SP_SEND_SOURCE_WAIT,  // pack_and_send: a synchronous send waits for its pack to read the source
   SP_COUNT
 };
 

@@ -84,7 +84,7 @@ const char* const kSubNames[SP_COUNT] = {
     "aql_pack",     "aql_args",     "aql_dispatch", "send_ti",       "send_tokens",
     "send_lookup",  "send_request", "send_track",   "recv_drain",    "recv_encode",
     "recv_dropold", "recv_finish",  "recv_release", "daemon_route",  "slot_flag",
-    "sample_new"};
+    "sample_new",   "send_source_wait"};
 
 struct SubProf {
   const bool on = g_subprof_on;

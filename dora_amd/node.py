@@ -22,6 +22,8 @@ from typing import Optional
 from . import _lib
 from ._lib import ARROW_DEVICE_CPU, ARROW_DEVICE_ROCM, DoraGpuError, call, load
 from .arrow_c import ArrowArray, ArrowSchema, CArray
+
+SEND_ASYNC = 1  # DORA_SEND_ASYNC (include/dora_gpu.h)
 from .device import DeviceArray, DeviceBuffer
 from .type_info import decode
 
@@ -147,17 +149,24 @@ class Node:
         self.device = device if device is not None else int(os.environ.get("DORA_GPU_DEVICE", "0"))
 
     # -------------------------------------------------------------------------------- sending
-    def send_output(self, output_id: str, data, metadata: Optional[dict] = None):
+    def send_output(self, output_id: str, data, metadata: Optional[dict] = None, *,
+                    asynchronous: bool = False):
+        """send_output (apis/python/node/src/lib.rs:157-185).  Returns once the sample no longer
+        needs `data`, as the reference (which copies inside the call): a device source's pack
+        has read it.  `asynchronous=True` (DORA_SEND_ASYNC) returns as soon as the pack is
+        queued; the caller then must not write a device source until `sync()`, or only by work
+        queued on `stream` fetched after the send."""
+        f = SEND_ASYNC if asynchronous else 0
         if isinstance(data, DeviceArray):
             a, s = data.send_addrs()
-            rc = _fast.send_array(self.handle, output_id, a, s, ARROW_DEVICE_ROCM, metadata)
+            rc = _fast.send_array(self.handle, output_id, a, s, ARROW_DEVICE_ROCM, metadata, f)
         elif isinstance(data, (bytes, bytearray, memoryview)):
             buf = ctypes.create_string_buffer(bytes(data), len(data))
             rc = _fast.send_bytes(self.handle, output_id, ctypes.addressof(buf), len(data),
                                   ARROW_DEVICE_CPU, metadata)
         elif isinstance(data, DeviceBuffer):
             rc = _fast.send_bytes(self.handle, output_id, data.ptr, data.size, ARROW_DEVICE_ROCM,
-                                  metadata)
+                                  metadata, f)
         elif hasattr(data, "_export_to_c"):
             with CArray.from_pyarrow(data) as c:
                 rc = _fast.send_array(self.handle, output_id, ctypes.addressof(c.array),
@@ -167,10 +176,20 @@ class Node:
         if rc:
             _lib.check(rc)
 
+    def send_output_async(self, output_id: str, data, metadata: Optional[dict] = None):
+        """send_output(..., asynchronous=True)."""
+        self.send_output(output_id, data, metadata, asynchronous=True)
+
+    def set_async_sends(self, enable: bool = True):
+        """Make every send of this node asynchronous (dora_node_set_async_sends)."""
+        call("dora_node_set_async_sends", self.handle, int(enable))
+
     def send_output_device_bytes(self, output_id: str, ptr: int, n: int,
-                                 metadata: Optional[dict] = None):
-        """send_output_raw with an HBM source: one pack kernel into a fresh device sample."""
-        rc = _fast.send_bytes(self.handle, output_id, ptr, n, ARROW_DEVICE_ROCM, metadata)
+                                 metadata: Optional[dict] = None, *, asynchronous: bool = False):
+        """send_output_raw with an HBM source: one pack kernel into a fresh device sample;
+        returns once the pack has read the source unless `asynchronous` (send_output)."""
+        rc = _fast.send_bytes(self.handle, output_id, ptr, n, ARROW_DEVICE_ROCM, metadata,
+                              SEND_ASYNC if asynchronous else 0)
         if rc:
             _lib.check(rc)
 

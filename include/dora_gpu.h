@@ -89,6 +89,12 @@ const char* dora_gpu_version(void);
  * rings (node event/drop rings, the daemon's request rings) and spent spinning on producers'
  * fill flags, in ns since start.  Busy time = wall - idle locates a pipeline's bottleneck. */
 int dora_gpu_busy_stats(uint64_t* idle_ns, uint64_t* fill_wait_ns);
+/* Diagnostics (no reference counterpart): raw AQL packets this process dispatched on HIP device
+ * `device`, per kernel of the embedded pack code object (min(cap, *n) entries written; *n = the
+ * kernel count), and kernel k's symbol name ("" past the end).  The driver's smoke names the
+ * kernels that packed its samples with these. */
+int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_t* n);
+const char* dora_gpu_aql_kernel_name(size_t k);
 
 int dora_gpu_device_count(int* count);
 int dora_gpu_set_device(int ordinal);
@@ -210,6 +216,16 @@ int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream
 int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uint64_t* out);
 /* Fill `len` device bytes with the splitmix64 stream of `seed` (BASELINE.md §2 payloads). */
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream);
+/* Test tool (no reference counterpart): one workgroup per CU reads all of [data, data + len)
+ * with plain cached loads, leaving the lines in every XCD's L2 (the acquire-fence negative
+ * control of tests/test_gpu_fence.py). */
+int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream);
+/* Test tools (no reference counterpart): device memory of `device`'s coarse-grained pool that
+ * the host writes directly through the PCIe BAR (stores + HDP flush + read-back), behind every
+ * XCD's L2 — the source rewrite of the acquire-fence negative control. */
+int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
+int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
+void dora_gpu_test_bar_free(void* ptr);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Node API — replaces DoraNode / EventStream (apis/rust/node/src/node/mod.rs:42-503,         */
@@ -255,16 +271,36 @@ int dora_node_send_output_sample(dora_node* node, const char* output_id, const u
                                  size_t type_info_len, const uint8_t* params, size_t params_len,
                                  dora_sample* sample);
 /* send_output (mod.rs:198-215): plan + allocate + HIP pack + send.  `device_type` as in
- * dora_gpu_plan. */
+ * dora_gpu_plan.  Like the reference, which copies the array inside the call
+ * (arrow_utils.rs:48), the call returns once the sample no longer needs the source: for a
+ * device source it waits (after the descriptor has left) until the pack kernel has read it, so
+ * the caller may rewrite or free the source on any stream right away. */
 int dora_node_send_output(dora_node* node, const char* output_id, const struct ArrowArray* array,
                           const struct ArrowSchema* schema, ArrowDeviceType device_type,
                           const uint8_t* params, size_t params_len);
 /* send_output_raw / send_output_bytes (mod.rs:180-196, 217-228): `len` bytes as
  * ArrowTypeInfo::byte_array, copied into a device sample (kernel for HBM sources, DMA for host
- * sources).  This is the benchmark's send path (examples/benchmark/node/src/main.rs:46-48). */
+ * sources); returns once the source has been read, as dora_node_send_output.  This is the
+ * benchmark's send path (examples/benchmark/node/src/main.rs:46-48). */
 int dora_node_send_output_bytes(dora_node* node, const char* output_id, const void* data,
                                 size_t len, ArrowDeviceType device_type, const uint8_t* params,
                                 size_t params_len);
+/* Flags of the _ex variants (no reference counterpart). */
+#define DORA_SEND_ASYNC 1u /* return before the pack has read a device source (below) */
+/* dora_node_send_output / _bytes with `flags`.  With DORA_SEND_ASYNC a device-source send
+ * returns as soon as its pack is queued: the caller must not write the source until the pack
+ * has read it — i.e. until dora_node_sync(), or only by work queued on dora_node_stream()
+ * fetched after the send (which orders every fill launched so far before it).  Senders that
+ * never rewrite their sources (frame rings, the benchmark) overlap packs this way; a host
+ * source is always safe to reuse on return. */
+int dora_node_send_output_ex(dora_node* node, const char* output_id, const struct ArrowArray* array,
+                             const struct ArrowSchema* schema, ArrowDeviceType device_type,
+                             const uint8_t* params, size_t params_len, uint32_t flags);
+int dora_node_send_output_bytes_ex(dora_node* node, const char* output_id, const void* data,
+                                   size_t len, ArrowDeviceType device_type, const uint8_t* params,
+                                   size_t params_len, uint32_t flags);
+/* Make DORA_SEND_ASYNC the default of every send of this node (also DORA_GPU_SEND_ASYNC=1). */
+int dora_node_set_async_sends(dora_node* node, int enable);
 /* Use compacting plans (dora_gpu_plan_compact) in dora_node_send_output for device arrays. */
 int dora_node_set_compact(dora_node* node, int enable);
 /* close_outputs (mod.rs:277-289). */

@@ -140,6 +140,9 @@ def test_aql_kernel_name_follows_the_coherent_knob(monkeypatch):
     import bench
     monkeypatch.delenv("DORA_GPU_AQL_COHERENT", raising=False)
     monkeypatch.delenv("DORA_GPU_PACK_VARIANT", raising=False)
+    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u4 (AQL)"
+    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
+    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "1")
     assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
     assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
     monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "all")

@@ -494,6 +494,7 @@ def test_default_queue_keeps_up_with_async_burst(launcher, tmp_path):
     warm = 40  # slots created and mapped (milliseconds each) before the burst
     with Dataflow(_bench_desc(res, queue_size=10), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(True)  # DORA_SEND_ASYNC: the contract under test
         for k in range(warm):
             node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size, {"seq": k})
         node.send_output("data", b"", {"seq": warm, "ack": True})
@@ -532,6 +533,7 @@ def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
     bufs, sums = _distinct_sources(nsrc, size)
     with Dataflow(_bench_desc(res, queue_size=1), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(True)  # DORA_SEND_ASYNC: the contract under test
         for k in range(n_msgs):
             node.send_output_device_bytes("data", bufs[k % nsrc].ptr, size,
                                           {"seq": k, "csum": sums[k % nsrc], "verify": True})
@@ -585,6 +587,7 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer):
     src = device.DeviceBuffer(size)
     with Dataflow(_bench_desc(res), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(True)  # DORA_SEND_ASYNC: the contract under test
         for k in range(n_msgs):
             # dora_node_stream orders every fill launched so far (the previous pack still reading
             # `src`) before the work queued on it next: the rewrite
@@ -609,6 +612,117 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer):
     assert sum(x["mismatches"] for x in out["series"]) == 0, out
     assert sum(x["verified"] for x in out["series"]) == n_msgs
     assert paths["aql"] >= n_msgs, paths
+
+
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_path, mode):
+    """The reference copies inside send_output (arrow_utils.rs:48, node/mod.rs:206-209): the
+    caller may rewrite its buffer as soon as the call returns.  Here the source is rewritten by
+    a kernel on a stream the library knows nothing about, right after every send returns, with
+    no synchronisation.  The default (synchronous) send must deliver every sample bit-exact;
+    DORA_SEND_ASYNC makes no such promise (its contract: rewrite only via dora_node_stream or
+    after dora_node_sync), and its count of corrupted samples is only reported."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    n_msgs, size = 200, 1 << 20
+    s = device.Stream()
+    scratch = device.DeviceBuffer(size)
+    sums = []
+    for k in range(n_msgs + 1):
+        device.fill_splitmix(scratch.ptr, size, 0xFACE00 + k, s)
+        sums.append(to_i64(device.csum64(scratch.ptr, size, s)))
+    scratch.free()
+    src = device.DeviceBuffer(size)
+    other = device.Stream()   # unrelated to the node: no ordering with its fills
+    device.fill_splitmix(src.ptr, size, 0xFACE00, other)
+    other.sync()
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        for k in range(n_msgs):
+            node.send_output_device_bytes("data", src.ptr, size,
+                                          {"seq": k, "csum": sums[k], "verify": True},
+                                          asynchronous=mode == "async")
+            device.fill_splitmix(src.ptr, size, 0xFACE00 + k + 1, other)  # no sync
+        other.sync()
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    src.free()
+    s.close()
+    other.close()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    bad = sum(x["mismatches"] for x in out["series"])
+    assert sum(x["verified"] for x in out["series"]) == n_msgs
+    print(f"{mode}: {bad} of {n_msgs} samples corrupted by the rewrite")
+    if mode == "sync":
+        assert bad == 0, out
+
+
+def test_device_array_send_waits_for_its_source(launcher):
+    """send_output of a DeviceArray (the Python node API, a multi-segment pack) returns once the
+    pack has read the array: both child buffers of a Struct<x,y:i64> are overwritten on an
+    unrelated stream right after each send, and every array arrives with its own checksum."""
+    import ctypes
+    import numpy as np
+    import pyarrow as pa
+    from dora_amd import device
+    from dora_amd._lib import call
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from dora_amd.verify import to_u64
+    from oracle.arrow_ffi import import_array
+    from oracle.checksum_ref import regions_csum
+    from oracle.pack_ref import node_regions
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["pc"], "inputs": {"result": "recv/result"}},
+        {"id": "recv", "path": sys.executable,
+         "args": [os.path.join(ROOT, "examples", "verify_receiver.py")],
+         "inputs": {"pc": {"source": "src/pc", "queue_size": 100}}, "outputs": ["result"]},
+    ]}
+    n, k_msgs = 1 << 18, 16
+    rng = np.random.default_rng(5)
+    arrs = [pa.StructArray.from_arrays([pa.array(rng.integers(-2**62, 2**62, n)),
+                                        pa.array(rng.integers(-2**62, 2**62, n))],
+                                       names=["x", "y"]) for _ in range(k_msgs)]
+    want = [regions_csum(node_regions(import_array(a))) for a in arrs]
+    devs = [DeviceArray.from_pyarrow(a) for a in arrs]
+
+    def child_values(da, c):
+        child = da.array.children[c].contents
+        return ctypes.cast(child.buffers, ctypes.POINTER(ctypes.c_void_p))[1]
+    other = device.Stream()
+    with Dataflow(desc, launcher=launcher) as df:
+        node = Node("src", dataflow=df.shm, device=0)
+        with DeviceArray.from_pyarrow(arrs[0]) as da:
+            for seq in range(k_msgs):
+                node.send_output("pc", da, {"seq": seq})
+                if seq + 1 < k_msgs:   # the next array's bytes into the sent one's buffers, no sync
+                    for c in range(2):
+                        call("dora_gpu_memcpy_async", child_values(da, c),
+                             child_values(devs[seq + 1], c), 8 * n, other.handle)
+            other.sync()
+            results = {}
+            deadline = time.time() + 120
+            while len(results) < k_msgs and time.time() < deadline:
+                ev = node.next(timeout=5)
+                if ev is None:
+                    break
+                if ev["type"] == "INPUT":
+                    results[ev["metadata"]["seq"]] = ev["metadata"]
+        node.close()
+        codes = df.wait(60)
+        log = df.log("recv")
+    for d in devs:
+        d.close()
+    other.close()
+    assert codes["recv"] == 0, log
+    for seq in range(k_msgs):
+        assert to_u64(results[seq]["csum"]) == want[seq], seq
 
 
 def test_host_source_reused_right_after_send_bit_exact(launcher, tmp_path):

@@ -1,0 +1,70 @@
+"""Rewritten device sources and the AQL packets' acquire fence (verdict r02 item 2).
+
+r02 dropped the agent-scope acquire fence from single-segment packs, which read their source
+with agent-coherent (`sc1 nt`) loads (`dora_aql_pack1c_u4`).  On gfx950 that fence invalidates
+the CUs' vector L1s (MI355X_MICROARCH.md § visibility: `buffer_inv sc1`, no L2 eviction), so
+the hazard it guards against is a source line still cached after the source was rewritten.  Per
+trial the source (4 KB: one workgroup per pack) is read by every CU (`dora_gpu_l2_touch`) and
+packed 256 times (its lines stay in the caches of the CUs those packs ran on), rewritten behind
+the GPU's back (host stores through the BAR; SDMA; a blit copy), and sent; the receiver
+compares the sample with the new pattern.
+
+The negative control — L1-cached plain loads (test kernel `dora_aql_pack1p_u4`) without the
+fence — never delivered a stale byte on MI355X (r03, 0 of 40 trials per writer).  With no
+evidence either way the fence is back on by default (plain non-temporal loads behind it,
+`dora_aql_pack1_u4`); the coherent no-fence kernel is opt-in (`DORA_GPU_AQL_COHERENT=1`).
+This test keeps every shipped configuration bit-exact under that sequence and reports the
+negative control's outcome (a stale delivery there would be the evidence, and is printed).
+
+Each configuration runs in its own process (tests/fence_probe.py), since the knobs are read once.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+TRIALS = 40
+# bar: host stores through the BAR (the negative control's writer); h2d / d2d: HIP copies
+ENGINES = ("bar", "h2d", "d2d")
+
+CONFIGS = {
+    # negative control (reported, not shipped): L1-cached loads, no fence
+    "plain_no_fence": ({"DORA_GPU_AQL_COHERENT": "plain", "DORA_GPU_AQL_ACQUIRE": "none"},
+                       "dora_aql_pack1p_u4"),
+    "plain_fence": ({"DORA_GPU_AQL_COHERENT": "plain"}, "dora_aql_pack1p_u4"),
+    # the default: non-temporal loads behind the agent-scope acquire fence
+    "default": ({}, "dora_aql_pack1_u4"),
+    # opt-in: agent-coherent loads, no fence
+    "coherent": ({"DORA_GPU_AQL_COHERENT": "1"}, "dora_aql_pack1c_u4"),
+}
+SHIPPED = ("plain_fence", "default", "coherent")
+SIZE = 4 << 10   # one chunk: one workgroup per pack
+WARM = 256       # fence_probe.WARM
+
+
+def _probe(cfg, engine):
+    env = dict(os.environ)
+    for k in ("DORA_GPU_AQL_COHERENT", "DORA_GPU_AQL_ACQUIRE"):
+        env.pop(k, None)
+    env.update(CONFIGS[cfg][0])
+    r = subprocess.run([sys.executable, os.path.join(HERE, "fence_probe.py"), engine,
+                        str(TRIALS), str(SIZE)], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.skipif(os.environ.get("DORA_GPU_AQL", "1") == "0", reason="AQL dispatch off")
+def test_acquire_fence_negative_control_and_coherent_loads():
+    res = {(c, e): _probe(c, e) for c in CONFIGS for e in ENGINES}
+    print(json.dumps({f"{c}/{e}": r for (c, e), r in res.items()}))
+    for (c, e), r in res.items():
+        assert r["kernels"].get(CONFIGS[c][1]) == TRIALS * (WARM + 1), r
+        if c in SHIPPED:
+            assert r["mismatched"] == 0, r   # every shipped configuration is bit-exact
+    stale = {e: res[("plain_no_fence", e)]["mismatched"] for e in ENGINES}
+    print(f"negative control (L1-cached loads, no acquire fence): stale trials {stale}")
