@@ -165,6 +165,31 @@ def pmc_traffic(msg_bytes: int):
     return best
 
 
+def cpu_share():
+    """This box's CPU share: the cgroup's quota, its throttling counters and the load average
+    (the boxes are a 16-CPU share of a shared host; a throttled period stalls every thread of
+    the dataflow for the rest of the 100 ms period)."""
+    out = {"nproc_affinity": len(os.sched_getaffinity(0))}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        out["cpu_max"] = None if q == "max" else round(int(q) / int(per), 2)
+        st = dict(line.split() for line in open("/sys/fs/cgroup/cpu.stat"))
+        for k in ("nr_periods", "nr_throttled", "throttled_usec"):
+            out[k] = int(st.get(k, 0))
+    except (OSError, ValueError):
+        pass
+    try:
+        out["loadavg_1m"] = float(open("/proc/loadavg").read().split()[0])
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def share_delta(a, b):
+    return {k: b[k] - a[k] for k in ("nr_periods", "nr_throttled", "throttled_usec")
+            if k in a and k in b}
+
+
 def busy_union_ms(intervals):
     """Length of the union of [start, stop] intervals (ms)."""
     total, end = 0.0, None
@@ -468,6 +493,7 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
     late = min(4, steps)
     before = node.stats()
     node.sync()
+    kern0, bs0 = device.aql_dispatch_counts(node.device), device.aql_batch_stats(node.device)
     node.region_begin()
     t0 = time.perf_counter()
     for k in range(steps):
@@ -484,6 +510,7 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
     elapsed = time.perf_counter() - t0
     region = node.region_end()
     after = node.stats()
+    kern1, bs1 = device.aql_dispatch_counts(node.device), device.aql_batch_stats(node.device)
     for a in srcs:
         a.close()
     span_ms, packs = region["span_ms"], region["packs"]
@@ -498,7 +525,10 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "kernel": aql_kernel_name("c3", S),
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
-                     "region_packs": packs, "algorithmic_bytes_per_launch": 2 * S},
+                     "region_packs": packs, "algorithmic_bytes_per_launch": 2 * S,
+                     "region_kernels": {k: kern1[k] - kern0.get(k, 0) for k in kern1
+                                        if kern1[k] - kern0.get(k, 0)},
+                     "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"]},
         "parity": {"oracle_sample_bytes": golden["sample_bytes"], "oracle_csum64": want,
                    "reference_pack_matches_oracle": ref_csum == want and S == golden["sample_bytes"],
                    "late_verified_msgs": late},
@@ -635,6 +665,7 @@ def main():
 
     # ---- latency ladder (reference latency mode: spaced messages, output `latency`) ----
     ladder_bufs = {}
+    share_lat0 = share_lat1 = None
     if not args.no_ladder:
         for size in LADDER:
             b = device.DeviceBuffer(size)
@@ -653,6 +684,7 @@ def main():
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
         wait_ack(seq)
         seq += 1
+        share_lat0 = cpu_share()
         for size in sizes:
             for _ in range(args.lat_n):
                 node.send_output_device_bytes("latency", ladder_bufs[size].ptr, size,
@@ -662,6 +694,7 @@ def main():
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
         wait_ack(seq)
         seq += 1
+        share_lat1 = cpu_share()
         for b in {id(b): b for b in ladder_bufs.values()}.values():
             b.free()
 
@@ -681,6 +714,7 @@ def main():
             wait_ack(seq)
             seq += 1
             d0 = node.dataflow_counters("sink")["dropped_inputs"]
+            bs0 = device.aql_batch_stats(local_rank)
             # small sizes run ~1-2 us per message: >= 2000 of them, so a host hiccup does not
             # set the rate of a ~0.3 ms burst
             tp_n = args.tp_n if size > (4 << 20) else max(args.tp_n, 2000)
@@ -695,13 +729,17 @@ def main():
             # the sink's queue (queue_size 10, the reference default) may drop inputs when it
             # falls behind: only delivered messages count
             dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
+            bs1 = device.aql_batch_stats(local_rank)
             got = tp_n - dropped
             tp_ladder[str(size)] = {"GBps": round(got * size / dt / 1e9, 2),
                                     "msgs_per_s": round(got / dt, 1),
                                     "us_per_msg": round(dt / got * 1e6, 2),
                                     "hbm_frac_2S": round(2 * got * size / dt / 1e9 /
                                                          HBM_PEAK_GBPS, 4),
-                                    "dropped": dropped}
+                                    "dropped": dropped,
+                                    # sends that left in batch packs (aql.cpp), and batches
+                                    "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"],
+                                    "batches": bs1["batches"] - bs0["batches"]}
             for b in bufs:
                 b.free()
 
@@ -732,6 +770,7 @@ def main():
         call("dora_gpu_device_sync")
     elif presync == "node":
         node.sync()
+    kern0 = device.aql_dispatch_counts(local_rank)
     if not args.no_kernel_timing:
         node.region_begin()  # setup (profiling signals) before the clock starts
     t0_ns = time.time_ns()
@@ -763,6 +802,8 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     region = node.region_end() if not args.no_kernel_timing else None
+    kern1 = device.aql_dispatch_counts(local_rank)
+    region_kernels = {k: kern1[k] - kern0.get(k, 0) for k in kern1 if kern1[k] - kern0.get(k, 0)}
     sink_after = node.dataflow_counters("sink")
     node_after = node.stats()
     region_setup = {
@@ -856,6 +897,10 @@ def main():
                    "msg_bytes": S, "parallelism": f"dp{world} (one dataflow per GPU)",
                    "sources_rotated": nsrc},
         "latency_us": lat,
+        # the cgroup's CPU quota and how often it throttled the box during the latency ladder
+        "cpu_share": dict(share_lat1 or cpu_share(),
+                          during_latency_ladder=(share_delta(share_lat0, share_lat1)
+                                                 if share_lat0 and share_lat1 else None)),
         "throughput_per_size": tp_ladder,
         # sources rotated past the L2s / Infinity Cache: every byte read and written in HBM
         "throughput_per_size_native": native,
@@ -869,6 +914,8 @@ def main():
                      "traffic_source": traffic[0] if traffic else None,
                      "kernel": (aql_kernel_name(args.workload, S) if stats["fill_paths"]["aql"]
                                 else "pack_kernel (HIP fill streams)"),
+                     # AQL packets of the timed region per kernel (dora_gpu_aql_dispatch_counts)
+                     "region_kernels": region_kernels,
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
                      "region_packs": packs, "region_span_us": round(span_ms * 1e3, 1),
                      "timing": "every timed pack stamps its first workgroup's start and its "

@@ -53,6 +53,8 @@ _SIGS = {
     "dora_gpu_busy_stats": (c_int, [POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_gpu_aql_dispatch_counts": (c_int, [c_int, POINTER(c_uint64), c_size_t, POINTER(c_size_t)]),
     "dora_gpu_aql_kernel_name": (c_char_p, [c_size_t]),
+    "dora_gpu_aql_batch_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_uint64),
+                                         POINTER(c_uint64)]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),
@@ -102,6 +104,7 @@ _SIGS = {
     "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
     "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
     "dora_gpu_test_bar_free": (None, [c_void_p]),
+    "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
     "dora_gpu_fill_splitmix": (c_int, [c_void_p, c_size_t, c_uint64, c_void_p]),
     # node API
     "dora_node_init": (c_int, [c_char_p, c_char_p, c_int, POINTER(c_void_p)]),

@@ -12,11 +12,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -33,12 +36,16 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
 size_t aql_args_size();
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
                     uint32_t* grid, int* unroll);
+size_t aql_batch_args_size();
+uint32_t aql_chunk_bytes(const Segment* segs, size_t n);
+int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t cap,
+                         uint32_t* grid);
 
 namespace {
 
 constexpr uint32_t kQueuePackets = 4096;
 constexpr uint32_t kRingSlots = 512;
-constexpr uint32_t kSlotBytes = 512;
+constexpr uint32_t kSlotBytes = 1024;    // AqlPackArgs 272 B, AqlBatchArgs 640 B
 constexpr uint32_t kArgs1Bytes = 56;    // preloaded arguments of the single-segment kernels
 constexpr uint32_t kHostSlotBytes = 64;
 constexpr uint32_t kProfileSignals = 4096;
@@ -49,16 +56,33 @@ struct Use {
   uint64_t epoch = 0;
 };
 
+constexpr size_t kMaxItemSegs = 8;   // segments of one message the AQL path takes
+constexpr size_t kBatchMsgs = 8;     // pack_device.h kMaxBatchMsgs
+constexpr size_t kBatchSegs = 16;    // pack_device.h kMaxBatchSegs
+
+// A send waiting for queue capacity (the backlog) or being dispatched.
+struct Pending {
+  Segment segs[kMaxItemSegs];
+  size_t n = 0;
+  uint8_t* dst = nullptr;
+  FillSignal sig{};
+  const std::atomic<uint64_t>* flag_host = nullptr;
+  uint64_t dst_cap = 0, bytes = 0;
+  uint32_t chunk = 0;
+  bool profile = false;
+};
+
 }  // namespace
 
 constexpr int kMaxQueues = 8;
 
 // The kernels of the embedded code object, in AqlQueue::kobj order.
-constexpr int kKernels = 7;
+constexpr int kKernels = 8;
+constexpr int kBatchKernel = 7;
 constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4",   "dora_aql_pack_u8",
                                                 "dora_aql_pack1_u4",  "dora_aql_pack1_u8",
                                                 "dora_aql_pack1c_u4", "dora_aql_packc_u4",
-                                                "dora_aql_pack1p_u4"};
+                                                "dora_aql_pack1p_u4", "dora_aql_packb_u4"};
 
 struct AqlQueue {
   std::mutex mu;
@@ -72,9 +96,9 @@ struct AqlQueue {
   hsa_queue_t* qs[kMaxQueues] = {};
   uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
   int nq = 0;
-  // u4, u8, pack1_u4, pack1_u8, pack1c_u4, packc_u4, pack1p_u4 (kKernelNames)
-  uint64_t kobj[7] = {};
-  uint32_t group[7] = {}, priv[7] = {};
+  // kKernelNames order
+  uint64_t kobj[kKernels] = {};
+  uint32_t group[kKernels] = {}, priv[kKernels] = {};
   uint8_t* ring = nullptr;    // kRingSlots x kSlotBytes of device memory, host-mapped
   uint8_t* hring = nullptr;   // kRingSlots x kHostSlotBytes of host memory (single-segment packs)
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
@@ -84,7 +108,16 @@ struct AqlQueue {
   bool profiling = false;
   std::vector<hsa_signal_t> free_sigs, used_sigs;
   uint64_t ts_freq = 0;
-  uint64_t dispatched[7] = {};  // packets per kernel (kKernelNames order)
+  uint64_t dispatched[kKernels] = {};  // packets per kernel (kKernelNames order)
+  // Batching (aql_pack): per queue, the packets dispatched and not yet seen complete (the fill
+  // flag + epoch their last message signals); sends that find every queue `depth` packets deep
+  // wait in the backlog and leave together, one batch pack per dispatch, when a queue drains.
+  std::deque<Use> outq[kMaxQueues];
+  std::deque<Pending> backlog;
+  std::condition_variable cv;  // backlog non-empty (the dispatcher thread waits on it)
+  bool dispatcher = false;
+  bool hold = false;  // test tool (aql_hold): every batchable send waits in the backlog
+  uint64_t batches = 0, batched_msgs = 0, backlogged = 0;
   // test tool (bar_alloc): the GPU's coarse-grained pool, host-accessible through the BAR
   hsa_agent_t cpu{};
   hsa_amd_memory_pool_t coarse{};
@@ -282,7 +315,10 @@ AqlQueue* create(int device) {
         hsa_executable_symbol_get_info(
             sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &a->priv[k]) !=
             HSA_STATUS_SUCCESS ||
-        ka != (k < 2 ? aql_args_size() : k == 5 ? sizeof(void*) : size_t(kArgs1Bytes)) ||
+        ka != (k < 2                  ? aql_args_size()
+               : k == kBatchKernel    ? aql_batch_args_size()
+               : k == 5               ? sizeof(void*)
+                                      : size_t(kArgs1Bytes)) ||
         ka > kSlotBytes) {
       delete a;
       return note("kernel symbol / argument size");  // no hidden arguments expected
@@ -363,6 +399,22 @@ AqlQueue* aql_queue(int device) {
 
 size_t aql_max_segments() { return 8; }
 
+namespace {
+// Wait (bounded) until the dispatcher has dispatched every backlogged send: their fill flags are
+// in no argument slot before that.
+void drain_backlog(AqlQueue* a, std::chrono::steady_clock::time_point t0,
+                   std::chrono::steady_clock::duration limit) {
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> g(a->mu);
+      if (a->backlog.empty() || a->failed.load()) return;
+    }
+    if (std::chrono::steady_clock::now() - t0 > limit) return;
+    std::this_thread::yield();
+  }
+}
+}  // namespace
+
 void aql_fence_all() {
   AqlQueue* qs[64];
   {
@@ -372,6 +424,7 @@ void aql_fence_all() {
   const auto t0 = std::chrono::steady_clock::now();
   for (AqlQueue* a : qs) {
     if (!a) continue;
+    drain_backlog(a, t0, std::chrono::seconds(5));
     std::lock_guard<std::mutex> g(a->mu);
     for (Use& u : a->uses)
       while (u.flag && u.flag->load(std::memory_order_acquire) < u.epoch &&
@@ -383,9 +436,18 @@ void aql_fence_all() {
 void aql_forget_flags(int device, const void* base, size_t size) {
   AqlQueue* a = aql_queue(device);
   if (!a) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  drain_backlog(a, t0, std::chrono::seconds(2));
   std::lock_guard<std::mutex> g(a->mu);
   const auto* lo = static_cast<const uint8_t*>(base);
-  const auto t0 = std::chrono::steady_clock::now();
+  for (auto& o : a->outq) {  // outstanding entries pointing into the region go too
+    std::deque<Use> keep;
+    for (const Use& u : o) {
+      const auto* f = reinterpret_cast<const uint8_t*>(u.flag);
+      if (f < lo || f >= lo + size) keep.push_back(u);
+    }
+    o.swap(keep);
+  }
   for (Use& u : a->uses) {
     const auto* f = reinterpret_cast<const uint8_t*>(u.flag);
     if (!u.flag || f < lo || f >= lo + size) continue;
@@ -396,11 +458,24 @@ void aql_forget_flags(int device, const void* base, size_t size) {
   }
 }
 
-int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap) {
-  if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
-  SubSpan sp_all(SP_AQL_PACK);
-  std::lock_guard<std::mutex> g(a->mu);
+namespace {
+
+uint64_t barrier_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
+  }();
+  return v;
+}
+
+// Write and ring one packet on queue `qi` (a->mu held): one message with the single- or
+// multi-segment kernels, or a batch of `n` > 1 messages with dora_aql_packb_u4.
+int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big) {
+  const Pending& it0 = items[0];
+  const Segment* segs = it0.segs;
+  uint8_t* const dst = it0.dst;
+  const FillSignal& sig = it0.sig;
+  const bool profile = std::any_of(items, items + n, [](const Pending& x) { return x.profile; });
   // the argument slot of the dispatch kRingSlots back must have completed
   const uint64_t r = a->next % kRingSlots;
   Use& u = a->uses[r];
@@ -419,9 +494,19 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   uint32_t grid = 0;
   int unroll = 4;
   // one segment at sample offset 0: the preloaded kernels, arguments from host memory
-  const bool one = a->hring && n == 1 && segs[0].dst_off == 0;
-  int rc = one ? build_aql_args1(segs[0], dst, sig, args, &grid, &unroll)
-               : build_aql_args(segs, n, dst, sig, args, sizeof(args), &grid, &unroll, dst_cap);
+  const bool batch = n > 1;
+  const bool one = !batch && a->hring && it0.n == 1 && segs[0].dst_off == 0;
+  int rc;
+  if (batch) {
+    BatchItem bi[kBatchMsgs];
+    for (size_t m = 0; m < n; ++m)
+      bi[m] = {items[m].segs, items[m].n, items[m].dst, items[m].sig, items[m].dst_cap};
+    rc = build_aql_batch_args(bi, n, args, sizeof(args), &grid);
+  } else if (one) {
+    rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll);
+  } else {
+    rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll, it0.dst_cap);
+  }
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};
   static const bool no_prof = [] {
@@ -442,7 +527,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   }
   // Coherent multi-segment packs (DORA_GPU_AQL_COHERENT=all, coherent_level): the kernel reads
   // its arguments from the device-ring slot through a pointer preloaded from the host ring.
-  const bool coh_multi = coherent_level() >= 2 && !one && unroll == 4 && a->hring;
+  const bool coh_multi = coherent_level() >= 2 && !one && !batch && unroll == 4 && a->hring;
   uint8_t* slot;
   if (one) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
@@ -450,7 +535,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     std::memcpy(slot, args, kArgs1Bytes);
   } else {
     slot = a->ring + r * kSlotBytes;
-    std::memcpy(slot, args, aql_args_size());
+    std::memcpy(slot, args, batch ? aql_batch_args_size() : aql_args_size());
     // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both
     // are posted writes ordered before the doorbell
     __builtin_ia32_sfence();
@@ -467,15 +552,6 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // the barrier; profiles/r02_aql_big_ab.jsonl).  Smaller packs overlap freely on all queues.
   sp_args.stop();
   SubSpan sp_disp(SP_AQL_DISPATCH);
-  static const uint64_t barrier_bytes = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
-  }();
-  uint64_t bytes = 0;
-  for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
-  const bool big = barrier_bytes && bytes >= barrier_bytes;
-  const size_t qi = big ? size_t(a->next_big++ % uint64_t(std::min(a->nq, 3)))
-                        : size_t(a->next % uint64_t(a->nq));
   hsa_queue_t* const q = a->qs[qi];
   // Wait for a free packet slot before reserving one: a reserved packet must be written, or the
   // command processor stalls at its INVALID header for good.  This process is the queue's only
@@ -502,7 +578,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // one box, sources rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 ->
   // 1.23-1.26 us per message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.
   const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi;
-  const int k = coh                                        ? (one ? 4 : 5)
+  const int k = batch                                      ? kBatchKernel
+                : coh                                        ? (one ? 4 : 5)
                 : (one && coherent_level() < 0 && unroll == 4) ? 6
                                                                : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
   p->workgroup_size_x = 256;
@@ -548,10 +625,168 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
                    __ATOMIC_RELEASE);
   hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
-  u.flag = flag_host;
-  u.epoch = sig.epoch;
+  // every message of a batch signals at its end: the last one's flag stands for the packet
+  u.flag = items[n - 1].flag_host;
+  u.epoch = items[n - 1].sig.epoch;
+  a->outq[qi].push_back(u);
   ++a->next;
   ++a->dispatched[k];
+  if (batch) {
+    ++a->batches;
+    a->batched_msgs += n;
+  }
+  return DORA_OK;
+}
+
+bool batching_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BATCH");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// Packets a queue may hold before sends wait in the backlog: one running, one ready behind it
+// (DORA_GPU_AQL_DEPTH).
+size_t queue_depth() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_DEPTH");
+    const long d = e ? std::atol(e) : 2;
+    return size_t(std::max(1L, std::min(64L, d)));
+  }();
+  return v;
+}
+
+// Drop the completed packets at the front of queue `i`'s outstanding list.
+void prune(AqlQueue* a, int i) {
+  auto& o = a->outq[i];
+  while (!o.empty() && o.front().flag->load(std::memory_order_acquire) >= o.front().epoch)
+    o.pop_front();
+}
+
+// The queue with the fewest outstanding packets below the depth (ties: round robin), or -1.
+int pick_queue(AqlQueue* a) {
+  if (a->hold) return -1;
+  int best = -1;
+  size_t best_n = queue_depth();
+  for (int j = 0; j < a->nq; ++j) {
+    const int i = int((a->next + uint64_t(j)) % uint64_t(a->nq));
+    prune(a, i);
+    if (a->outq[i].size() < best_n) {
+      best = i;
+      best_n = a->outq[i].size();
+    }
+  }
+  return best;
+}
+
+// Dispatch the backlog into queues with room, as batches of consecutive sends that share a
+// chunk size (a->mu held).
+void pump_locked(AqlQueue* a) {
+  while (!a->backlog.empty() && !a->failed.load()) {
+    const int qi = pick_queue(a);
+    if (qi < 0) return;
+    Pending batch[kBatchMsgs];
+    size_t n = 0, segs = 0;
+    uint64_t bytes = 0;
+    while (n < kBatchMsgs && !a->backlog.empty()) {
+      const Pending& p = a->backlog.front();
+      if (n && (segs + p.n > kBatchSegs || p.chunk != batch[0].chunk ||
+                bytes + p.bytes > barrier_bytes()))
+        break;
+      segs += p.n;
+      bytes += p.bytes;
+      batch[n++] = p;
+      a->backlog.pop_front();
+    }
+    if (dispatch_locked(a, size_t(qi), batch, n, false) != DORA_OK) {
+      // the fills of these messages never signal: their receivers report them failed
+      a->failed.store(true);
+      return;
+    }
+  }
+}
+
+// The dispatcher thread: dispatches the backlog as queues drain while no send is being made.
+void dispatcher_main(AqlQueue* a) {
+  std::unique_lock<std::mutex> lk(a->mu);
+  for (;;) {
+    a->cv.wait(lk, [a] { return !a->backlog.empty(); });
+    pump_locked(a);
+    if (a->backlog.empty() || a->failed.load()) {
+      if (a->failed.load()) a->backlog.clear();
+      continue;
+    }
+    // every queue is full: wait (unlocked) for the oldest packet of any queue to complete
+    Use front[kMaxQueues];
+    for (int i = 0; i < a->nq; ++i) front[i] = a->outq[i].empty() ? Use{} : a->outq[i].front();
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      bool any = false;
+      for (int i = 0; i < a->nq && !any; ++i)
+        any = !front[i].flag || front[i].flag->load(std::memory_order_acquire) >= front[i].epoch;
+      if (any) break;
+      if ((spin & 1023) == 1023) {
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt > std::chrono::milliseconds(2)) break;  // re-check under the lock
+        if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
+      }
+      __builtin_ia32_pause();
+    }
+    lk.lock();
+  }
+}
+
+}  // namespace
+
+int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
+             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap) {
+  if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
+  if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
+  SubSpan sp_all(SP_AQL_PACK);
+  Pending p;
+  std::copy(segs, segs + n, p.segs);
+  p.n = n;
+  p.dst = dst;
+  p.sig = sig;
+  p.flag_host = flag_host;
+  p.dst_cap = dst_cap;
+  p.profile = profile;
+  for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
+  std::lock_guard<std::mutex> g(a->mu);
+  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
+  // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
+  // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
+  // the barrier; profiles/r02_aql_big_ab.jsonl).
+  const bool big = barrier_bytes() && p.bytes >= barrier_bytes();
+  if (big || !batching_enabled()) {
+    const size_t qi = big ? size_t(a->next_big++ % uint64_t(std::min(a->nq, 3)))
+                          : size_t(a->next % uint64_t(a->nq));
+    const int rc = dispatch_locked(a, qi, &p, 1, big);
+    prune(a, int(qi));
+    return rc;
+  }
+  // Below that, a queue holds at most queue_depth() packets (one running, one ready): the
+  // command processor runs a queue's packets one after another with a ~1-2 us gap, four queues
+  // at most share the compute pipes (DESIGN §6 "4 MB"), so a send that finds them all busy
+  // waits in the backlog and leaves with the sends queued behind it as one batch pack — fewer,
+  // larger dispatches instead of more queues.
+  p.chunk = aql_chunk_bytes(segs, n);
+  if (a->backlog.empty()) {
+    const int qi = pick_queue(a);
+    if (qi >= 0) return dispatch_locked(a, size_t(qi), &p, 1, false);
+  }
+  a->backlog.push_back(p);
+  ++a->backlogged;
+  pump_locked(a);
+  if (!a->backlog.empty()) {
+    if (!a->dispatcher) {
+      a->dispatcher = true;
+      std::thread(dispatcher_main, a).detach();
+    }
+    a->cv.notify_one();
+  }
   return DORA_OK;
 }
 
@@ -587,6 +822,34 @@ void bar_free(void* p) {
 size_t aql_kernel_count() { return kKernels; }
 
 const char* aql_kernel_name(size_t k) { return k < size_t(kKernels) ? kKernelNames[k] : nullptr; }
+
+int aql_hold(int device, bool hold) {
+  AqlQueue* a = aql_queue(device);
+  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
+  std::lock_guard<std::mutex> g(a->mu);
+  a->hold = hold;
+  if (!hold) {
+    pump_locked(a);
+    if (!a->backlog.empty()) a->cv.notify_one();
+  }
+  return DORA_OK;
+}
+
+int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint64_t* backlogged) {
+  *batches = *batched_msgs = *backlogged = 0;
+  if (device < 0 || device >= 64) return DORA_OK;
+  AqlQueue* a;
+  {
+    std::lock_guard<std::mutex> g(g_queues_mu);
+    a = g_queues[device];
+  }
+  if (!a) return DORA_OK;
+  std::lock_guard<std::mutex> g(a->mu);
+  *batches = a->batches;
+  *batched_msgs = a->batched_msgs;
+  *backlogged = a->backlogged;
+  return DORA_OK;
+}
 
 uint64_t aql_dispatched(int device, size_t k) {
   if (k >= size_t(kKernels) || device < 0 || device >= 64) return 0;

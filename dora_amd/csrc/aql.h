@@ -47,6 +47,11 @@ void aql_fence_all();
 size_t aql_kernel_count();
 const char* aql_kernel_name(size_t k);
 uint64_t aql_dispatched(int device, size_t k);
+// Test tool: while held, every batchable send of this process on `device` waits in the
+// backlog; releasing dispatches the backlog as batch packs (tests/test_gpu_dataflow.py).
+int aql_hold(int device, bool hold);
+// Batch packs dispatched, the sends they carried, and sends that waited in the backlog.
+int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint64_t* backlogged);
 
 // Test tool (tests/fence_probe.py): device memory of the GPU's coarse-grained pool that the host
 // writes directly through the BAR (bar_write: stores + HDP flush + read-back), i.e. behind every

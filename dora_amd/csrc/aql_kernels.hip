@@ -12,6 +12,13 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u4(AqlPackA
   dora::pack::pack_body<4, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
 }
 
+// Batch packs (aql.cpp): up to kMaxBatchMsgs queued sends in one dispatch, each signalled
+// on its own flag when the batch completes.
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_packb_u4(
+    dora::pack::AqlBatchArgs a) {
+  dora::pack::pack_body<4, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
+}
+
 extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u8(AqlPackArgs a) {
   dora::pack::pack_body<8, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
 }

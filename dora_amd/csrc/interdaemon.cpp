@@ -379,8 +379,11 @@ Gateway::~Gateway() {
   for (auto& kv : proxies_) kv.second->cv.notify_all();
   if (accept_th_.joinable()) accept_th_.join();
   {
+    // only connections still open: a reader removes its fd under this lock before it closes
+    // it, so no number here can belong to a later, unrelated socket
     std::lock_guard<std::mutex> g(readers_mu_);
-    for (int fd : reader_fds_) ::shutdown(fd, SHUT_RDWR);
+    for (int fd : reader_fds_)
+      if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
   }
   for (auto& t : readers_)
     if (t.joinable()) t.join();
@@ -414,13 +417,34 @@ void Gateway::accept_loop() {
   }
 }
 
+// Largest inter-daemon frame accepted (DORA_GPU_MAX_FRAME_BYTES, default 4 GiB + 1 MiB of
+// metadata): a longer length prefix is a corrupt or hostile frame.
+uint64_t max_frame_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_MAX_FRAME_BYTES");
+    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
+    return x ? x : (uint64_t(4) << 30) + (uint64_t(1) << 20);
+  }();
+  return v;
+}
+
 void Gateway::read_loop(int fd) {
   std::vector<uint8_t> buf;
   while (!stop_) {
     uint64_t len = 0;
     if (!recv_all(fd, reinterpret_cast<uint8_t*>(&len), 8)) break;
-    if (len > (uint64_t(1) << 36)) break;  // a corrupt frame: drop the connection
-    buf.resize(len);
+    if (len > max_frame_bytes()) {  // a corrupt frame: drop this connection only
+      std::fprintf(stderr, "dora-gpu daemon: inter-daemon frame of %llu bytes refused\n",
+                   static_cast<unsigned long long>(len));
+      break;
+    }
+    try {
+      buf.resize(len);
+    } catch (const std::bad_alloc&) {
+      std::fprintf(stderr, "dora-gpu daemon: no memory for a %llu-byte inter-daemon frame\n",
+                   static_cast<unsigned long long>(len));
+      break;
+    }
     if (!recv_all(fd, buf.data(), len)) break;
     InterDaemonEvent e;
     try {
@@ -443,6 +467,11 @@ void Gateway::read_loop(int fd) {
       p->q.push_back(std::move(e));
     }
     p->cv.notify_one();
+  }
+  {
+    std::lock_guard<std::mutex> g(readers_mu_);
+    for (int& r : reader_fds_)
+      if (r == fd) r = -1;
   }
   ::close(fd);
   last_disconnect_ns_.store(mono_ns());

@@ -434,6 +434,74 @@ int launch_pack_wait(const Segment* segs, size_t n, uint8_t* dst, hipStream_t st
 }
 
 size_t aql_args_size() { return sizeof(AqlPackArgs); }
+size_t aql_batch_args_size() { return sizeof(dora::pack::AqlBatchArgs); }
+
+// The chunk size a message's pack would use on its own (a batch holds messages of one size).
+uint32_t aql_chunk_bytes(const Segment* segs, size_t n) {
+  uint64_t body = 0;
+  for (size_t k = 0; k < n; ++k) body += segs[k].len;
+  Variant var = pack_variant();
+  if (var.unroll == 0) var.unroll = default_unroll(body);
+  return choose_chunk_bytes(body, var.unroll);
+}
+
+// Arguments of dora_aql_packb_u4: the segments of `n` messages with absolute destinations,
+// sorted by address, each message's stitched-edge bits carried over from its own edge_mask.
+int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t cap,
+                         uint32_t* grid_out) {
+  using dora::pack::AqlBatchArgs;
+  using dora::pack::kMaxBatchMsgs;
+  using dora::pack::kMaxBatchSegs;
+  if (n == 0 || n > size_t(kMaxBatchMsgs)) return fail(DORA_ERR_INVALID, "batch of %zu", n);
+  if (cap < sizeof(AqlBatchArgs)) return fail(DORA_ERR_INVALID, "AQL batch: argument buffer");
+  struct S {
+    uint64_t dst;
+    const uint8_t* src;
+    uint64_t len;
+    uint32_t edge;
+  };
+  S all[kMaxBatchSegs];
+  size_t ns = 0;
+  const uint32_t chunk = aql_chunk_bytes(items[0].segs, items[0].n);
+  for (size_t m = 0; m < n; ++m) {
+    const BatchItem& it = items[m];
+    if (ns + it.n > size_t(kMaxBatchSegs)) return fail(DORA_ERR_INVALID, "AQL batch: segments");
+    if (aql_chunk_bytes(it.segs, it.n) != chunk)
+      return fail(DORA_ERR_INVALID, "AQL batch: messages of different chunk sizes");
+    const uint64_t em = edge_mask(it.segs, it.n, it.dst, it.dst_cap);
+    for (size_t k = 0; k < it.n; ++k) {
+      if (it.segs[k].op != SEG_COPY) return fail(DORA_ERR_INVALID, "AQL batch: transform");
+      all[ns++] = {reinterpret_cast<uintptr_t>(it.dst) + it.segs[k].dst_off,
+                   static_cast<const uint8_t*>(it.segs[k].src), it.segs[k].len,
+                   static_cast<uint32_t>(em >> (2 * k)) & 3u};
+    }
+  }
+  std::sort(all, all + ns, [](const S& a, const S& b) { return a.dst < b.dst; });
+  AqlBatchArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.chunk_bytes = chunk;
+  uint64_t chunks = 0;
+  for (size_t k = 0; k < ns; ++k) {
+    a.seg[k] = {all[k].src, all[k].dst, all[k].len};
+    chunks += segment_chunks(0, all[k].dst, all[k].len, chunk, line_chunks());
+    if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
+    a.chunk_end[k] = static_cast<uint32_t>(chunks);
+    a.edge_mask |= uint64_t(all[k].edge) << (2 * k);
+  }
+  a.nseg = static_cast<uint32_t>(ns) | (line_chunks() ? 0u : kUnitChunks);
+  a.n_chunks = static_cast<uint32_t>(chunks);
+  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
+  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  a.flag = items[0].sig.flag;
+  a.done = items[0].sig.done;
+  a.epoch = items[0].sig.epoch;
+  a.nmsg = static_cast<uint32_t>(n);
+  for (size_t m = 0; m < n; ++m) a.msg[m] = {items[m].sig.flag, items[m].sig.epoch};
+  std::memcpy(out, &a, sizeof(a));
+  *grid_out = a.grid;
+  return DORA_OK;
+}
 
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.

@@ -606,6 +606,7 @@ struct dora_event {
   std::shared_ptr<dora::InputData> data;
   std::string error;
   bool pending = false;  // device input not yet completed (fill wait / cross-GPU pull)
+  uint64_t arrived_ns = 0;  // mono_ns when the descriptor was drained (transit age bound)
   dora::DeviceIpc ipc{};
   // dora_event_type_info's reference (inline-validity) form, built on first request when the
   // type info points into the sample's validity tail
@@ -934,6 +935,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
   switch (kind) {
     case EV_INPUT: {
       ev->type = DORA_EVENT_INPUT;
+      ev->arrived_ns = mono_ns();
       ev->id = r.str();
       const uint64_t meta_len = r.u64();
       r.need(meta_len);
@@ -1091,6 +1093,14 @@ void finish_input(dora_node* n, dora_event* ev) {
       if (mono_ns() - t0 > uint64_t(spin_budget_us()) * 1000) usleep(20);
     }
     add_fill_wait_ns(mono_ns() - t0);
+    if (trace_enabled()) {
+      // the pack's own stamps (s_memrealtime), for the GPU side of a message's latency; the
+      // line may already carry a later fill's stamps if the slot was refilled meanwhile
+      const FillFlag& ff = h->nodes[d.flag_node].fill[d.flag_index];
+      const double ns_per_tick = 1e9 / kRealtimeHz;
+      trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
+      trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
+    }
   } else if (d.fill == FILL_EVENT) {
     // the producer's fill completes when its interprocess event fires
     hipEvent_t fill = nullptr;
@@ -1204,12 +1214,26 @@ int ensure_local(InputData* in) {
 // async sender with more samples in flight than a receiver's queue_size (12 vs the default 10)
 // made the receiver drop inputs whenever it waited on the GPU: 20-25 % of a 1-4 MB burst from
 // the Python node (scripts/py_tp.py), inputs the reference would have delivered.
+// How long an input may sit in the queue uncounted because its producer's fill has not
+// signalled (DORA_GPU_TRANSIT_LIMIT_MS, default 2000): past that the drop-oldest policy counts
+// it again, so a fill that never completes (a lost queue, a GPU fault) cannot grow the queue
+// beyond its queue_size.
+uint64_t transit_limit_ns() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_TRANSIT_LIMIT_MS");
+    return uint64_t(e ? std::strtoull(e, nullptr, 10) : 2000) * 1000000ull;
+  }();
+  return v;
+}
+
 bool fill_in_transit(dora_node* n, const dora_event* e) {
   if (!e->pending || e->ipc.fill != FILL_FLAG) return false;
   RegionHdr* h = n->core->region->hdr();
   if (e->ipc.flag_node >= h->n_nodes || e->ipc.flag_index >= kFillFlags) return false;
-  return h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch.load(std::memory_order_acquire) <
-         e->ipc.epoch;
+  if (h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch.load(std::memory_order_acquire) >=
+      e->ipc.epoch)
+    return false;
+  return mono_ns() - e->arrived_ns < transit_limit_ns();
 }
 
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input

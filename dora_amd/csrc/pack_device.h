@@ -76,6 +76,36 @@ struct PackArgsT {
 using PackArgs = PackArgsT<kMaxSegs>;
 using AqlPackArgs = PackArgsT<kMaxAqlSegs>;
 
+// A batch pack (aql.cpp: sends queued behind busy AQL queues go out together in one dispatch):
+// the segments of up to kMaxBatchMsgs messages, each into its own slot.  `dst` is null and every
+// segment's `dst_off` is its absolute destination address, so pack_chunk's alignment arithmetic
+// and stitched edges work unchanged; the segments are sorted by address (slots never overlap), so
+// a segment's predecessor never shares a 16-byte unit with it unless it is of the same message.
+// Every message keeps its own fill flag and epoch; the done words and their epoch are the first
+// message's.
+constexpr int kMaxBatchSegs = 16;
+constexpr int kMaxBatchMsgs = 8;
+struct BatchMsg {
+  uint64_t* flag;
+  uint64_t epoch;
+};
+struct AqlBatchArgs {
+  uint8_t* dst;          // null: segment dst_off are absolute addresses
+  uint64_t* flag;        // message 0's flag (non-null: the launch signals)
+  uint32_t* done;        // message 0's done words
+  uint64_t epoch;        // message 0's epoch
+  uint32_t n_chunks;
+  uint32_t nseg;
+  uint32_t chunk_bytes;
+  uint32_t grid;
+  uint64_t edge_mask;
+  uint32_t nmsg;
+  uint32_t pad;
+  uint32_t chunk_end[kMaxBatchSegs];
+  PackSeg seg[kMaxBatchSegs];
+  BatchMsg msg[kMaxBatchMsgs];
+};
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -381,6 +411,52 @@ __device__ __forceinline__ void signal_fill(const A& a, uint32_t blk, uint32_t n
   }
 }
 
+// A batch's signal: as signal_fill, and workgroup 0's lanes k < nmsg then stamp and signal
+// message k's flag (every message completes with the whole batch).
+__device__ __forceinline__ void signal_batch(const AqlBatchArgs& a, uint32_t blk, uint32_t nblk,
+                                             uint64_t t_start) {
+  const uint32_t e = static_cast<uint32_t>(a.epoch);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nblk > 1) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(a.done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blk != 0) return;
+    constexpr int kPer = kMaxSignalWgs / kThreads;
+    __shared__ uint32_t missing;
+    bool ok = false;
+    for (uint32_t round = 0; round < (1u << 22); ++round) {
+      if (threadIdx.x == 0) missing = 0;
+      __syncthreads();
+      uint32_t v[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = threadIdx.x + k * kThreads;
+        v[k] = i < nblk ? __hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : e;
+      }
+      bool mine = true;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) mine &= v[k] == e;
+      if (!mine) missing = 1;
+      __syncthreads();
+      const bool all = missing == 0;
+      __syncthreads();
+      if (all) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) return;  // a lost workgroup: the flags stay unset, receivers report the failure
+  }
+  if (threadIdx.x < a.nmsg) {
+    const BatchMsg m = a.msg[threadIdx.x];
+    stamp_fill(m.flag, t_start);
+    __hip_atomic_store(m.flag, m.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // A pack launch: its workgroups stride over the chunks; a signalling launch (NT >= 2) then
 // signals the fill flag.
 template <int U, int NT, class A>
@@ -391,7 +467,10 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
   }
   for (uint32_t c = blk; c < args.n_chunks; c += nblk) pack_chunk<U, NT>(args, c);
   if constexpr (NT >= 2) {
-    if (args.flag) signal_fill(args, blk, nblk, t_start);  // all-zero arguments are a no-op
+    if (args.flag) {  // all-zero arguments are a no-op
+      if constexpr (__is_same(A, AqlBatchArgs)) signal_batch(args, blk, nblk, t_start);
+      else signal_fill(args, blk, nblk, t_start);
+    }
   }
 }
 

@@ -85,6 +85,15 @@ struct FillSignal {
 };
 constexpr uint32_t kMaxSignalWgs = 4096;
 
+// One message of a batch pack (aql.cpp): its copy segments, slot, fill signal, writable bytes.
+struct BatchItem {
+  const Segment* segs;
+  size_t n;
+  uint8_t* dst;
+  FillSignal sig;
+  uint64_t dst_cap;
+};
+
 // Launch the pack of `segs` into `dst` on `stream` (kernels.hip).  With `signal`, the last
 // launch writes the fill flag itself when it can (`*signalled` says whether it did; compacting
 // transforms and host sources leave it to the caller).  `dst_cap`: bytes writable from `dst`

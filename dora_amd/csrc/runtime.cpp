@@ -92,6 +92,18 @@ int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_
   return DORA_OK;
 }
 
+int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs,
+                             uint64_t* backlogged) {
+  uint64_t a = 0, b = 0, c = 0;
+  dora::aql_batch_stats(device, &a, &b, &c);
+  if (batches) *batches = a;
+  if (batched_msgs) *batched_msgs = b;
+  if (backlogged) *backlogged = c;
+  return DORA_OK;
+}
+
+int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
+
 int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out) {
   if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
   return dora::bar_alloc(device, bytes, out);

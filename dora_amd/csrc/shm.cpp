@@ -371,7 +371,10 @@ bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_fla
   // One idle gap may span several calls that time out (a sender polling for drop tokens every
   // 1 ms): the gap — for the spin budget and the adaptive mean — runs from the first of them,
   // unless the caller did other work for a while in between.
-  if (empty()) {
+  // one emptiness check decides both the gap's start and Idle::was_empty: data arriving between
+  // two checks left idle_from_ set for a call that then measured nothing
+  const bool was_empty = empty();
+  if (was_empty) {
     if (!idle_from_ || t0 - last_return_ > 100000) idle_from_ = t0;
   } else {
     idle_from_ = 0;
@@ -393,7 +396,7 @@ bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_fla
         r->idle_from_ = 0;
       }
     }
-  } idle{this, t0, empty()};
+  } idle{this, t0, was_empty};
   while (empty()) {
     const uint64_t now = mono_ns();
     const int64_t el = int64_t(now - t0) / 1000;

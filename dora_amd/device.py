@@ -100,6 +100,27 @@ def csum64(ptr: int, n: int, stream: Stream | None = None) -> int:
     return out.value
 
 
+def aql_dispatch_counts(device: int = 0) -> dict:
+    """Raw AQL packets this process dispatched on `device`, per pack kernel."""
+    lib = _lib.load()
+    c = (c_uint64 * 16)()
+    n = ctypes.c_size_t()
+    call("dora_gpu_aql_dispatch_counts", device, c, 16, byref(n))
+    return {lib.dora_gpu_aql_kernel_name(k).decode(): c[k] for k in range(n.value)}
+
+
+def aql_batch_stats(device: int = 0) -> dict:
+    """Batch packs dispatched, the sends they carried, sends that waited for a queue."""
+    a, b, c = c_uint64(), c_uint64(), c_uint64()
+    call("dora_gpu_aql_batch_stats", device, byref(a), byref(b), byref(c))
+    return {"batches": a.value, "batched_msgs": b.value, "backlogged": c.value}
+
+
+def aql_hold(device: int, hold: bool):
+    """Test tool: hold batchable AQL sends in the backlog / release them as batch packs."""
+    call("dora_gpu_test_aql_hold", device, int(hold))
+
+
 def fill_splitmix(ptr: int, n: int, seed: int, stream: Stream | None = None):
     call("dora_gpu_fill_splitmix", ptr, n, seed, stream.handle if stream else None)
 

@@ -95,6 +95,11 @@ int dora_gpu_busy_stats(uint64_t* idle_ns, uint64_t* fill_wait_ns);
  * kernels that packed its samples with these. */
 int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_t* n);
 const char* dora_gpu_aql_kernel_name(size_t k);
+/* Diagnostics: batch packs dispatched on HIP device `device` by this process, the sends they
+ * carried, and the sends that waited for queue capacity (aql.cpp: sends that find every AQL
+ * queue busy leave together as one batch pack). */
+int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs,
+                             uint64_t* backlogged);
 
 int dora_gpu_device_count(int* count);
 int dora_gpu_set_device(int ordinal);
@@ -224,6 +229,10 @@ int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream);
  * the host writes directly through the PCIe BAR (stores + HDP flush + read-back), behind every
  * XCD's L2 — the source rewrite of the acquire-fence negative control. */
 int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
+/* Test tool: while `hold` is set, every batchable AQL send of this process on `device` waits in
+ * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
+ * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
+int dora_gpu_test_aql_hold(int device, int hold);
 int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
 void dora_gpu_test_bar_free(void* ptr);
 

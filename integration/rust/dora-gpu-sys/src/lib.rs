@@ -52,6 +52,9 @@ pub const DORA_ERR_CLOSED: i32 = -5;
 pub const DORA_ERR_TIMEOUT: i32 = -6;
 pub const DORA_ERR_NOT_FOUND: i32 = -7;
 
+/// Flags of dora_node_send_output_ex / _bytes_ex.
+pub const DORA_SEND_ASYNC: u32 = 1;
+
 pub const DORA_EVENT_STOP: i32 = 0;
 pub const DORA_EVENT_INPUT: i32 = 1;
 pub const DORA_EVENT_INPUT_CLOSED: i32 = 2;

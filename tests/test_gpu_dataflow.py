@@ -140,6 +140,61 @@ def test_python_receiver_c3_point_clouds(launcher):
     assert results[0]["arrow_equal_len"] == 4
 
 
+def test_c3_async_burst_batches_bit_exact(launcher):
+    """Twelve point clouds (nested, validity bitmaps in the sample tail, 7 segments each) sent
+    back to back with DORA_SEND_ASYNC from 12 distinct device arrays: the sends queued behind
+    busy AQL queues leave as batch packs of whole clouds, and every cloud's parity regions
+    checksum to the CPU oracle's at the receiver."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from dora_amd.verify import to_u64
+    from dora_amd.workloads import point_cloud
+    from oracle.arrow_ffi import import_array
+    from oracle.checksum_ref import regions_csum
+    from oracle.pack_ref import node_regions
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["pc"], "inputs": {"result": "recv/result"}},
+        {"id": "recv", "path": sys.executable,
+         "args": [os.path.join(ROOT, "examples", "verify_receiver.py")],
+         "inputs": {"pc": {"source": "src/pc", "queue_size": 100}}, "outputs": ["result"]},
+    ]}
+    clouds = [point_cloud(150000, 16, 100 + k) for k in range(12)]
+    want = [regions_csum(node_regions(import_array(pc))) for pc in clouds]
+    arrs = [DeviceArray.from_pyarrow(pc) for pc in clouds]
+    with Dataflow(desc, launcher=launcher) as df:
+        node = Node("src", dataflow=df.shm, device=0)
+        node.set_async_sends(True)
+        b0 = device.aql_batch_stats(0)
+        device.aql_hold(0, True)   # every cloud waits in the backlog: batches of two clouds
+        for seq, da in enumerate(arrs):
+            node.send_output("pc", da, {"seq": seq})
+        device.aql_hold(0, False)
+        node.sync()
+        b1 = device.aql_batch_stats(0)
+        results = {}
+        deadline = time.time() + 120
+        while len(results) < len(clouds) and time.time() < deadline:
+            ev = node.next(timeout=5)
+            if ev is None:
+                break
+            if ev["type"] == "INPUT":
+                results[ev["metadata"]["seq"]] = ev["metadata"]
+        node.close()
+        codes = df.wait(60)
+        log = df.log("recv")
+    for a in arrs:
+        a.close()
+    assert codes["recv"] == 0, log
+    for seq in range(len(clouds)):
+        assert to_u64(results[seq]["csum"]) == want[seq], seq
+    print(f"c3 async burst: {b1['batches'] - b0['batches']} batches carried "
+          f"{b1['batched_msgs'] - b0['batched_msgs']} of {len(clouds)} clouds")
+    if os.environ.get("DORA_GPU_AQL_BATCH", "1") != "0":
+        assert b1["batched_msgs"] - b0["batched_msgs"] == len(clouds), (b0, b1)
+
+
 @pytest.mark.parametrize("peer_copy", ["kernel", "sdma"])
 def test_c3_validity_tail_through_pulls_and_relay(launcher, peer_copy):
     """Point clouds (validity in the sample's tail) through a relay and a receiver with the
@@ -188,10 +243,12 @@ def test_c3_validity_tail_through_pulls_and_relay(launcher, peer_copy):
     assert results[0]["arrow_equal_len"] == 4
 
 
-def test_many_small_sends_bit_exact(launcher, tmp_path):
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_many_small_sends_bit_exact(launcher, tmp_path, mode):
     """More sends than the AQL argument ring holds (512 slots): every argument slot is reused
     after its launch signalled; 1200 messages of odd sizes from unaligned sources, each
-    checksummed by the sink."""
+    checksummed by the sink.  Async sends run ahead of the GPU: the sends that find every AQL
+    queue busy leave as batch packs (dora_aql_packb_u4), several slots per dispatch."""
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.node import Node
@@ -201,6 +258,8 @@ def test_many_small_sends_bit_exact(launcher, tmp_path):
     n_msgs = 1200
     with Dataflow(_bench_desc(res), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(mode == "async")
+        b0 = device.aql_batch_stats(0)
         s = device.Stream()
         srcs = []
         for k in range(3):
@@ -215,8 +274,14 @@ def test_many_small_sends_bit_exact(launcher, tmp_path):
                 b = srcs[key[0]]
                 sums[key] = device.csum64(b.ptr + key[1], key[2], s)
             b = srcs[key[0]]
+            if mode == "async" and i % 10 == 0:
+                device.aql_hold(0, True)   # the next 10 sends wait in the backlog ...
             node.send_output_device_bytes("data", b.ptr + key[1], key[2],
                                           {"csum": to_i64(sums[key]), "verify": True, "seq": i})
+            if mode == "async" and i % 10 == 9:
+                device.aql_hold(0, False)  # ... and leave as batch packs
+        node.sync()
+        b1 = device.aql_batch_stats(0)
         paths = node.fill_paths()
         node.close()
         codes = df.wait(60)
@@ -228,6 +293,10 @@ def test_many_small_sends_bit_exact(launcher, tmp_path):
     assert out["errors"] == 0
     assert sum(x["verified"] for x in out["series"]) == n_msgs
     assert sum(x["mismatches"] for x in out["series"]) == 0
+    batched = b1["batched_msgs"] - b0["batched_msgs"]
+    print(f"{mode}: {b1['batches'] - b0['batches']} batches carried {batched} of {n_msgs} sends")
+    if mode == "async" and os.environ.get("DORA_GPU_AQL_BATCH", "1") != "0":
+        assert batched > 0, (b0, b1)
     if os.environ.get("DORA_GPU_AQL", "1") != "0":
         assert paths["aql"] == n_msgs, paths
 

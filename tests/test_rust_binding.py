@@ -66,3 +66,65 @@ def test_device_ipc_wire_order_matches_wire_h():
     c_fields = [f for f in c_fields if f not in ("fill", "flag_node", "flag_index", "epoch",
                                                   "event")]
     assert r_fields == c_fields, (r_fields, c_fields)
+
+
+REF_NODE = "/root/reference/apis/rust/node/src"
+# DoraNode / EventStream functions the facade mirrors with the reference's signatures; the rest
+# (init(NodeConfig), dataflow_id, node_config, dataflow_descriptor) need the coordinator's
+# NodeConfig, which this data plane does not carry
+FACADE_NODE_FNS = ["init_from_env", "init_from_node_id", "init_flexible", "send_output_raw",
+                   "send_output", "send_output_bytes", "send_typed_output", "send_output_sample",
+                   "close_outputs", "id", "allocate_data_sample"]
+FACADE_STREAM_FNS = ["recv", "recv_timeout", "recv_async", "recv_async_timeout"]
+
+
+def _impl_fns(txt, type_name):
+    """{name: (params, return)} of the `pub fn`s in `impl <type_name> {`, normalised."""
+    i = txt.index(f"impl {type_name} {{")
+    depth, j = 0, txt.index("{", i)
+    for k in range(j, len(txt)):
+        depth += {"{": 1, "}": -1}.get(txt[k], 0)
+        if depth == 0:
+            body = txt[j:k]
+            break
+    out = {}
+    for m in re.finditer(r"pub (?:async )?fn (\w+)(<[^>]*>)?\((.*?)\)\s*(->\s*([^{\n]+?))?\s*(where|\{)",
+                         body, re.S):
+        params = [re.sub(r"\s+", " ", p).strip() for p in m.group(3).split(",")]
+        params = [p for p in params if p]
+        ret = re.sub(r"\s+", "", (m.group(5) or "")).replace("eyre::Result", "Result")
+        out[m.group(1)] = (params, ret)
+    return out
+
+
+def test_facade_matches_the_reference_node_api():
+    """api.rs: DoraNode (node/mod.rs:65-303), EventStream (event_stream/mod.rs:121-147) and
+    Event (event_stream/event.rs:10-26) with the reference's parameter lists, so the reference's
+    own nodes (examples/benchmark/{node,sink}) compile with only their `use` line changed."""
+    import pytest
+    if not os.path.isdir(REF_NODE):
+        pytest.skip("reference tree not present")
+    api = open(os.path.join(RUST, "dora-node-api-gpu", "src", "api.rs")).read()
+    ref_node = _impl_fns(open(os.path.join(REF_NODE, "node", "mod.rs")).read(), "DoraNode")
+    ref_stream = _impl_fns(open(os.path.join(REF_NODE, "event_stream", "mod.rs")).read(),
+                           "EventStream")
+    got_node = _impl_fns(api, "DoraNode")
+    got_stream = _impl_fns(api, "EventStream")
+    for name in FACADE_NODE_FNS:
+        assert name in ref_node, name
+        assert got_node.get(name) == ref_node[name], (name, got_node.get(name), ref_node[name])
+    for name in FACADE_STREAM_FNS:
+        assert got_stream.get(name) == ref_stream[name], (name, got_stream.get(name),
+                                                         ref_stream[name])
+    ev_ref = open(os.path.join(REF_NODE, "event_stream", "event.rs")).read()
+
+    def variants(txt):
+        body = txt[txt.index("pub enum Event {"):]
+        body = body[:body.index("\n}")]
+        return re.sub(r",\s*}", " }", re.sub(r"\s+", " ", body))
+    assert variants(api) == variants(ev_ref)
+    # the crate root re-exports what the reference's lib.rs does for these nodes
+    lib = open(os.path.join(RUST, "dora-node-api-gpu", "src", "lib.rs")).read()
+    for sym in ("pub use arrow;", "pub use dora_arrow_convert::*;", "pub use dora_core::{self, uhlc};",
+                "DoraNode", "Event", "EventStream", "MetadataParameters", "Metadata"):
+        assert sym in lib, sym
