@@ -715,6 +715,8 @@ def main():
             seq += 1
             d0 = node.dataflow_counters("sink")["dropped_inputs"]
             bs0 = device.aql_batch_stats(local_rank)
+            st0 = node.stats()
+            node.set_profiling(False)  # resets the send-phase counters for this size
             # small sizes run ~1-2 us per message: >= 2000 of them, so a host hiccup does not
             # set the rate of a ~0.3 ms burst
             tp_n = args.tp_n if size > (4 << 20) else max(args.tp_n, 2000)
@@ -730,6 +732,8 @@ def main():
             # falls behind: only delivered messages count
             dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
             bs1 = device.aql_batch_stats(local_rank)
+            st1 = node.stats()
+            phases = node.send_profile()
             got = tp_n - dropped
             tp_ladder[str(size)] = {"GBps": round(got * size / dt / 1e9, 2),
                                     "msgs_per_s": round(got / dt, 1),
@@ -739,7 +743,13 @@ def main():
                                     "dropped": dropped,
                                     # sends that left in batch packs (aql.cpp), and batches
                                     "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"],
-                                    "batches": bs1["batches"] - bs0["batches"]}
+                                    "batches": bs1["batches"] - bs0["batches"],
+                                    # where a send's host time goes, and whether its slots
+                                    # came from the cache (verdict r02: the bimodal 40.96 MB
+                                    # Python ladder)
+                                    "send_phase_us": {k: round(v, 3) for k, v in phases.items()},
+                                    "slots_created": st1["slots_created"] - st0["slots_created"],
+                                    "cache_hits": st1["cache_hits"] - st0["cache_hits"]}
             for b in bufs:
                 b.free()
 

@@ -347,6 +347,14 @@ AqlQueue* create(int device) {
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
       break;
     a->nq = i + 1;
+    // DORA_GPU_AQL_PRIORITY=high|low: the queues' scheduling priority against other queues
+    // of the GPU (other processes, HIP streams); default normal
+    if (const char* pr = std::getenv("DORA_GPU_AQL_PRIORITY")) {
+      const std::string v(pr);
+      if (v == "high" || v == "low")
+        (void)hsa_amd_queue_set_priority(
+            a->qs[i], v == "high" ? HSA_AMD_QUEUE_PRIORITY_HIGH : HSA_AMD_QUEUE_PRIORITY_LOW);
+    }
   }
   if (a->nq == 0) {
     hsa_amd_memory_pool_free(ring);

@@ -213,6 +213,12 @@ int main() {
   uint64_t slots = 0, hits = 0, inflight = 0, dropped = 0;
   dora_node_stats(node, &slots, &hits, &inflight, &dropped);
 
+  uint64_t batches = 0, batched = 0, backlogged = 0;
+  {
+    int dev = 0;
+    dora_gpu_get_device(&dev);
+    dora_gpu_aql_batch_stats(dev, &batches, &batched, &backlogged);
+  }
   uint64_t bgroups = 0, bsent = 0;
   const char* berr = "";
   dora_node_bcast_stats(node, &bgroups, nullptr, &bsent, nullptr, nullptr, &berr);
@@ -224,13 +230,14 @@ int main() {
                "\"send_phase_us\": {\"alloc_us\": %.2f, \"launch_us\": %.2f, \"fill_us\": %.2f, "
                "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu, "
                "\"bcast_groups\": %llu, \"bcast_sent\": %llu, \"bcast_error\": \"%s\", "
-               "\"tp_busy_us_per_msg\": %.3f}\n",
+               "\"tp_busy_us_per_msg\": %.3f, \"aql_batches\": %llu, \"aql_batched_msgs\": %llu}\n",
                errors, ok ? "true" : "false", acks, (unsigned long long)tp_size, tp_n, tp_s,
                tp_s > 0 ? delivered / tp_s / 1e9 : 0.0,
                tp_s > 0 ? double(tp_size) * double(tp_n) / tp_s / 1e9 : 0.0, phase[0], phase[1],
                phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits,
                (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str(),
-               tp_n > 0 ? (tp_s * 1e9 - double(idle1 - idle0)) / 1e3 / double(tp_n) : 0.0);
+               tp_n > 0 ? (tp_s * 1e9 - double(idle1 - idle0)) / 1e3 / double(tp_n) : 0.0,
+               (unsigned long long)batches, (unsigned long long)batched);
   if (f != stdout) std::fclose(f);
   for (auto& kv : src) {
     dora_gpu_free(kv.second.ptr);

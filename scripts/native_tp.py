@@ -57,6 +57,7 @@ def main():
                           "us_per_msg": round(size / (r["tp_delivered_GBps"] * 1e3), 3)
                           if r.get("tp_delivered_GBps") else None,
                           "send_phase_us": r.get("send_phase_us"), "ok": r.get("ok"),
+                          "aql_batched_msgs": r.get("aql_batched_msgs"),
                           "busy_us_per_msg": {
                               "source": r.get("tp_busy_us_per_msg"),
                               "sink": sink.get("busy_us_per_input"),
