@@ -152,10 +152,10 @@ def aql_kernel_name(workload: str, body: int) -> str:
 
 def pmc_traffic(msg_bytes: int):
     """HBM bytes per pack launch from the newest committed PMC run for this message size
-    (profiles/*pack_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md)."""
+    (profiles/r*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md)."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pack_pmc_traffic.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
@@ -526,6 +526,8 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
                      "kernel": aql_kernel_name("c3", S),
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
                      "region_packs": packs, "algorithmic_bytes_per_launch": 2 * S,
+                     "traffic": (pmc_traffic(S) or (None, None))[1],
+                     "traffic_source": (pmc_traffic(S) or (None, None))[0],
                      "region_kernels": {k: kern1[k] - kern0.get(k, 0) for k in kern1
                                         if kern1[k] - kern0.get(k, 0)},
                      "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"]},
@@ -834,6 +836,23 @@ def main():
     stats["fill_paths"] = node.fill_paths()
     # the timed region's packs, each from its own stamps (first workgroup start -> fill signal)
     intervals = node.pack_intervals() if region else []
+    # the default (synchronous) send at the headline size: each send returns once its pack has
+    # read the source, as the reference's copy inside send_output
+    sync_headline = None
+    if not sync_sends and world == 1 and args.steps:
+        node.set_async_sends(False)
+        n_sync = min(20, args.steps)
+        t_s = time.perf_counter()
+        for k in range(n_sync):
+            send(k, {"seq": seq})
+            seq += 1
+        node.send_output("throughput", b"", {"seq": seq, "ack": True})
+        wait_ack(seq)
+        seq += 1
+        dt_s = time.perf_counter() - t_s
+        node.set_async_sends(True)
+        sync_headline = {"msgs": n_sync, "GBps": round(n_sync * S / dt_s / 1e9, 1),
+                         "us_per_msg": round(dt_s / n_sync * 1e6, 2)}
     c3 = None
     if args.workload == "c2" and not args.no_c3 and world == 1 and args.c3_steps > 0:
         seq, c3 = run_c3_block(node, stream, wait_ack, seq, steps=args.c3_steps)
@@ -953,6 +972,10 @@ def main():
         "sink_dropped_inputs": sink.get("dropped_inputs"),
         "node_stats": stats, "exit_codes": codes,
     }
+    line["send_mode"] = ("synchronous (DORA_BENCH_SYNC_SENDS=1)" if sync_sends else
+                         "DORA_SEND_ASYNC: the benchmark node never rewrites its sources")
+    if sync_headline is not None:
+        line["sync_send_headline"] = sync_headline
     if c3 is not None:
         s3 = [x for x in sink.get("series", []) if x["size"] == c3["msg_bytes"]]
         c3["parity"]["verified_msgs"] = sum(x["verified"] for x in s3)

@@ -39,6 +39,7 @@ def main():
     from dora_amd.node import Node
     from dora_amd.workloads import point_cloud
     node = Node("node", dataflow=df.shm, device=0)
+    node.set_async_sends(True)  # sources never rewritten: packs overlap
     if a.size:
         s = device.Stream()
         srcs = [device.DeviceBuffer(a.size) for _ in range(max(2, min(16, (640 << 20) // a.size)))]

@@ -44,6 +44,7 @@ def main():
     ]}
     df = Dataflow(desc).start()
     node = Node("node", dataflow=df.shm, device=0)
+    node.set_async_sends(True)  # sources never rewritten: packs overlap
     stream = device.Stream()
     bufs = [device.DeviceBuffer(a.size) for _ in range(a.sources)]
     for b in bufs:

@@ -40,6 +40,7 @@ def main():
     ]}
     df = Dataflow(desc).start()
     node = Node("node", dataflow=df.shm, device=0)
+    node.set_async_sends(True)  # sources never rewritten: packs overlap
     stream = device.Stream()
     seq = 0
     out = []
