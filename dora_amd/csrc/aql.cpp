@@ -672,13 +672,15 @@ void prune(AqlQueue* a, int i) {
     o.pop_front();
 }
 
-// The queue with the fewest outstanding packets below the depth (ties: round robin), or -1.
-int pick_queue(AqlQueue* a) {
+// The queue with the fewest outstanding packets below the depth (ties: round robin) among the
+// first `nq` (0: all), or -1.
+int pick_queue(AqlQueue* a, int nq = 0) {
   if (a->hold) return -1;
+  if (nq <= 0 || nq > a->nq) nq = a->nq;
   int best = -1;
   size_t best_n = queue_depth();
-  for (int j = 0; j < a->nq; ++j) {
-    const int i = int((a->next + uint64_t(j)) % uint64_t(a->nq));
+  for (int j = 0; j < nq; ++j) {
+    const int i = int((a->next + uint64_t(j)) % uint64_t(nq));
     prune(a, i);
     if (a->outq[i].size() < best_n) {
       best = i;
@@ -688,26 +690,51 @@ int pick_queue(AqlQueue* a) {
   return best;
 }
 
+// Bytes a batch may carry (DORA_GPU_AQL_BATCH_BYTES, default the barrier size), and the size from
+// which a batch runs like a big pack — barrier bit, at most three queues — instead of
+// overlapping on all four (DORA_GPU_AQL_BATCH_BIG_BYTES, default: never).
+uint64_t batch_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BATCH_BYTES");
+    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
+    return x ? x : barrier_bytes();
+  }();
+  return v;
+}
+uint64_t batch_big_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BATCH_BIG_BYTES");
+    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
+    return x ? x : ~uint64_t(0);
+  }();
+  return v;
+}
+
 // Dispatch the backlog into queues with room, as batches of consecutive sends that share a
 // chunk size (a->mu held).
 void pump_locked(AqlQueue* a) {
   while (!a->backlog.empty() && !a->failed.load()) {
-    const int qi = pick_queue(a);
-    if (qi < 0) return;
-    Pending batch[kBatchMsgs];
+    // the batch at the front of the backlog
     size_t n = 0, segs = 0;
     uint64_t bytes = 0;
-    while (n < kBatchMsgs && !a->backlog.empty()) {
-      const Pending& p = a->backlog.front();
-      if (n && (segs + p.n > kBatchSegs || p.chunk != batch[0].chunk ||
-                bytes + p.bytes > barrier_bytes()))
+    for (const Pending& p : a->backlog) {
+      if (n == kBatchMsgs) break;
+      if (n && (segs + p.n > kBatchSegs || p.chunk != a->backlog.front().chunk ||
+                bytes + p.bytes > batch_bytes()))
         break;
       segs += p.n;
       bytes += p.bytes;
-      batch[n++] = p;
+      ++n;
+    }
+    const bool big = n > 1 && bytes >= batch_big_bytes();
+    const int qi = pick_queue(a, big ? 3 : 0);
+    if (qi < 0) return;
+    Pending batch[kBatchMsgs];
+    for (size_t k = 0; k < n; ++k) {
+      batch[k] = a->backlog.front();
       a->backlog.pop_front();
     }
-    if (dispatch_locked(a, size_t(qi), batch, n, false) != DORA_OK) {
+    if (dispatch_locked(a, size_t(qi), batch, n, big) != DORA_OK) {
       // the fills of these messages never signal: their receivers report them failed
       a->failed.store(true);
       return;

@@ -28,7 +28,15 @@ def main():
     ap.add_argument("--sizes", default="1048576,4096000,16777216")
     ap.add_argument("--n", type=int, default=2000)
     ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--cfg", action="append", default=[],
+                    help="name=K=V[,K=V...]: replaces the built-in configs")
     a = ap.parse_args()
+    if a.cfg:
+        CONFIGS.clear()
+        for c in a.cfg:
+            name, _, kv = c.partition("=")
+            CONFIGS[name] = dict(x.split("=", 1) for x in kv.split(",") if x)
+        a.configs = ",".join(CONFIGS)
     import bench
     for r in range(a.rounds):
         for name in a.configs.split(","):
