@@ -35,6 +35,7 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
 struct Variant {
   int unroll;
   bool nt;
+  bool wt = false;  // write-through (sc1 nt) stores without a fill signal (microbenchmark)
 };
 
 std::atomic<int> g_unroll{0};       // 0 = default (4) / env
@@ -74,7 +75,10 @@ Variant pack_variant() {
   }();
   Variant v = env;
   if (const int u = g_unroll.load(std::memory_order_relaxed)) v.unroll = u;
-  if (const int nt = g_nt.load(std::memory_order_relaxed); nt >= 0) v.nt = nt != 0;
+  if (const int nt = g_nt.load(std::memory_order_relaxed); nt >= 0) {
+    v.nt = nt != 0;
+    v.wt = nt == 2;
+  }
   return v;
 }
 
@@ -329,6 +333,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     void (*kern)(PackArgs) = pack_kernel<4, 0>;
     if (var.unroll == 8) kern = var.nt ? pack_kernel<8, 1> : pack_kernel<8, 0>;
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, 1> : pack_kernel<2, 0>;
+    else if (var.wt) kern = pack_kernel<4, 2>;
     else if (var.nt) kern = pack_kernel<4, 1>;
     if (last && signal) {
       // signalling launch: write-through stores, at most kMaxSignalWgs workgroups
@@ -652,7 +657,9 @@ int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
   if (chunk_bytes % dora::pack::kLine)
     return dora::fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 128 (a cache line)");
   dora::g_unroll.store(unroll);
-  dora::g_nt.store(nontemporal < 0 ? -1 : (nontemporal ? 1 : 0));
+  // 2: the signalling kernels' write-through stores in a launch that signals nothing (to
+  // separate the store policy's cost from the fill signal's in scripts/pack_microbench.py)
+  dora::g_nt.store(nontemporal < 0 ? -1 : nontemporal == 2 ? 2 : (nontemporal ? 1 : 0));
   dora::g_chunk.store(chunk_bytes);
   return DORA_OK;
 }

@@ -178,8 +178,9 @@ int dora_gpu_plan_type_info(const dora_plan* plan, uint8_t* buf, size_t cap, siz
  */
 int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_t stream);
 /* Tuning knob of the pack kernel (process-wide): 16-B loads in flight per lane (0 = default,
- * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1), bytes per workgroup (0 = auto,
- * else a multiple of 128: chunks start on cache lines). */
+ * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1; 2 = the signalling kernels'
+ * write-through stores without a signal, a microbenchmark variant), bytes per workgroup (0 =
+ * auto, else a multiple of 128: chunks start on cache lines). */
 int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
 /* Tuning of packs that signal their fill from the kernel (node sends): workgroups of such a
  * launch, which then strides over the chunks (0: up to 4096).  With `bench_signal`,

@@ -42,8 +42,9 @@ def main():
         variants = [("memcpy", 0, 0, 0)] + [("pack", u, nt, ch) for u, nt, ch in itertools.product(
             [2, 4, 8], [1], [0, 4096, 8192, 16384, 20480, 32768])]
     elif args.signal_sweep:
-        # (kind, signalling grid): the pack signals a scratch flag from its workgroup 0
-        variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)] + [
+        # (kind, signalling grid): the pack signals a scratch flag from its workgroup 0;
+        # ("pack", 0, 2, 0): the same write-through stores without the signal
+        variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0), ("pack", 0, 2, 0)] + [
             ("sig", w, u, ch) for w in [512, 1024] for u in [0, 4, 8]
             for ch in [0, 8192, 16384, 32768]]
     else:
