@@ -684,6 +684,26 @@ int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uin
   return rc;
 }
 
+int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
+                             const uint64_t* dsts, const uint64_t* dst_caps,
+                             const uint64_t* flags, const uint64_t* epochs, uint8_t* out,
+                             size_t cap, uint32_t* grid) {
+  if (!n_msgs || !seg_counts || !segs || !dsts || !dst_caps || !flags || !epochs || !out || !grid)
+    return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  if (n_msgs > 8) return dora::fail(DORA_ERR_INVALID, "batch of %zu messages", n_msgs);
+  std::vector<std::vector<dora::Segment>> s(n_msgs);
+  dora::BatchItem items[8];
+  size_t k = 0;
+  for (size_t m = 0; m < n_msgs; ++m) {
+    for (size_t j = 0; j < seg_counts[m]; ++j, ++k)
+      s[m].push_back({reinterpret_cast<const void*>(segs[3 * k]), segs[3 * k + 1], segs[3 * k + 2]});
+    items[m] = {s[m].data(), s[m].size(), reinterpret_cast<uint8_t*>(dsts[m]),
+                dora::FillSignal{reinterpret_cast<uint64_t*>(flags[m]), epochs[m], nullptr},
+                dst_caps[m]};
+  }
+  return dora::build_aql_batch_args(items, n_msgs, out, cap, grid);
+}
+
 int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream) {
   if (!data && len) return dora::fail(DORA_ERR_INVALID, "data is NULL");
   return dora::launch_l2_touch(data, len, static_cast<hipStream_t>(stream));

@@ -234,6 +234,14 @@ int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
  * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
  * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
 int dora_gpu_test_aql_hold(int device, int hold);
+/* Test tool (host only): the 640-byte argument block of a batch pack (dora_aql_packb_u4) for
+ * `n_msgs` (<= 8) messages; message m has seg_counts[m] segments, given as (src, dst_off, len)
+ * triples in `segs`, its slot at dsts[m] with dst_caps[m] writable bytes, and fill flag /
+ * epoch flags[m] / epochs[m].  *grid = the workgroups the dispatch would launch. */
+int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
+                             const uint64_t* dsts, const uint64_t* dst_caps,
+                             const uint64_t* flags, const uint64_t* epochs, uint8_t* out,
+                             size_t cap, uint32_t* grid);
 int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
 void dora_gpu_test_bar_free(void* ptr);
 
