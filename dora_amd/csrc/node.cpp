@@ -159,6 +159,29 @@ size_t max_in_flight(uint64_t len) {
   return len < kSmallInFlightBytes ? 11 : 8;
 }
 
+// Opt-in (DORA_GPU_SPLIT_IN_FLIGHT=1): the cap above bounds only the samples whose fill has
+// COMPLETED and whose token is not back, while samples still being packed count against this
+// larger total (24 below 8 MiB, 12 below 32 MiB, 8 above; DORA_GPU_MAX_TOTAL_IN_FLIGHT), so a
+// burst keeps the GPU's queues and batch packs fed.  Not the default: fills still in transit
+// complete while a receiver pauses, so a queue_size-10 receiver that pauses during a burst then
+// finds more than 10 ready inputs and drops (r03: 473 of 2000 4 MB inputs in
+// test_default_queue_keeps_up_with_async_burst) — the total in flight is what bounds it.
+size_t max_total_in_flight(uint64_t len) {
+  static const long env = [] {
+    const char* e = std::getenv("DORA_GPU_MAX_TOTAL_IN_FLIGHT");
+    return e ? std::atol(e) : 0L;
+  }();
+  static const bool split = [] {
+    const char* e = std::getenv("DORA_GPU_SPLIT_IN_FLIGHT");
+    return e && *e == '1';
+  }();
+  const size_t cap = max_in_flight(len);
+  if (!split) return cap;
+  if (env > 0) return std::max(cap, static_cast<size_t>(env));
+  const size_t d = len < kSmallInFlightBytes ? 24 : len < (uint64_t(32) << 20) ? 12 : 8;
+  return std::max(cap, d);
+}
+
 // Streams the sends of a node spread their fills over (DORA_GPU_FILL_STREAMS, default 3).  A
 // pack ends in a drain tail (its last workgroups, the fill signal) and starts with a ramp; on
 // one stream consecutive fills serialise those, on three hardware queues the next fill streams
@@ -624,6 +647,9 @@ struct dora_node {
   // samples sent, by drop token (map nodes from a pool: no malloc per send)
   std::pmr::unsynchronized_pool_resource sent_pool;
   std::pmr::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out{&sent_pool};
+  // fills of sent samples not yet seen complete, in send order (flag, epoch): the in-transit
+  // part of sent_out (max_total_in_flight)
+  std::deque<std::pair<const std::atomic<uint64_t>*, uint64_t>> transit;
   dora::WBuf send_buf;                 // request encoding scratch of send_sample, reused
   std::vector<uint8_t> ti_buf;         // type-info scratch of pack_and_send, reused
   dora_plan bytes_plan;                // send_output_bytes: the one-buffer plan, re-pointed
@@ -1369,10 +1395,27 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
   SubSpan sp_track(SP_SEND_TRACK);
   if (slot) {
     n->sent_out[d.ipc.token] = slot;
+    if (d.ipc.fill == FILL_FLAG) {
+      auto& t = n->transit;
+      t.emplace_back(n->core->flag_host(static_cast<int>(d.ipc.flag_index)), d.ipc.epoch);
+      // bounded even for a sender that never reaches its cap
+      while (t.size() > 256 && t.front().first->load(std::memory_order_acquire) >= t.front().second)
+        t.pop_front();
+      if (t.size() > 1024) t.pop_front();
+    }
     if (token_out) *token_out = d.ipc.token;
     trace(TP_SENT, d.ipc.token);
   }
   return DORA_OK;
+}
+
+// Sent samples whose fill has not been seen complete (the front of `transit` completes first:
+// fills of one sender finish roughly in order; one flag load per completed fill).
+size_t in_transit(dora_node* n) {
+  auto& t = n->transit;
+  while (!t.empty() && t.front().first->load(std::memory_order_acquire) >= t.front().second)
+    t.pop_front();
+  return t.size();
 }
 
 constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
@@ -1415,8 +1458,14 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
     // reference would (a receiver may legitimately hold many inputs).
     SubSpan sp_wait(SP_ALLOC_WAIT);
     const uint64_t t0 = mono_ns();
-    while (async_sends() && n->sent_out.size() >= max_in_flight(len) &&
-           mono_ns() - t0 < slot_wait_ns()) {
+    // completed-and-unreturned samples against the cap, everything against the total
+    auto blocked = [&] {
+      const size_t total = n->sent_out.size();
+      if (total >= max_total_in_flight(len)) return true;
+      if (total < max_in_flight(len)) return false;
+      return total - std::min(total, in_transit(n)) >= max_in_flight(len);
+    };
+    while (async_sends() && blocked() && mono_ns() - t0 < slot_wait_ns()) {
       n->core->drops.wait(1000);
       handle_finished_drop_tokens(n);
       if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
