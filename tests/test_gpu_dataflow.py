@@ -711,6 +711,9 @@ def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_pa
     with Dataflow(_bench_desc(res), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
         for k in range(n_msgs):
+            # the rewrite launched after the previous send has finished before this send: a
+            # source must be complete when it is sent (only what follows a send is under test)
+            other.sync()
             node.send_output_device_bytes("data", src.ptr, size,
                                           {"seq": k, "csum": sums[k], "verify": True},
                                           asynchronous=mode == "async")
