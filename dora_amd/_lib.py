@@ -105,6 +105,15 @@ _SIGS = {
     "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
     "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
+    "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
+                                         c_void_p, c_size_t, c_uint64, c_uint64, c_void_p,
+                                         c_void_p, c_size_t, c_int, c_void_p, c_size_t,
+                                         POINTER(c_size_t)]),
+    "dora_gpu_test_ide_inputs_closed": (c_int, [c_char_p, POINTER(c_char_p), POINTER(c_char_p),
+                                                c_size_t, c_uint64, c_void_p, c_void_p,
+                                                c_size_t, POINTER(c_size_t)]),
+    "dora_gpu_test_ide_decode": (c_int, [c_void_p, c_size_t, c_char_p, c_size_t,
+                                         POINTER(c_size_t)]),
     "dora_gpu_test_batch_args": (c_int, [c_size_t, POINTER(c_size_t), POINTER(c_uint64),
                                          POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
                                          POINTER(c_uint64), c_void_p, c_size_t,

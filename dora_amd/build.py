@@ -19,7 +19,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = "gfx950"
 
 LIB_SOURCES = ["runtime.cpp", "plan.cpp", "device_array.cpp", "kernels.hip", "shm.cpp", "bcast.cpp", "operator_api.cpp", "stdout_capture.cpp",
-               "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp", "aql.cpp", "interdaemon.cpp"]
+               "wire.cpp", "trace.cpp", "daemon.cpp", "node.cpp", "aql.cpp", "interdaemon.cpp",
+               "bincode.cpp"]
 AQL_KERNELS = "aql_kernels.hip"  # standalone gfx950 code object embedded in the library
 LIB_NAME = "libdora_gpu.so"
 

@@ -147,7 +147,7 @@ class Daemon {
     if (any_remote) fwd_.reset(new Forwarder(region_.get(), dataflow_id_, peers_));
     if (listen_port_ >= 0 || !proxies_.empty())
       gw_.reset(new Gateway(shm, dataflow_id_, listen_host_, listen_port_ < 0 ? 0 : listen_port_,
-                            proxies_));
+                            proxies_, input_src_));
   }
 
   ~Daemon() {
@@ -257,6 +257,7 @@ class Daemon {
     std::vector<In> inputs;
     struct Remote {
       std::string node, out, machine;
+      std::vector<std::pair<std::string, std::string>> inputs;  // receiver/input over there
     };
     std::vector<Remote> remote_lines;
     while (std::getline(in, line)) {
@@ -293,11 +294,19 @@ class Daemon {
         ls >> name >> a.host >> a.port;
         if (ls.fail()) throw std::invalid_argument("bad machine line: " + line);
         peers_[name] = a;
-      } else if (kw == "remote") {  // remote <node> <output> <machine>: receivers over there
-        std::string node, out, machine;
-        ls >> node >> out >> machine;
+      } else if (kw == "remote") {
+        // remote <node> <output> <machine> <receiver>/<input>...: receivers over there
+        Remote r;
+        ls >> r.node >> r.out >> r.machine;
         if (ls.fail()) throw std::invalid_argument("bad remote line: " + line);
-        remote_lines.push_back({node, out, machine});
+        std::string ri;
+        while (ls >> ri) {
+          const size_t slash = ri.find('/');
+          if (slash == std::string::npos || slash == 0 || slash + 1 == ri.size())
+            throw std::invalid_argument("bad remote input `" + ri + "` in: " + line);
+          r.inputs.emplace_back(ri.substr(0, slash), ri.substr(slash + 1));
+        }
+        remote_lines.push_back(std::move(r));
       } else if (kw == "proxy") {  // proxy <node> <gpu>: a remote node feeding local inputs
         ProxySpec p;
         ls >> p.node_id >> p.device;
@@ -325,6 +334,13 @@ class Daemon {
       if (!peers_.count(r.machine))
         throw std::invalid_argument("remote line names unknown machine " + r.machine);
       remote_[idx[r.node]][r.out].push_back(r.machine);
+      auto& ri = remote_inputs_[{r.node, r.out}][r.machine];
+      ri.insert(ri.end(), r.inputs.begin(), r.inputs.end());
+    }
+    // local inputs fed by proxies (remote nodes): what an InputsClosed from their machine closes
+    for (auto& x : inputs) {
+      for (auto& p : proxies_)
+        if (p.node_id == x.src) input_src_[{x.node, x.input}] = {x.src, x.out};
     }
     for (auto& p : proxies_) {
       if (!idx.count(p.node_id)) throw std::invalid_argument("proxy of unknown node " + p.node_id);
@@ -546,7 +562,8 @@ class Daemon {
       job.machines = rit->second;
       job.node_id = nodes_[i].id;
       job.closed = true;
-      job.closed_outputs = {output};
+      auto ri = remote_inputs_.find({nodes_[i].id, output});
+      if (ri != remote_inputs_.end()) job.closed_inputs = ri->second;
       fwd_->push(std::move(job));
     }
     auto it = outputs_[i].find(output);
@@ -605,6 +622,11 @@ class Daemon {
   // inter-daemon (interdaemon.h): per node, output -> machines with receivers; peers; proxies
   static constexpr int kForwarder = -2;  // the forwarder's hold on a drop token
   std::vector<std::map<std::string, std::vector<std::string>, std::less<>>> remote_;
+  // (node, output) -> machine -> its receivers' (node, input): InputsClosed when it closes
+  std::map<std::pair<std::string, std::string>,
+           std::map<std::string, std::vector<std::pair<std::string, std::string>>>>
+      remote_inputs_;
+  Gateway::InputSources input_src_;
   std::map<std::string, PeerAddr> peers_;
   std::vector<ProxySpec> proxies_;
   std::string dataflow_id_ = "local", listen_host_ = "127.0.0.1";

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "bincode.h"
 #include "common.h"
 #include "device_array.h"
 #include "dora_gpu.h"
@@ -27,50 +28,6 @@ namespace dora {
 // node.cpp: send a sample with the producer's original timestamp (the remote message's).
 int proxy_send(dora_node* n, const char* output_id, const uint8_t* ti, size_t ti_len,
                const uint8_t* params, size_t params_len, dora_sample* sample, uint64_t ts);
-
-void encode_ide(const InterDaemonEvent& e, std::vector<uint8_t>& out) {
-  WBuf w;
-  w.u8(e.kind);
-  w.str(e.dataflow_id);
-  w.str(e.node_id);
-  if (e.kind == IDE_OUTPUT) {
-    w.str(e.output_id);
-    w.u16(e.meta_version);
-    w.u64(e.timestamp_ns);
-    w.bytes(e.type_info);
-    w.bytes(e.parameters);
-    w.u8(e.has_data ? 1 : 0);
-    if (e.has_data) w.bytes(e.data);
-  } else {
-    w.u32(static_cast<uint32_t>(e.outputs.size()));
-    for (const auto& o : e.outputs) w.str(o);
-  }
-  out = w.take();
-}
-
-InterDaemonEvent decode_ide(const uint8_t* p, size_t n) {
-  RBuf r(p, n);
-  InterDaemonEvent e;
-  e.kind = r.u8();
-  e.dataflow_id = r.str();
-  e.node_id = r.str();
-  if (e.kind == IDE_OUTPUT) {
-    e.output_id = r.str();
-    e.meta_version = r.u16();
-    e.timestamp_ns = r.u64();
-    e.type_info = r.bytes();
-    e.parameters = r.bytes();
-    e.has_data = r.u8() != 0;
-    if (e.has_data) e.data = r.bytes();
-  } else if (e.kind == IDE_OUTPUTS_CLOSED) {
-    const uint32_t k = r.u32();
-    for (uint32_t i = 0; i < k; ++i) e.outputs.push_back(r.str());
-  } else {
-    throw std::invalid_argument("unknown inter-daemon event kind");
-  }
-  if (r.pos() != r.size()) throw std::invalid_argument("trailing bytes in inter-daemon event");
-  return e;
-}
 
 namespace {
 
@@ -142,6 +99,10 @@ std::string ipc_key(const DeviceIpc& d) {
 Forwarder::Forwarder(Region* region, std::string dataflow_id,
                      std::map<std::string, PeerAddr> peers)
     : region_(region), dataflow_id_(std::move(dataflow_id)), peers_(std::move(peers)) {
+  // a random uhlc ID, as uhlc's HLC::default() draws one (non-zero: ID wraps a NonZeroU128)
+  const DropToken t = generate_drop_token();
+  std::memcpy(hlc_id_.data(), t.b, 16);
+  hlc_id_[0] |= 1;
   th_ = std::thread([this] { loop(); });
 }
 
@@ -293,10 +254,25 @@ bool Forwarder::send_to(const std::string& machine, const std::vector<uint8_t>& 
 void Forwarder::handle(ForwardJob& job) {
   InterDaemonEvent e;
   e.dataflow_id = dataflow_id_;
+  e.hlc_id = hlc_id_;
+  e.event_ns = now_ns();
   e.node_id = job.node_id;
   if (job.closed) {
-    e.kind = IDE_OUTPUTS_CLOSED;
-    e.outputs = job.closed_outputs;
+    // InputsClosed per machine, naming its receivers' inputs (lib.rs:1418-1440)
+    e.kind = IDE_INPUTS_CLOSED;
+    for (const auto& kv : job.closed_inputs) {
+      e.inputs = kv.second;
+      std::vector<uint8_t> frame;
+      try {
+        encode_ide(e, frame);
+      } catch (const std::exception& ex) {
+        std::fprintf(stderr, "dora-gpu daemon: forwarding: %s\n", ex.what());
+        continue;
+      }
+      send_to(kv.first, frame);
+    }
+    forwarded_.fetch_add(1, std::memory_order_relaxed);
+    return;
   } else {
     e.kind = IDE_OUTPUT;
     e.output_id = job.output_id;
@@ -333,7 +309,13 @@ void Forwarder::handle(ForwardJob& job) {
     }
   }
   std::vector<uint8_t> frame;
-  encode_ide(e, frame);
+  try {
+    encode_ide(e, frame);
+  } catch (const std::exception& ex) {
+    std::fprintf(stderr, "dora-gpu daemon: forwarding `%s/%s`: %s; dropped\n", job.node_id.c_str(),
+                 job.output_id.c_str(), ex.what());
+    return;
+  }
   for (const auto& m : job.machines) send_to(m, frame);
   forwarded_.fetch_add(1, std::memory_order_relaxed);
 }
@@ -342,8 +324,11 @@ void Forwarder::handle(ForwardJob& job) {
 // Gateway
 // ------------------------------------------------------------------------------------------
 Gateway::Gateway(std::string shm_name, std::string dataflow_id, std::string listen_host,
-                 int listen_port, std::vector<ProxySpec> proxies)
-    : shm_(std::move(shm_name)), dataflow_id_(std::move(dataflow_id)) {
+                 int listen_port, std::vector<ProxySpec> proxies, InputSources input_src)
+    : shm_(std::move(shm_name)),
+      dataflow_id_(std::move(dataflow_id)),
+      dataflow_uuid_(dataflow_uuid(dataflow_id_)),
+      input_src_(std::move(input_src)) {
   listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
   if (listen_fd_ < 0) throw std::runtime_error("gateway: socket");
   int one = 1;
@@ -453,20 +438,40 @@ void Gateway::read_loop(int fd) {
       std::fprintf(stderr, "dora-gpu daemon: bad inter-daemon frame: %s\n", ex.what());
       break;
     }
-    if (e.dataflow_id != dataflow_id_) {
-      std::fprintf(stderr, "dora-gpu daemon: event of dataflow `%s` (this is `%s`) ignored\n",
-                   e.dataflow_id.c_str(), dataflow_id_.c_str());
+    if (e.dataflow_uuid != dataflow_uuid_) {
+      std::fprintf(stderr, "dora-gpu daemon: event of another dataflow (this is `%s`) ignored\n",
+                   dataflow_id_.c_str());
       continue;
     }
-    auto it = proxies_.find(e.node_id);
-    if (it == proxies_.end()) continue;  // no local receiver of that node
+    auto deliver = [this](const std::string& node, InterDaemonEvent&& ev) {
+      auto it = proxies_.find(node);
+      if (it == proxies_.end()) return;  // no local receiver of that node
+      Proxy* p = it->second.get();
+      {
+        std::lock_guard<std::mutex> g(p->mu);
+        p->q.push_back(std::move(ev));
+      }
+      p->cv.notify_one();
+    };
     received_.fetch_add(1, std::memory_order_relaxed);
-    Proxy* p = it->second.get();
-    {
-      std::lock_guard<std::mutex> g(p->mu);
-      p->q.push_back(std::move(e));
+    if (e.kind == IDE_INPUTS_CLOSED) {
+      // the closed inputs -> the proxy outputs feeding them (lib.rs:581-592 closes the inputs;
+      // here the proxy closes its output, which closes every local input it feeds)
+      std::map<std::string, std::vector<std::string>> by_src;
+      for (const auto& in : e.inputs) {
+        auto s = input_src_.find(in);
+        if (s != input_src_.end()) by_src[s->second.first].push_back(s->second.second);
+      }
+      for (auto& kv : by_src) {
+        InterDaemonEvent c;
+        c.kind = IDE_PROXY_CLOSE;
+        c.outputs = std::move(kv.second);
+        deliver(kv.first, std::move(c));
+      }
+      continue;
     }
-    p->cv.notify_one();
+    const std::string node = e.node_id;
+    deliver(node, std::move(e));
   }
   {
     std::lock_guard<std::mutex> g(readers_mu_);
@@ -497,7 +502,7 @@ void Gateway::proxy_loop(Proxy* p) {
           // the remote node's daemon went away without closing its outputs: close them here
           std::fprintf(stderr, "dora-gpu daemon: peers of proxy `%s` gone; closing its outputs\n",
                        p->spec.node_id.c_str());
-          e.kind = IDE_OUTPUTS_CLOSED;
+          e.kind = IDE_PROXY_CLOSE;
           e.outputs = open;
         } else {
           continue;
@@ -508,7 +513,7 @@ void Gateway::proxy_loop(Proxy* p) {
       }
     }
 
-    if (e.kind == IDE_OUTPUTS_CLOSED) {
+    if (e.kind == IDE_PROXY_CLOSE) {
       std::vector<const char*> ids;
       for (const auto& o : e.outputs) {
         auto k = std::find(open.begin(), open.end(), o);

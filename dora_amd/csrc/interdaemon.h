@@ -15,16 +15,13 @@
 // proxies, an inline sample for host-only ones), so local receivers see an ordinary input;
 // OutputsClosed closes the proxy's outputs and, once all are closed, finishes the proxy.
 //
-// Wire (little endian, one frame = u64 length + payload; str / bytes = u64 length + bytes):
-//   u8 kind, str dataflow_id, str node_id,
-//   kind 0 Output:        str output_id, u16 metadata_version, u64 timestamp_ns,
-//                         bytes type_info (C ABI form, validity inline), bytes parameters,
-//                         u8 has_data [bytes data]
-//   kind 1 OutputsClosed: u32 n, n x str output_id
-// The reference frames bincode of Timestamped<InterDaemonEvent>; its InputsClosed names the
-// receiving inputs, ours the closed outputs (the receiving daemon maps them to its inputs).
+// Wire: the reference's — one frame = u64 little-endian length + bincode of
+// Timestamped<InterDaemonEvent> (bincode.h); InputsClosed names the receivers' inputs on the
+// machine it is sent to (lib.rs:1398-1440), which the receiving daemon maps to the proxy outputs
+// feeding them.
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -41,22 +38,24 @@
 
 namespace dora {
 
-enum : uint8_t { IDE_OUTPUT = 0, IDE_OUTPUTS_CLOSED = 1 };
+// InterDaemonEvent variants (wire indices), and the gateway's own close request to a proxy
+enum : uint8_t { IDE_OUTPUT = 0, IDE_INPUTS_CLOSED = 1, IDE_PROXY_CLOSE = 2 };
 
 struct InterDaemonEvent {
   uint8_t kind = IDE_OUTPUT;
-  std::string dataflow_id, node_id;
-  std::string output_id;                 // Output
-  std::vector<std::string> outputs;      // OutputsClosed
+  std::string dataflow_id;                  // sending: this dataflow's id (bincode.h dataflow_uuid)
+  std::array<uint8_t, 16> dataflow_uuid{};  // received
+  std::string node_id, output_id;           // Output
+  std::vector<std::pair<std::string, std::string>> inputs;  // InputsClosed: (receiver, input)
+  std::vector<std::string> outputs;         // IDE_PROXY_CLOSE: the proxy outputs to close
   uint16_t meta_version = 0;
-  uint64_t timestamp_ns = 0;
+  uint64_t timestamp_ns = 0;                // Metadata.timestamp (UNIX ns)
+  uint64_t event_ns = 0;                    // Timestamped.timestamp (UNIX ns)
+  std::array<uint8_t, 16> hlc_id{};         // the sending daemon's uhlc ID (non-zero)
   std::vector<uint8_t> type_info, parameters;
   bool has_data = false;
   std::vector<uint8_t> data;
 };
-
-void encode_ide(const InterDaemonEvent& e, std::vector<uint8_t>& out);
-InterDaemonEvent decode_ide(const uint8_t* p, size_t n);  // throws on malformed input
 
 struct PeerAddr {
   std::string host;
@@ -69,8 +68,8 @@ struct ForwardJob {
   std::string node_id, output_id;
   std::vector<uint8_t> tail;  // the request's metadata + data bytes (REQ_SEND_MESSAGE tail)
   DataMsg data;
-  bool closed = false;                   // OutputsClosed instead of a message
-  std::vector<std::string> closed_outputs;
+  bool closed = false;  // InputsClosed instead of a message: per machine, its inputs to close
+  std::map<std::string, std::vector<std::pair<std::string, std::string>>> closed_inputs;
 };
 
 class Forwarder {
@@ -95,6 +94,7 @@ class Forwarder {
   std::map<std::string, PeerAddr> peers_;
   std::map<std::string, int> socks_;
   std::map<std::string, uint64_t> down_until_;  // a peer that refused us: skip it until then
+  std::array<uint8_t, 16> hlc_id_{};             // this daemon's uhlc ID (random, non-zero)
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<ForwardJob> q_;
@@ -118,8 +118,11 @@ struct ProxySpec {
 
 class Gateway {
  public:
+  // `input_src`: the local inputs fed by remote nodes, (receiver, input) -> (source, output)
+  using InputSources =
+      std::map<std::pair<std::string, std::string>, std::pair<std::string, std::string>>;
   Gateway(std::string shm_name, std::string dataflow_id, std::string listen_host, int listen_port,
-          std::vector<ProxySpec> proxies);
+          std::vector<ProxySpec> proxies, InputSources input_src);
   ~Gateway();
   int port() const { return port_; }
   uint64_t received() const { return received_.load(); }
@@ -137,11 +140,13 @@ class Gateway {
   void proxy_loop(Proxy* p);
 
   std::string shm_, dataflow_id_;
+  std::array<uint8_t, 16> dataflow_uuid_{};
+  InputSources input_src_;
   int listen_fd_ = -1, port_ = 0;
   std::atomic<bool> stop_{false};
   // peer connections: once every peer that connected has gone for longer than the grace period
   // (DORA_GPU_PEER_GRACE_MS, default 10 s) the proxies close their outputs — a crashed remote
-  // daemon never sends OutputsClosed, and the local dataflow must still finish
+  // daemon never sends InputsClosed, and the local dataflow must still finish
   std::atomic<int> conns_{0};
   std::atomic<bool> ever_connected_{false};
   std::atomic<uint64_t> last_disconnect_ns_{0};

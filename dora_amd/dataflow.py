@@ -179,14 +179,15 @@ def daemon_spec(nodes: List[NodeSpec], machine: Optional[str] = None,
         lines.append(f"proxy {src} {gpu}")
     for n in local:
         lines += [f"input {n.id} {i} {s} {o} {q}" for i, (s, o, q) in n.inputs.items()]
-    remote = set()
+    remote = {}  # (src, out, machine) -> receivers' (node, input) there (InputsClosed)
     for n in nodes:
         if n.id in local_ids:
             continue
-        for _, (src, out, _) in n.inputs.items():
+        for inp, (src, out, _) in n.inputs.items():
             if src in local_ids:
-                remote.add((src, out, n.machine))
-    lines += [f"remote {s} {o} {m}" for s, o, m in sorted(remote)]
+                remote.setdefault((src, out, n.machine), set()).add((n.id, inp))
+    lines += [" ".join([f"remote {s} {o} {m}"] + [f"{r}/{i}" for r, i in sorted(ins)])
+              for (s, o, m), ins in sorted(remote.items())]
     return "\n".join(lines) + "\n"
 
 

@@ -244,6 +244,22 @@ int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint
                              size_t cap, uint32_t* grid);
 int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
 void dora_gpu_test_bar_free(void* ptr);
+/* Test hooks of the inter-daemon wire, bincode of Timestamped<InterDaemonEvent> (replaces
+ * bincode::serialize in binaries/daemon/src/inter_daemon.rs:66 and its deserialize at :156;
+ * layouts in csrc/bincode.h): an Output event built from this library's type-info and parameter
+ * encodings, an InputsClosed event of `n` (receiver, input) pairs, and a frame decoded into
+ * JSON.  `hlc_id`: 16 bytes.  A buffer too small fails with *len set to the size needed. */
+int dora_gpu_test_ide_output(const char* dataflow_id, const char* node_id, const char* output_id,
+                             const uint8_t* type_info, size_t type_info_len, const uint8_t* params,
+                             size_t params_len, uint64_t meta_ns, uint64_t event_ns,
+                             const uint8_t* hlc_id, const uint8_t* data, size_t data_len,
+                             int has_data, uint8_t* out, size_t cap, size_t* out_len);
+int dora_gpu_test_ide_inputs_closed(const char* dataflow_id, const char* const* receivers,
+                                    const char* const* inputs, size_t n, uint64_t event_ns,
+                                    const uint8_t* hlc_id, uint8_t* out, size_t cap,
+                                    size_t* out_len);
+int dora_gpu_test_ide_decode(const uint8_t* frame, size_t len, char* json, size_t cap,
+                             size_t* json_len);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Node API — replaces DoraNode / EventStream (apis/rust/node/src/node/mod.rs:42-503,         */
