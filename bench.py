@@ -461,13 +461,14 @@ C3_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "g
                          "c3_cloud.json")
 
 
-def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
+def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24, steady_steps=200):
     """BASELINE configs[2] beside the C2 headline: `send_output` of device-resident 1M-point
     clouds (List<Struct<x,y,z:f32,intensity:u8>>, 16 lists, validity bitmaps; one multi-segment
     AQL pack each), `steps` back-to-back sends from `nsrc` rotating clouds, device time from the
     packs' own stamps.  Parity: the last 4 timed clouds are held by the sink and checksummed
     against the CPU oracle's sample (tests/golden/c3_cloud.json, make_c3_golden.py), and so is
-    a reference pack of the same cloud made before the clock."""
+    a reference pack of the same cloud made before the clock.  `steady`: a second region of
+    `steady_steps` sends, the pipeline's steady state."""
     from dora_amd import device
     from dora_amd.arrow_utils import Plan
     from dora_amd.device import DeviceArray
@@ -490,6 +491,28 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     wait_ack(seq)
     seq += 1
+    # the same pipeline over `steady_steps` sends first: the steady state without the first
+    # packs' ramp and the last ones' drain (reported beside the 20-step figure, which stays the
+    # line's; before it, since the sink holds that region's late-verified clouds)
+    steady = None
+    if steady_steps > 0:
+        node.region_begin()
+        t_s = time.perf_counter()
+        for k in range(steady_steps):
+            node.send_output("throughput", srcs[k % nsrc],
+                             {"seq": seq, "ack": True} if k == steady_steps - 1 else {"seq": seq})
+            seq += 1
+        node.region_mark()
+        wait_ack(seq - 1)
+        node.sync()
+        dt_s = time.perf_counter() - t_s
+        r2 = node.region_end()
+        if r2["span_ms"] > 0 and r2["packs"]:
+            a2 = 2.0 * S * r2["packs"] / (r2["span_ms"] * 1e-3) / 1e9
+            steady = {"steps": steady_steps, "region_packs": r2["packs"],
+                      "device_us_per_launch": round(r2["span_ms"] * 1e3 / r2["packs"], 3),
+                      "achieved": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBPS, 4),
+                      "ms_per_step": round(dt_s / steady_steps * 1e3, 4)}
     late = min(4, steps)
     before = node.stats()
     node.sync()
@@ -531,6 +554,7 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24):
                      "region_kernels": {k: kern1[k] - kern0.get(k, 0) for k in kern1
                                         if kern1[k] - kern0.get(k, 0)},
                      "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"]},
+        "steady": steady,
         "parity": {"oracle_sample_bytes": golden["sample_bytes"], "oracle_csum64": want,
                    "reference_pack_matches_oracle": ref_csum == want and S == golden["sample_bytes"],
                    "late_verified_msgs": late},
