@@ -13,7 +13,8 @@
 // feeds a local input has a proxy node in the local region, served by a thread of the gateway:
 // it re-sends each remote message on the proxy's output (a device sample uploaded H2D for GPU
 // proxies, an inline sample for host-only ones), so local receivers see an ordinary input;
-// OutputsClosed closes the proxy's outputs and, once all are closed, finishes the proxy.
+// InputsClosed closes the proxy outputs feeding the named inputs and, once all are closed,
+// finishes the proxy.
 //
 // Wire: the reference's — one frame = u64 little-endian length + bincode of
 // Timestamped<InterDaemonEvent> (bincode.h); InputsClosed names the receivers' inputs on the

@@ -1,5 +1,5 @@
 """Dataflows spanning machines: one daemon per machine, InterDaemonEvent::Output /
-OutputsClosed over TCP (libraries/message/src/daemon_to_daemon.rs:9-21, the remote branch of
+InputsClosed over TCP (libraries/message/src/daemon_to_daemon.rs:9-21, the remote branch of
 send_out in binaries/daemon/src/lib.rs:955-1000), modelled on examples/multiple-daemons
 (a source on one machine, its receivers on another).  CPU only: host-only nodes, inline
 samples; the device-sample staging path is covered by tests/test_gpu_dataflow.py."""
@@ -142,7 +142,7 @@ def test_wrong_dataflow_id_is_ignored(tmp_path):
 
 
 def test_crashed_peer_daemon_closes_remote_inputs(tmp_path, monkeypatch):
-    """A remote daemon that dies without sending OutputsClosed (killed) must not strand the
+    """A remote daemon that dies without sending InputsClosed (killed) must not strand the
     local receivers: once every peer connection has been gone for the grace period
     (DORA_GPU_PEER_GRACE_MS) the proxy closes its outputs and the local dataflow finishes.
     The reference only ends the connection's read loop on EOF/reset
@@ -173,7 +173,7 @@ def test_crashed_peer_daemon_closes_remote_inputs(tmp_path, monkeypatch):
             assert ev is not None and ev["type"] == "INPUT", ev
             seqs.append(ev["metadata"]["seq"])
         assert seqs == list(range(5))
-        a.daemon.kill()  # no OutputsClosed ever leaves machine A
+        a.daemon.kill()  # no InputsClosed ever leaves machine A
         t0 = time.time()
         closed = set()
         while closed != {"data", "side"}:
