@@ -105,6 +105,8 @@ _SIGS = {
     "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
     "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
+    "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
+                                           POINTER(ctypes.c_double)]),
     "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
                                          c_void_p, c_size_t, c_uint64, c_uint64, c_void_p,
                                          c_void_p, c_size_t, c_int, c_void_p, c_size_t,

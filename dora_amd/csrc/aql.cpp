@@ -898,6 +898,138 @@ uint64_t aql_dispatched(int device, size_t k) {
   return a->dispatched[k];
 }
 
+// Test hook (microbenchmark, dora_gpu_test_aql_pipeline): `n` single-segment packs of `bytes`
+// from rotating HBM sources over `nq` of the queues, at most `depth` packets outstanding per
+// queue, completion seen by the host.  mode 0: the product's in-kernel fill signal (flag in
+// pinned host memory, polled); 1: no in-kernel signal, the packet's completion signal (the
+// command processor's, after the kernel ends), release fence none; 2: as 1, release fence agent.
+int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
+                       double* us_per_msg) {
+  AqlQueue* a = aql_queue(device);
+  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
+  if (!a->hring) return fail(DORA_ERR_UNSUPPORTED, "no host argument ring");
+  if (bytes == 0 || n <= 0 || mode < 0 || mode > 2 || nq < 1 || nq > a->nq || depth < 1 ||
+      depth > 8)
+    return fail(DORA_ERR_INVALID, "bad pipeline bench parameters");
+  const size_t stride = (bytes + 4095) & ~size_t(4095);
+  const size_t nbuf = std::max<size_t>(2, std::min<size_t>(256, (size_t(640) << 20) / stride));
+  uint8_t *src = nullptr, *dst = nullptr;
+  uint32_t* done = nullptr;
+  uint64_t* flags = nullptr;
+  const int slots = nq * depth + 1;
+  if (hipMalloc(&src, nbuf * stride) != hipSuccess || hipMalloc(&dst, nbuf * stride) != hipSuccess ||
+      hipMalloc(&done, size_t(slots) * kMaxSignalWgs * 4) != hipSuccess ||
+      hipHostMalloc(&flags, size_t(slots) * 64, hipHostMallocCoherent) != hipSuccess) {
+    if (src) (void)hipFree(src);
+    if (dst) (void)hipFree(dst);
+    if (done) (void)hipFree(done);
+    return fail(DORA_ERR_HIP, "pipeline bench: allocation");
+  }
+  (void)hipMemset(src, 0x5a, nbuf * stride);
+  (void)hipMemset(done, 0, size_t(slots) * kMaxSignalWgs * 4);
+  std::memset(flags, 0, size_t(slots) * 64);
+  (void)hipDeviceSynchronize();
+  std::vector<hsa_signal_t> sigs(static_cast<size_t>(slots));
+  for (auto& sg : sigs) (void)hsa_signal_create(1, 0, nullptr, &sg);
+  struct Out {
+    int slot;
+    uint64_t epoch;
+  };
+  std::vector<std::deque<Out>> outq(static_cast<size_t>(nq));
+  std::vector<int> free_slots;
+  for (int k = slots - 1; k >= 0; --k) free_slots.push_back(k);
+  uint64_t epoch = 0;
+  int rc = DORA_OK;
+  auto complete = [&](const Out& o) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const bool ok = mode == 0 ? __atomic_load_n(flags + 8 * o.slot, __ATOMIC_ACQUIRE) >= o.epoch
+                                : hsa_signal_load_scacquire(sigs[size_t(o.slot)]) == 0;
+      if (ok) return true;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
+    }
+  };
+  auto run = [&](int count) -> int {
+    std::lock_guard<std::mutex> g(a->mu);
+    for (int i = 0; i < count; ++i) {
+      const int qi = i % nq;
+      auto& oq = outq[size_t(qi)];
+      if (int(oq.size()) >= depth) {
+        if (!complete(oq.front())) return fail(DORA_ERR_TIMEOUT, "pipeline bench: pack lost");
+        free_slots.push_back(oq.front().slot);
+        oq.pop_front();
+      }
+      const int sl = free_slots.back();
+      free_slots.pop_back();
+      ++epoch;
+      const size_t b = size_t(epoch) % nbuf;
+      Segment sg{src + b * stride, 0, bytes};
+      FillSignal fs{mode == 0 ? flags + 8 * sl : nullptr, epoch,
+                    mode == 0 ? done + size_t(sl) * kMaxSignalWgs : nullptr};
+      uint8_t args[kArgs1Bytes];
+      uint32_t grid = 0;
+      int unroll = 4;
+      if (build_aql_args1(sg, dst + b * stride, fs, args, &grid, &unroll) != DORA_OK)
+        return DORA_ERR_INVALID;
+      const uint64_t r = a->next++ % kRingSlots;
+      uint8_t* slot = a->hring + r * kHostSlotBytes;
+      std::memcpy(slot, args, kArgs1Bytes);
+      if (mode != 0) hsa_signal_store_relaxed(sigs[size_t(sl)], 1);
+      hsa_queue_t* const q = a->qs[qi];
+      const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+      while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) __builtin_ia32_pause();
+      hsa_queue_store_write_index_relaxed(q, idx + 1);
+      auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
+      const int k = 2;  // dora_aql_pack1_u4
+      p->workgroup_size_x = 256;
+      p->workgroup_size_y = 1;
+      p->workgroup_size_z = 1;
+      p->reserved0 = 0;
+      p->grid_size_x = grid * 256u;
+      p->grid_size_y = 1;
+      p->grid_size_z = 1;
+      p->private_segment_size = a->priv[k];
+      p->group_segment_size = a->group[k];
+      p->kernel_object = a->kobj[k];
+      p->kernarg_address = slot;
+      p->reserved2 = 0;
+      p->completion_signal = mode == 0 ? hsa_signal_t{0} : sigs[size_t(sl)];
+      const uint32_t rel = mode == 2 ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE;
+      const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                              (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                              (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+      const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+      __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
+                       __ATOMIC_RELEASE);
+      hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+      oq.push_back({sl, epoch});
+    }
+    for (auto& oq : outq) {
+      while (!oq.empty()) {
+        if (!complete(oq.front())) return fail(DORA_ERR_TIMEOUT, "pipeline bench: pack lost");
+        free_slots.push_back(oq.front().slot);
+        oq.pop_front();
+      }
+    }
+    return DORA_OK;
+  };
+  rc = run(std::min(n, 64));  // warm
+  if (rc == DORA_OK) {
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = run(n);
+    const auto t1 = std::chrono::steady_clock::now();
+    *us_per_msg = std::chrono::duration<double, std::micro>(t1 - t0).count() / n;
+  }
+  for (auto& sg : sigs) (void)hsa_signal_destroy(sg);
+  if (rc == DORA_OK) {
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(done);
+    (void)hipHostFree(flags);
+  }  // else: a pack may still run, leak its buffers rather than free them under it
+  return rc;
+}
+
 int aql_profile_enable(AqlQueue* a, bool on) {
   if (!a) return DORA_OK;
   std::lock_guard<std::mutex> g(a->mu);

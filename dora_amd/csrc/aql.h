@@ -50,6 +50,10 @@ uint64_t aql_dispatched(int device, size_t k);
 // Test tool: while held, every batchable send of this process on `device` waits in the
 // backlog; releasing dispatches the backlog as batch packs (tests/test_gpu_dataflow.py).
 int aql_hold(int device, bool hold);
+// Test hook: packs pipelined over the queues with in-kernel or command-processor completion
+// signals (dora_gpu_test_aql_pipeline).
+int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
+                       double* us_per_msg);
 // Batch packs dispatched, the sends they carried, and sends that waited in the backlog.
 int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint64_t* backlogged);
 

@@ -335,6 +335,12 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, 1> : pack_kernel<2, 0>;
     else if (var.wt) kern = pack_kernel<4, 2>;
     else if (var.nt) kern = pack_kernel<4, 1>;
+    // microbenchmark: the write-through launch that signals nothing, with the signalling grid
+    // (dora_gpu_pack_signal_tune) — the grid's cost apart from the signal's
+    if (var.wt && !signal) {
+      const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+      if (g && grid > g) grid = g;
+    }
     if (last && signal) {
       // signalling launch: write-through stores, at most kMaxSignalWgs workgroups
       a.flag = signal->flag;

@@ -104,6 +104,12 @@ int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_ms
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
+int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
+                               double* us_per_msg) {
+  if (!us_per_msg) return dora::fail(DORA_ERR_INVALID, "us_per_msg is NULL");
+  return dora::aql_pipeline_bench(device, bytes, n, mode, queues, depth, us_per_msg);
+}
+
 int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out) {
   if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
   return dora::bar_alloc(device, bytes, out);

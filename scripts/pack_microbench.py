@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="sweep unroll x nt x chunk")
     ap.add_argument("--signal-sweep", action="store_true",
                     help="packs that signal their fill from the kernel, by workgroups per XCD")
+    ap.add_argument("--grids", default="512,1024", help="signal sweep: signalling grids")
+    ap.add_argument("--units", default="0,4,8", help="signal sweep: loads in flight per lane")
+    ap.add_argument("--chunks", default="0,8192,16384,32768", help="signal sweep: chunk bytes")
     ap.add_argument("--c3", action="store_true",
                     help="C3 shape: 1M-point List<Struct<x,y,z,intensity>> clouds (f32 buffers "
                          "at 4 mod 16) instead of byte buffers; memcpy = one D2D of the sample")
@@ -45,8 +48,10 @@ def main():
         # (kind, signalling grid): the pack signals a scratch flag from its workgroup 0;
         # ("pack", 0, 2, 0): the same write-through stores without the signal
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0), ("pack", 0, 2, 0)] + [
-            ("sig", w, u, ch) for w in [512, 1024] for u in [0, 4, 8]
-            for ch in [0, 8192, 16384, 32768]]
+            ("wtgrid", w, 2, 0) for w in [int(x) for x in args.grids.split(",")]] + [
+            ("sig", w, u, ch) for w in [int(x) for x in args.grids.split(",")]
+            for u in [int(x) for x in args.units.split(",")]
+            for ch in [int(x) for x in args.chunks.split(",")]]
     else:
         variants = [("memcpy", 0, 0, 0), ("pack", 0, -1, 0)]
     sizes = [int(x) for x in args.sizes.split(",")]
@@ -73,12 +78,15 @@ def main():
                 kind, u, nt, ch = v
                 if kind == "pack":
                     call("dora_gpu_pack_tune", u, nt, ch)
+                elif kind == "wtgrid":  # write-through stores, no signal, grid capped at u
+                    call("dora_gpu_pack_tune", 0, 2, ch)
                 elif kind == "sig":  # (grid, unroll, chunk)
                     call("dora_gpu_pack_tune", nt, -1, ch)
-                call("dora_gpu_pack_signal_tune", u if kind == "sig" else 0, int(kind == "sig"))
+                call("dora_gpu_pack_signal_tune", u if kind in ("sig", "wtgrid") else 0,
+                     int(kind == "sig"))
 
                 def launch(k):
-                    if kind in ("pack", "sig"):
+                    if kind in ("pack", "sig", "wtgrid"):
                         plans[k].pack(dsts[k].ptr, size, s)
                     else:
                         call("dora_gpu_memcpy_async", dsts[k].ptr, srcs[k].ptr + args.misalign,
