@@ -902,13 +902,17 @@ uint64_t aql_dispatched(int device, size_t k) {
 // from rotating HBM sources over `nq` of the queues, at most `depth` packets outstanding per
 // queue, completion seen by the host.  mode 0: the product's in-kernel fill signal (flag in
 // pinned host memory, polled); 1: no in-kernel signal, the packet's completion signal (the
-// command processor's, after the kernel ends), release fence none; 2: as 1, release fence agent.
+// command processor's, after the kernel ends), release fence none; 2: as 1, release fence agent;
+// 3: as 0 without the acquire fence; 4: as 1 without the acquire fence.
 int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
                        double* us_per_msg) {
+  const bool no_acquire = mode >= 3;
+  if (mode == 3) mode = 0;
+  if (mode == 4) mode = 1;
   AqlQueue* a = aql_queue(device);
   if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
   if (!a->hring) return fail(DORA_ERR_UNSUPPORTED, "no host argument ring");
-  if (bytes == 0 || n <= 0 || mode < 0 || mode > 2 || nq < 1 || nq > a->nq || depth < 1 ||
+  if (bytes == 0 || n <= 0 || mode < 0 || mode > 4 || nq < 1 || nq > a->nq || depth < 1 ||
       depth > 8)
     return fail(DORA_ERR_INVALID, "bad pipeline bench parameters");
   const size_t stride = (bytes + 4095) & ~size_t(4095);
@@ -996,7 +1000,8 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
       p->completion_signal = mode == 0 ? hsa_signal_t{0} : sigs[size_t(sl)];
       const uint32_t rel = mode == 2 ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE;
       const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                              (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                              ((no_acquire ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT)
+                               << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                               (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
       const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
       __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
