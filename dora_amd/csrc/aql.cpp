@@ -903,12 +903,15 @@ uint64_t aql_dispatched(int device, size_t k) {
 // queue, completion seen by the host.  mode 0: the product's in-kernel fill signal (flag in
 // pinned host memory, polled); 1: no in-kernel signal, the packet's completion signal (the
 // command processor's, after the kernel ends), release fence none; 2: as 1, release fence agent;
-// 3: as 0 without the acquire fence; 4: as 1 without the acquire fence.
+// 3: as 0 without the acquire fence; 4: as 1 without the acquire fence; 5: as 1, every wave
+// waiting for its stores to complete before it ends (so the completion signal, written after
+// the last wave ended, follows every store of the pack without relying on a release fence).
 int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
                        double* us_per_msg) {
-  const bool no_acquire = mode >= 3;
+  const bool no_acquire = mode == 3 || mode == 4;
+  const bool wave_wait = mode == 5;
   if (mode == 3) mode = 0;
-  if (mode == 4) mode = 1;
+  if (mode == 4 || mode == 5) mode = 1;
   AqlQueue* a = aql_queue(device);
   if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
   if (!a->hring) return fail(DORA_ERR_UNSUPPORTED, "no host argument ring");
@@ -969,7 +972,7 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
       const size_t b = size_t(epoch) % nbuf;
       Segment sg{src + b * stride, 0, bytes};
       FillSignal fs{mode == 0 ? flags + 8 * sl : nullptr, epoch,
-                    mode == 0 ? done + size_t(sl) * kMaxSignalWgs : nullptr};
+                    mode == 0 || wave_wait ? done + size_t(sl) * kMaxSignalWgs : nullptr};
       uint8_t args[kArgs1Bytes];
       uint32_t grid = 0;
       int unroll = 4;

@@ -470,6 +470,10 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
     if (args.flag) {  // all-zero arguments are a no-op
       if constexpr (__is_same(A, AqlBatchArgs)) signal_batch(args, blk, nblk, t_start);
       else signal_fill(args, blk, nblk, t_start);
+    } else if (args.done) {
+      // done words but no flag: the dispatch's completion signal reports the fill (aql.cpp
+      // pipeline probe); every wave's stores are complete before it ends
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 }

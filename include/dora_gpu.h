@@ -247,7 +247,8 @@ int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes
  * round robin over `queues` of the device's AQL queues with at most `depth` outstanding per
  * queue; mode 0 completes them with the in-kernel fill signal, 1 with the packet's completion
  * signal (release fence none), 2 the same with an agent release fence, 3 and 4 as 0 and 1 without
- * the acquire fence.  *us_per_msg = host time per pack. */
+ * the acquire fence, 5 as 1 with every wave waiting for its stores.  *us_per_msg = host time
+ * per pack. */
 int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
                                double* us_per_msg);
 void dora_gpu_test_bar_free(void* ptr);
