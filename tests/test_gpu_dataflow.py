@@ -74,6 +74,53 @@ def test_bench_sink_bit_exact_c2(launcher, tmp_path):
         assert paths == {"aql": 0, "hip": 30}, paths
 
 
+def test_payload_beyond_4_gib_bit_exact(launcher, tmp_path):
+    """A maximum-size case: one UInt8 payload of 4.5 GiB + 13 bytes (offsets, lengths and chunk
+    counts past 32 bits; a ragged tail) from a source 3 bytes past alignment, sent twice through
+    the AQL path (the barrier policy of >= 32 MiB packs) to the sink, which checksums each
+    delivered sample.  The source's bytes are the oracle generator's at three windows; the
+    checksum of checksums holds for the whole payload (size-independent property)."""
+    import numpy as np
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    from oracle.checksum_ref import GOLDEN, MASK, fmix64_np
+    res = str(tmp_path / "sink.json")
+    size, mis, seed = (4 << 30) + (1 << 29) + 13, 3, 0xB16
+    s = device.Stream()
+    buf = device.DeviceBuffer(size + mis)
+    try:
+        device.fill_splitmix(buf.ptr + mis, size, seed, s)
+        s.sync()
+        csum = device.csum64(buf.ptr + mis, size, s)
+        for w0 in (0, (size // 2) & ~7, (size - (1 << 20)) & ~7):   # word-aligned windows
+            n = min(1 << 20, size - w0)
+            got = buf.to_bytes(n, offset=mis + w0)
+            k = np.arange(w0 // 8 + 1, w0 // 8 + 1 + (n + 7) // 8, dtype=np.uint64)
+            with np.errstate(over="ignore"):
+                want = fmix64_np(np.uint64(seed & MASK) + k * GOLDEN).astype("<u8").tobytes()[:n]
+            assert got == want, w0
+        with Dataflow(_bench_desc(res), launcher=launcher) as df:
+            node = Node("node", dataflow=df.shm, device=0)
+            for k in range(2):
+                node.send_output_device_bytes("data", buf.ptr + mis, size,
+                                              {"csum": to_i64(csum), "verify": True, "seq": k})
+            paths = node.fill_paths()
+            node.close()
+            codes = df.wait(120)
+            log = df.log("sink")
+    finally:
+        buf.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    got = {x["size"]: x for x in out["series"]}
+    assert got[size]["verified"] == 2 and got[size]["mismatches"] == 0, got
+    if os.environ.get("DORA_GPU_AQL", "1") != "0":
+        assert paths["aql"] == 2, paths
+
+
 def test_slots_recycle_through_drop_tokens(launcher, tmp_path):
     """The 20-entry slot cache (node/mod.rs:321-371) serves repeated sends once tokens return."""
     from dora_amd import device
