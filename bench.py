@@ -519,19 +519,24 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24, steady_steps=20
     kern0, bs0 = device.aql_dispatch_counts(node.device), device.aql_batch_stats(node.device)
     node.region_begin()
     t0 = time.perf_counter()
+    t_send = []
     for k in range(steps):
         meta = {"seq": seq}
         if k >= steps - late:
             meta.update({"csum": to_i64(want), "verify_late": True})
         if k == steps - 1:
             meta["ack"] = True
+        t_send.append(time.perf_counter())
         node.send_output("throughput", srcs[k % nsrc], meta)
         seq += 1
+    t_send.append(time.perf_counter())
     node.region_mark()
     wait_ack(seq - 1)
     node.sync()
     elapsed = time.perf_counter() - t0
     region = node.region_end()
+    # each timed pack's own (start, end) stamps, us after the region's first start (sorted)
+    intervals = sorted((round(a * 1e3, 2), round(b * 1e3, 2)) for a, b in node.pack_intervals(64))
     after = node.stats()
     kern1, bs1 = device.aql_dispatch_counts(node.device), device.aql_batch_stats(node.device)
     for a in srcs:
@@ -555,6 +560,8 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24, steady_steps=20
                                         if kern1[k] - kern0.get(k, 0)},
                      "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"]},
         "steady": steady,
+        "pack_intervals_us": intervals,
+        "send_calls_us": [round((t - t_send[0]) * 1e6, 1) for t in t_send],
         "parity": {"oracle_sample_bytes": golden["sample_bytes"], "oracle_csum64": want,
                    "reference_pack_matches_oracle": ref_csum == want and S == golden["sample_bytes"],
                    "late_verified_msgs": late},

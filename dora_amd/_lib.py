@@ -55,6 +55,9 @@ _SIGS = {
     "dora_gpu_aql_kernel_name": (c_char_p, [c_size_t]),
     "dora_gpu_aql_batch_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_uint64),
                                          POINTER(c_uint64)]),
+    "dora_gpu_aql_cp_signalled": (c_int, [c_int, POINTER(c_uint64)]),
+    "dora_gpu_test_fill_reached": (c_int, [c_void_p, c_uint64]),
+    "dora_gpu_test_cp_arm": (c_int, [c_void_p, c_uint64]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),

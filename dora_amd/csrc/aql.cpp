@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <hsa/hsa.h>
+#include <hsa/amd_hsa_signal.h>
 #include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
@@ -23,6 +24,14 @@
 #include <vector>
 
 #include "common.h"
+#include "shm.h"
+
+static_assert(offsetof(amd_signal_t, value) == offsetof(dora::CpSignal, value) &&
+                  offsetof(amd_signal_t, event_mailbox_ptr) ==
+                      offsetof(dora::CpSignal, event_mailbox_ptr) &&
+                  offsetof(amd_signal_t, start_ts) == offsetof(dora::CpSignal, start_ts) &&
+                  sizeof(amd_signal_t) == sizeof(dora::CpSignal),
+              "CpSignal must be laid out as amd_signal_t");
 #include "subprof.h"
 
 extern "C" const char dora_aql_code_object[];
@@ -70,6 +79,8 @@ struct Pending {
   uint64_t dst_cap = 0, bytes = 0;
   uint32_t chunk = 0;
   bool profile = false;
+  bool cp = false;  // may be signalled by the command processor (cp_signal_window) when alone
+  uint64_t* cp_stamps = nullptr;  // CP-signalled: the timed region's stamp area (device), or none
 };
 
 }  // namespace
@@ -117,7 +128,7 @@ struct AqlQueue {
   std::condition_variable cv;  // backlog non-empty (the dispatcher thread waits on it)
   bool dispatcher = false;
   bool hold = false;  // test tool (aql_hold): every batchable send waits in the backlog
-  uint64_t batches = 0, batched_msgs = 0, backlogged = 0;
+  uint64_t batches = 0, batched_msgs = 0, backlogged = 0, cp_signalled = 0;
   // test tool (bar_alloc): the GPU's coarse-grained pool, host-accessible through the BAR
   hsa_agent_t cpu{};
   hsa_amd_memory_pool_t coarse{};
@@ -435,7 +446,7 @@ void aql_fence_all() {
     drain_backlog(a, t0, std::chrono::seconds(5));
     std::lock_guard<std::mutex> g(a->mu);
     for (Use& u : a->uses)
-      while (u.flag && u.flag->load(std::memory_order_acquire) < u.epoch &&
+      while (u.flag && !fill_reached(u.flag, u.epoch) &&
              std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
         __builtin_ia32_pause();
   }
@@ -459,7 +470,7 @@ void aql_forget_flags(int device, const void* base, size_t size) {
   for (Use& u : a->uses) {
     const auto* f = reinterpret_cast<const uint8_t*>(u.flag);
     if (!u.flag || f < lo || f >= lo + size) continue;
-    while (u.flag->load(std::memory_order_acquire) < u.epoch &&
+    while (!fill_reached(u.flag, u.epoch) &&
            std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
       __builtin_ia32_pause();
     u.flag = nullptr;  // the slot is free; the flag's region goes away
@@ -467,6 +478,40 @@ void aql_forget_flags(int device, const void* base, size_t size) {
 }
 
 namespace {
+
+// Single-segment packs of [min, max) bytes are signalled by the command processor when they go out
+// alone (DORA_GPU_AQL_CP_SIGNAL=min:max in bytes, "0": never).  The in-kernel signal's tail —
+// every workgroup waiting for its stores' acknowledgement, workgroup 0's last poll of the done
+// words — keeps a queue from starting its next packet, so a queue runs one pack at a time; with
+// the CP's completion signal instead, consecutive packets of a queue overlap.
+// DESIGN §9 (profiles/r03_aql_pipeline_probe.jsonl, mode 5): 4 MB packs over 4 queues
+// 1.95 -> 1.59-1.64 us each, 1 MB 1.38-1.42 -> 1.51 (so not below 2 MiB), 16 / 40.96 MB flat.
+// DORA_GPU_AQL_CP_MULTI=1: multi-segment packs (C3's point clouds) in the window too.  Opt-in:
+// C3's 200-send steady state gains (0.71-0.73 -> 0.75-0.78 of HBM), but its 20-send burst lost
+// (0.68-0.70 -> 0.35-0.63): the burst's first sends stall on the host (the first send call
+// 34-43 us instead of 4, then ~5 us per call instead of 2), which is not explained yet
+// (profiles/r03_cp_signal_ab.jsonl).
+bool cp_multi() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_CP_MULTI");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
+std::pair<uint64_t, uint64_t> cp_signal_window() {
+  static const std::pair<uint64_t, uint64_t> v = [] {
+    std::pair<uint64_t, uint64_t> w{uint64_t(1) << 20, uint64_t(32) << 20};
+    if (const char* e = std::getenv("DORA_GPU_AQL_CP_SIGNAL")) {
+      if (*e == '0' && e[1] == 0) return std::pair<uint64_t, uint64_t>{0, 0};
+      char* end = nullptr;
+      const uint64_t lo = std::strtoull(e, &end, 10);
+      if (end && *end == ':') w = {lo, std::strtoull(end + 1, nullptr, 10)};
+    }
+    return w;
+  }();
+  return v;
+}
 
 uint64_t barrier_bytes() {
   static const uint64_t v = [] {
@@ -487,9 +532,9 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // the argument slot of the dispatch kRingSlots back must have completed
   const uint64_t r = a->next % kRingSlots;
   Use& u = a->uses[r];
-  if (u.flag && u.flag->load(std::memory_order_acquire) < u.epoch) {
+  if (u.flag && !fill_reached(u.flag, u.epoch)) {
     const auto t0 = std::chrono::steady_clock::now();
-    while (u.flag->load(std::memory_order_acquire) < u.epoch) {
+    while (!fill_reached(u.flag, u.epoch)) {
       __builtin_ia32_pause();
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
         a->failed.store(true);  // a pack that never completes: stop dispatching here
@@ -504,12 +549,22 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // one segment at sample offset 0: the preloaded kernels, arguments from host memory
   const bool batch = n > 1;
   const bool one = !batch && a->hring && it0.n == 1 && segs[0].dst_off == 0;
+  // A lone mid-size single-segment pack signalled by the command processor (cp_signal_window):
+  // no in-kernel flag, every wave waits for its own stores, the packet's completion signal is
+  // the flag's CpSignal line (shm.h FillFlag)
+  const bool cp = !batch && it0.cp && it0.flag_host && (one || cp_multi());
   int rc;
   if (batch) {
     BatchItem bi[kBatchMsgs];
     for (size_t m = 0; m < n; ++m)
       bi[m] = {items[m].segs, items[m].n, items[m].dst, items[m].sig, items[m].dst_cap};
     rc = build_aql_batch_args(bi, n, args, sizeof(args), &grid);
+  } else if (cp) {
+    // no flag, done words non-null: per-wave store waits; `epoch` carries the stamp area
+    const FillSignal per_wave{nullptr, reinterpret_cast<uintptr_t>(it0.cp_stamps), sig.done};
+    rc = one ? build_aql_args1(segs[0], dst, per_wave, args, &grid, &unroll)
+             : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, &unroll,
+                              it0.dst_cap);
   } else if (one) {
     rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll);
   } else {
@@ -521,7 +576,15 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     const char* e = std::getenv("DORA_GPU_AQL_PROFILE");
     return e && *e == '0';
   }();
-  if (profile && a->profiling && !no_prof) {
+  if (cp) {
+    // set the flag up for this fill (its previous fill has completed: the slot was reused), then
+    // name the epoch; the command processor's decrement completes it (fill_reached)
+    static_assert(AMD_SIGNAL_KIND_USER == 1, "cp_arm's signal kind");
+    cp_arm(reinterpret_cast<FillFlag*>(const_cast<std::atomic<uint64_t>*>(it0.flag_host)),
+           sig.epoch);
+    // the device address of the CpSignal line: the flag's device address + its offset
+    done.handle = reinterpret_cast<uint64_t>(sig.flag) + offsetof(FillFlag, cp);
+  } else if (profile && a->profiling && !no_prof) {
     if (a->free_sigs.empty() && a->used_sigs.size() < kProfileSignals) {
       hsa_signal_t s;
       if (hsa_signal_create(1, 0, nullptr, &s) == HSA_STATUS_SUCCESS) a->free_sigs.push_back(s);
@@ -639,6 +702,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   a->outq[qi].push_back(u);
   ++a->next;
   ++a->dispatched[k];
+  if (cp) ++a->cp_signalled;
   if (batch) {
     ++a->batches;
     a->batched_msgs += n;
@@ -665,20 +729,33 @@ size_t queue_depth() {
   return v;
 }
 
+// Packets a queue may hold when the send would be signalled by the command processor
+// (DORA_GPU_AQL_CP_DEPTH, default 3): such packets of one queue overlap, so a third one keeps
+// the queue busy (native ladder, profiles/r03_cp_signal_ab.jsonl: 4 MB 1.88 -> 1.66 us per
+// message at depth 3, 8 MB 2.74 -> 2.70-2.77, 16 MB 5.30 -> 5.39-5.48).
+size_t cp_queue_depth() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_CP_DEPTH");
+    const long d = e ? std::atol(e) : 3;
+    return size_t(std::max(1L, std::min(64L, d)));
+  }();
+  return v;
+}
+
 // Drop the completed packets at the front of queue `i`'s outstanding list.
 void prune(AqlQueue* a, int i) {
   auto& o = a->outq[i];
-  while (!o.empty() && o.front().flag->load(std::memory_order_acquire) >= o.front().epoch)
+  while (!o.empty() && fill_reached(o.front().flag, o.front().epoch))
     o.pop_front();
 }
 
 // The queue with the fewest outstanding packets below the depth (ties: round robin) among the
 // first `nq` (0: all), or -1.
-int pick_queue(AqlQueue* a, int nq = 0) {
+int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
   if (a->hold) return -1;
   if (nq <= 0 || nq > a->nq) nq = a->nq;
   int best = -1;
-  size_t best_n = queue_depth();
+  size_t best_n = depth ? depth : queue_depth();
   for (int j = 0; j < nq; ++j) {
     const int i = int((a->next + uint64_t(j)) % uint64_t(nq));
     prune(a, i);
@@ -727,7 +804,8 @@ void pump_locked(AqlQueue* a) {
       ++n;
     }
     const bool big = n > 1 && bytes >= batch_big_bytes();
-    const int qi = pick_queue(a, big ? 3 : 0);
+    const int qi = pick_queue(a, big ? 3 : 0,
+                              n == 1 && a->backlog.front().cp ? cp_queue_depth() : 0);
     if (qi < 0) return;
     Pending batch[kBatchMsgs];
     for (size_t k = 0; k < n; ++k) {
@@ -760,7 +838,7 @@ void dispatcher_main(AqlQueue* a) {
     for (uint32_t spin = 0;; ++spin) {
       bool any = false;
       for (int i = 0; i < a->nq && !any; ++i)
-        any = !front[i].flag || front[i].flag->load(std::memory_order_acquire) >= front[i].epoch;
+        any = !front[i].flag || fill_reached(front[i].flag, front[i].epoch);
       if (any) break;
       if ((spin & 1023) == 1023) {
         const auto dt = std::chrono::steady_clock::now() - t0;
@@ -776,7 +854,8 @@ void dispatcher_main(AqlQueue* a) {
 }  // namespace
 
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap) {
+             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
+             uint64_t* cp_stamps) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -788,7 +867,13 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.flag_host = flag_host;
   p.dst_cap = dst_cap;
   p.profile = profile;
+  p.cp_stamps = cp_stamps;
   for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
+  // inside a timed region only with a stamp area for the pack's own stamps
+  const auto cw = cp_signal_window();
+  p.cp = (!profile || cp_stamps) && flag_host &&
+         ((n == 1 && segs[0].dst_off == 0) || cp_multi()) && p.bytes >= cw.first &&
+         p.bytes < cw.second;
   std::lock_guard<std::mutex> g(a->mu);
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
@@ -809,7 +894,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // larger dispatches instead of more queues.
   p.chunk = aql_chunk_bytes(segs, n);
   if (a->backlog.empty()) {
-    const int qi = pick_queue(a);
+    const int qi = pick_queue(a, 0, p.cp ? cp_queue_depth() : 0);
     if (qi >= 0) return dispatch_locked(a, size_t(qi), &p, 1, false);
   }
   a->backlog.push_back(p);
@@ -884,6 +969,18 @@ int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint6
   *batched_msgs = a->batched_msgs;
   *backlogged = a->backlogged;
   return DORA_OK;
+}
+
+uint64_t aql_cp_signalled(int device) {
+  if (device < 0 || device >= 64) return 0;
+  AqlQueue* a;
+  {
+    std::lock_guard<std::mutex> g(g_queues_mu);
+    a = g_queues[device];
+  }
+  if (!a) return 0;
+  std::lock_guard<std::mutex> g(a->mu);
+  return a->cp_signalled;
 }
 
 uint64_t aql_dispatched(int device, size_t k) {
@@ -971,7 +1068,8 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
       ++epoch;
       const size_t b = size_t(epoch) % nbuf;
       Segment sg{src + b * stride, 0, bytes};
-      FillSignal fs{mode == 0 ? flags + 8 * sl : nullptr, epoch,
+      // (a CP-signalled pack's `epoch` is its stamp area: none here)
+      FillSignal fs{mode == 0 ? flags + 8 * sl : nullptr, mode == 0 ? epoch : 0,
                     mode == 0 || wave_wait ? done + size_t(sl) * kMaxSignalWgs : nullptr};
       uint8_t args[kArgs1Bytes];
       uint32_t grid = 0;

@@ -29,9 +29,12 @@ AqlQueue* aql_queue(int device);
 // of that flag (kernarg slots are recycled once the launch that used them has signalled).
 // `dst_cap`: bytes writable from `dst` (0: unknown; see launch_pack).
 // With `profile`, the packet carries a completion signal whose dispatch times
-// aql_profile_take() reports.
+// aql_profile_take() reports.  `profile` packs (a timed region's) are signalled by the command
+// processor only when `cp_stamps` (device memory, (1 + kMaxSignalWgs) zeroed words) takes their
+// stamps: [0] the first workgroup's start, [1 + k] workgroup k's completion (s_memrealtime).
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0);
+             const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
+             uint64_t* cp_stamps = nullptr);
 
 // Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
 // region about to be unmapped), after waiting (bounded) for those fills to signal.
@@ -54,6 +57,8 @@ int aql_hold(int device, bool hold);
 // signals (dora_gpu_test_aql_pipeline).
 int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
                        double* us_per_msg);
+// Packs signalled by the command processor (cp_signal_window, aql.cpp).
+uint64_t aql_cp_signalled(int device);
 // Batch packs dispatched, the sends they carried, and sends that waited in the backlog.
 int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint64_t* backlogged);
 

@@ -164,7 +164,7 @@ bool Forwarder::stage(const ForwardJob& job, std::vector<uint8_t>* bytes,
     if (d.flag_node >= h->n_nodes || d.flag_index >= kFillFlags) return false;
     const std::atomic<uint64_t>& f = h->nodes[d.flag_node].fill[d.flag_index].epoch;
     const auto t0 = std::chrono::steady_clock::now();
-    while (f.load(std::memory_order_acquire) < d.epoch) {
+    while (!fill_reached(&f, d.epoch)) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return false;
       std::this_thread::sleep_for(std::chrono::microseconds(5));
     }

@@ -105,6 +105,7 @@ struct Slot {
   int flag = -1;              // FillFlag index in the node's region entry (async sends)
   uint64_t fill_epoch = 0;    // epoch the last fill into this slot stores into `flag`
   uint64_t region_epoch = 0;  // that fill belongs to a timed region: harvest its stamps
+  int region_cp_area = -1;    // ... its stamp area, if the command processor signalled it
   hipEvent_t done = nullptr;  // fallback: interprocess completion event of the last fill
   hipIpcEventHandle_t done_handle;
   // node-stream work on the slot with no fill flag (a broadcast group's pack + broadcast):
@@ -362,7 +363,7 @@ struct NodeCore {
     if (v.size() >= 256) {
       size_t k = 0;
       for (auto& x : v)
-        if (x.first->load(std::memory_order_acquire) < x.second) v[k++] = x;
+        if (!fill_reached(x.first, x.second)) v[k++] = x;
       v.resize(k);
     }
     v.push_back({f, epoch});
@@ -531,7 +532,7 @@ struct NodeCore {
     // AQL fills are on no HIP stream: wait for their flags on the host
     const uint64_t t0 = mono_ns();
     for (auto& x : aql_pending)
-      while (x.first->load(std::memory_order_acquire) < x.second && mono_ns() - t0 < 10000000000ull)
+      while (!fill_reached(x.first, x.second) && mono_ns() - t0 < 10000000000ull)
         __builtin_ia32_pause();
     aql_pending.clear();
     for (size_t i = 0; i < fill_streams.size(); ++i) {
@@ -672,6 +673,11 @@ struct dora_node {
   // kernel stamps (s_memrealtime ticks) of the region's packs, harvested from their flag lines
   uint64_t region_stamped = 0, region_unstamped = 0, region_tmin = 0, region_tmax = 0;
   std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
+  // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory,
+  // zeroed at region_begin, read back once at region_end
+  uint64_t* region_cp_stamps = nullptr;
+  uint32_t region_cp_next = 0;
+  std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
   bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
@@ -726,7 +732,10 @@ namespace {
 void harvest_region_stamp(dora_node* n, Slot* s) {
   if (!s->region_epoch || s->flag < 0) return;
   const FillFlag& ff = n->core->region->hdr()->nodes[n->core->idx].fill[s->flag];
-  if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch) {
+  if (s->region_cp_area >= 0 && ff.epoch.load(std::memory_order_acquire) != s->region_epoch &&
+      ff.cp_epoch.load(std::memory_order_acquire) == s->region_epoch) {
+    n->region_cp_used.push_back(uint32_t(s->region_cp_area));  // resolved at region_end
+  } else if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch) {
     const uint64_t a = ff.t_start, b = ff.t_end;
     if (b >= a && a) {
       if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
@@ -739,13 +748,14 @@ void harvest_region_stamp(dora_node* n, Slot* s) {
     }
   }
   s->region_epoch = 0;
+  s->region_cp_area = -1;
 }
 
 bool wait_slot_idle(dora_node* n, Slot* s, uint64_t timeout_ns = 10000000000ull) {
   const uint64_t t0 = mono_ns();
   if (s->flag >= 0 && s->fill_epoch) {
     const std::atomic<uint64_t>* f = n->core->flag_host(s->flag);
-    while (f->load(std::memory_order_acquire) < s->fill_epoch) {
+    while (!fill_reached(f, s->fill_epoch)) {
       if (mono_ns() - t0 > timeout_ns) return false;
       __builtin_ia32_pause();
     }
@@ -1104,7 +1114,7 @@ void finish_input(dora_node* n, dora_event* ev) {
     const std::atomic<uint64_t>& f = h->nodes[d.flag_node].fill[d.flag_index].epoch;
     const uint64_t t0 = mono_ns();
     unsigned spins = 0;
-    while (f.load(std::memory_order_acquire) < d.epoch) {
+    while (!fill_reached(&f, d.epoch)) {
       if (++spins < 4096) {
         __builtin_ia32_pause();
         continue;
@@ -1256,8 +1266,7 @@ bool fill_in_transit(dora_node* n, const dora_event* e) {
   if (!e->pending || e->ipc.fill != FILL_FLAG) return false;
   RegionHdr* h = n->core->region->hdr();
   if (e->ipc.flag_node >= h->n_nodes || e->ipc.flag_index >= kFillFlags) return false;
-  if (h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch.load(std::memory_order_acquire) >=
-      e->ipc.epoch)
+  if (fill_reached(&h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch, e->ipc.epoch))
     return false;
   return mono_ns() - e->arrived_ns < transit_limit_ns();
 }
@@ -1399,7 +1408,7 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       auto& t = n->transit;
       t.emplace_back(n->core->flag_host(static_cast<int>(d.ipc.flag_index)), d.ipc.epoch);
       // bounded even for a sender that never reaches its cap
-      while (t.size() > 256 && t.front().first->load(std::memory_order_acquire) >= t.front().second)
+      while (t.size() > 256 && fill_reached(t.front().first, t.front().second))
         t.pop_front();
       if (t.size() > 1024) t.pop_front();
     }
@@ -1413,7 +1422,7 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
 // fills of one sender finish roughly in order; one flag load per completed fill).
 size_t in_transit(dora_node* n) {
   auto& t = n->transit;
-  while (!t.empty() && t.front().first->load(std::memory_order_acquire) >= t.front().second)
+  while (!t.empty() && fill_reached(t.front().first, t.front().second))
     t.pop_front();
   return t.size();
 }
@@ -1484,6 +1493,9 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
 }
 
 constexpr size_t kTimingPairs = 64;
+// Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k] workgroup k's end.
+constexpr uint32_t kRegionCpAreas = 256;
+constexpr size_t kCpAreaWords = 1 + kMaxSignalWgs;
 constexpr size_t kMaxIntervals = 1 << 16;  // stamped packs whose (start, stop) are kept
 
 void harvest(dora_node* n, TimingPair& p) {
@@ -1588,8 +1600,16 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
     // host-bound size: one raw AQL packet instead of hipLaunchKernel (aql.h)
     if (AqlQueue* q = aql_queue(n->core->device)) {
       const std::atomic<uint64_t>* fh = n->core->flag_host(s->slot->flag);
+      // a timed region's pack may be signalled by the command processor if it has a stamp area
+      int area = -1;
+      uint64_t* stamps = nullptr;
+      if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas) {
+        area = int(n->region_cp_next++);
+        stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
+      }
+      s->slot->region_cp_area = area;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap)) == DORA_OK) {
+                   n->region_armed, slot_bytes(s->slot->cap), stamps) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -1780,7 +1800,7 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
   if (w.kind == FILL_FLAG && w.flag) {
     const uint64_t t0 = mono_ns();
     uint32_t spins = 0;
-    while (w.flag->load(std::memory_order_acquire) < w.epoch) {
+    while (!fill_reached(w.flag, w.epoch)) {
       if (++spins < 4096) {
         __builtin_ia32_pause();
         continue;
@@ -2076,6 +2096,10 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   if (n->timing_ref) (void)hipEventDestroy(n->timing_ref);
   if (n->region_start) (void)hipEventDestroy(n->region_start);
   for (hipEvent_t e : n->region_stop) (void)hipEventDestroy(e);
+  if (n->region_cp_stamps) {
+    dora::aql_fence_all();  // no pack of this node may still write its stamps
+    (void)hipFree(n->region_cp_stamps);
+  }
   delete n;
 }
 
@@ -2088,7 +2112,7 @@ int dora_node_sync(dora_node* n) {
   const uint64_t t0 = dora::mono_ns();
   for (auto* v : {&c->aql_pending, &c->flag_pending}) {
     for (auto& x : *v)
-      while (x.first->load(std::memory_order_acquire) < x.second) {
+      while (!dora::fill_reached(x.first, x.second)) {
         if (dora::mono_ns() - t0 > 10000000000ull)
           return dora::fail(DORA_ERR_TIMEOUT, "a fill did not complete within 10 s");
         __builtin_ia32_pause();
@@ -2441,6 +2465,19 @@ int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
   if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
+  // zeroed stamp areas for the region's CP-signalled packs (made once; re-zeroed per region,
+  // before its clock starts)
+  const size_t cp_bytes = size_t(dora::kRegionCpAreas) * dora::kCpAreaWords * 8;
+  if (!n->region_cp_stamps && hipMalloc(&n->region_cp_stamps, cp_bytes) != hipSuccess) {
+    n->region_cp_stamps = nullptr;  // the region's packs then signal in-kernel
+    (void)hipGetLastError();
+  }
+  if (n->region_cp_stamps) {
+    DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, cp_bytes, n->core->stream));
+    DORA_HIP(hipStreamSynchronize(n->core->stream));
+  }
+  n->region_cp_next = 0;
+  n->region_cp_used.clear();
   n->region_armed = true;
   n->region_started = false;
   n->region_packs = n->region_bytes = n->region_aql = 0;
@@ -2492,6 +2529,26 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
     for (dora::Slot* s : live)
       if (s->region_epoch && !dora::wait_slot_idle(n, s))
         return dora::fail(DORA_ERR_TIMEOUT, "a timed pack did not complete within 10 s");
+    if (!n->region_cp_used.empty()) {
+      // CP-signalled packs: their first workgroup's start and their last workgroup's end, from
+      // the stamp areas (written through by the packs, all of which have completed)
+      std::vector<uint64_t> st(size_t(n->region_cp_next) * dora::kCpAreaWords);
+      DORA_HIP(hipMemcpy(st.data(), n->region_cp_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+      for (uint32_t area : n->region_cp_used) {
+        const uint64_t* w = st.data() + size_t(area) * dora::kCpAreaWords;
+        const uint64_t a = w[0];
+        const uint64_t b = *std::max_element(w + 1, w + dora::kCpAreaWords);
+        if (!a || b < a) continue;
+        if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
+        if (!n->region_stamped || b > n->region_tmax) n->region_tmax = b;
+        ++n->region_stamped;
+        if (n->region_ticks.size() < 2 * (1u << 16)) {
+          n->region_ticks.push_back(a);
+          n->region_ticks.push_back(b);
+        }
+      }
+      n->region_cp_used.clear();
+    }
     if (n->region_stamped)
       *span_ms = double(n->region_tmax - n->region_tmin) / dora::kRealtimeHz * 1e3;
     if (packs) *packs = n->region_stamped;

@@ -471,9 +471,23 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
       if constexpr (__is_same(A, AqlBatchArgs)) signal_batch(args, blk, nblk, t_start);
       else signal_fill(args, blk, nblk, t_start);
     } else if (args.done) {
-      // done words but no flag: the dispatch's completion signal reports the fill (aql.cpp
-      // pipeline probe); every wave's stores are complete before it ends
+      // done words but no flag: the dispatch's completion signal reports the fill (the command
+      // processor's, aql.cpp cp_signal_window); every wave's stores are complete before it ends
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (args.epoch) {
+        // a pack inside a timed region: `epoch` is its stamp area (device memory, zeroed by the
+        // host) — [0] the first workgroup's start, [1 + blk] the time workgroup blk's stores
+        // were all complete; written through, before the wave ends (so before the CP's signal)
+        uint64_t* st = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(args.epoch));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __hip_atomic_store(st + 1 + blk, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          if (blk == 0)
+            __hip_atomic_store(st, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
     }
   }
 }

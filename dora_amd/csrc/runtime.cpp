@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include "aql.h"
+#include "shm.h"
 #include "common.h"
 
 namespace dora {
@@ -89,6 +90,25 @@ int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_
   const size_t k = dora::aql_kernel_count();
   if (n) *n = k;
   for (size_t i = 0; i < k && i < cap && counts; ++i) counts[i] = dora::aql_dispatched(device, i);
+  return DORA_OK;
+}
+
+int dora_gpu_test_fill_reached(const void* flag, uint64_t epoch) {
+  if (!flag || (reinterpret_cast<uintptr_t>(flag) & 63))
+    return dora::fail(DORA_ERR_INVALID, "fill flag must be 64-byte aligned");
+  return dora::fill_reached(static_cast<const std::atomic<uint64_t>*>(flag), epoch) ? 1 : 0;
+}
+
+int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
+  if (!flag || (reinterpret_cast<uintptr_t>(flag) & 63) || epoch == 0)
+    return dora::fail(DORA_ERR_INVALID, "fill flag must be 64-byte aligned, epoch > 0");
+  dora::cp_arm(static_cast<dora::FillFlag*>(flag), epoch);
+  return DORA_OK;
+}
+
+int dora_gpu_aql_cp_signalled(int device, uint64_t* count) {
+  if (!count) return dora::fail(DORA_ERR_INVALID, "NULL count");
+  *count = dora::aql_cp_signalled(device);
   return DORA_OK;
 }
 

@@ -20,7 +20,7 @@
 namespace dora {
 
 constexpr uint64_t kRegionMagic = 0x444f5241474d5358ull;  // "DORAGMSX"
-constexpr uint32_t kRegionVersion = 4;
+constexpr uint32_t kRegionVersion = 5;  // 5: FillFlag carries a CP completion signal
 // Upper bound on the nodes of one dataflow.  The region holds only the `n_nodes` entries in use
 // (region_header_bytes), so the bound costs nothing.
 constexpr uint32_t kMaxNodes = 4096;
@@ -43,11 +43,58 @@ constexpr uint32_t kFillFlags = 64;  // per node: one per live device slot
 // plain loads.  The same line carries the pack's first workgroup's start and its signal time
 // (s_memrealtime, 100 MHz ticks): device timing of the fill without profiling the queue.  One
 // cache line each.
+//
+// Mid-size single-segment packs (aql.cpp, cp_signal_window) are signalled by the command
+// processor instead: the packet's completion signal is the `cp` line below, laid out as the
+// runtime's amd_signal_t (hsa/amd_hsa_signal.h: the CP decrements `value` once the dispatch's
+// last wave has ended; no mailbox, so no interrupt), and every wave of the pack waits for its
+// own write-through stores before it ends.  Before such a dispatch the sender stores
+// cp.value = 1, epoch = e - 1 and then cp_epoch = e (release): the fill of epoch e is complete
+// once cp_epoch == e and cp.value has reached 0.  fill_reached() is the one completion test.
+struct alignas(64) CpSignal {
+  int64_t kind;                  // AMD_SIGNAL_KIND_USER
+  std::atomic<int64_t> value;    // 1 while the dispatch runs, 0 after
+  uint64_t event_mailbox_ptr;    // 0: no interrupt
+  uint32_t event_id, reserved1;
+  uint64_t start_ts, end_ts;     // written by the CP when the queue is profiled
+  uint64_t queue_ptr;
+  uint32_t reserved3[2];
+};
+static_assert(sizeof(CpSignal) == 64, "amd_signal_t layout");
+
 struct FillFlag {
   alignas(64) std::atomic<uint64_t> epoch;
   uint64_t t_start, t_end;
+  std::atomic<uint64_t> cp_epoch;  // epoch of the CP-signalled fill `cp` reports
+  CpSignal cp;
 };
+static_assert(offsetof(FillFlag, cp) == 64 && sizeof(FillFlag) == 128, "FillFlag layout");
 constexpr double kRealtimeHz = 100e6;  // s_memrealtime
+
+// Has the fill of epoch `e` into the flag whose `epoch` word `f` points at completed?  In-kernel
+// signals store the epoch (epochs of a flag only grow); a CP-signalled fill is the one cp_epoch
+// names, complete when the CP's decrement has brought cp.value to 0.  A sender sets a flag up for
+// a new fill only after its previous fill has completed (slot reuse waits for it).
+inline bool fill_reached(const std::atomic<uint64_t>* f, uint64_t e) {
+  if (f->load(std::memory_order_acquire) >= e) return true;
+  const FillFlag* ff = reinterpret_cast<const FillFlag*>(f);
+  return ff->cp_epoch.load(std::memory_order_acquire) == e &&
+         ff->cp.value.load(std::memory_order_acquire) <= 0;
+}
+
+// Set flag `ff` up for the CP-signalled fill of epoch `e` (the sender, before the dispatch; the
+// flag's previous fill has completed).  The epoch word first, so that a check of an earlier
+// epoch of this flag never sees it incomplete; cp_epoch last, with release.
+inline void cp_arm(FillFlag* ff, uint64_t e) {
+  ff->cp.kind = 1;  // AMD_SIGNAL_KIND_USER
+  ff->cp.event_mailbox_ptr = 0;
+  ff->cp.event_id = 0;
+  ff->cp.queue_ptr = 0;
+  if (ff->epoch.load(std::memory_order_relaxed) < e - 1)
+    ff->epoch.store(e - 1, std::memory_order_relaxed);
+  ff->cp.value.store(1, std::memory_order_relaxed);
+  ff->cp_epoch.store(e, std::memory_order_release);
+}
 
 struct NodeEntry {
   FillFlag fill[kFillFlags];

@@ -109,6 +109,13 @@ def aql_dispatch_counts(device: int = 0) -> dict:
     return {lib.dora_gpu_aql_kernel_name(k).decode(): c[k] for k in range(n.value)}
 
 
+def aql_cp_signalled(device: int = 0) -> int:
+    """Packs whose fill the command processor signalled (DORA_GPU_AQL_CP_SIGNAL window)."""
+    a = c_uint64()
+    call("dora_gpu_aql_cp_signalled", device, byref(a))
+    return a.value
+
+
 def aql_batch_stats(device: int = 0) -> dict:
     """Batch packs dispatched, the sends they carried, sends that waited for a queue."""
     a, b, c = c_uint64(), c_uint64(), c_uint64()

@@ -100,6 +100,10 @@ const char* dora_gpu_aql_kernel_name(size_t k);
  * queue busy leave together as one batch pack). */
 int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs,
                              uint64_t* backlogged);
+/* Diagnostics: packs on HIP device `device` whose fill the command processor signalled (the
+ * packet's completion signal instead of the in-kernel flag store; mid-size single-segment packs
+ * sent alone, DORA_GPU_AQL_CP_SIGNAL). */
+int dora_gpu_aql_cp_signalled(int device, uint64_t* count);
 
 int dora_gpu_device_count(int* count);
 int dora_gpu_set_device(int ordinal);
@@ -243,6 +247,11 @@ int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint
                              const uint64_t* flags, const uint64_t* epochs, uint8_t* out,
                              size_t cap, uint32_t* grid);
 int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
+/* Test tools (host only) of the fill-flag protocol (FillFlag, 128 bytes, 64-byte aligned): the
+ * completion test of epoch `epoch` (1: complete) and the sender's set-up of a fill the command
+ * processor signals. */
+int dora_gpu_test_fill_reached(const void* flag, uint64_t epoch);
+int dora_gpu_test_cp_arm(void* flag, uint64_t epoch);
 /* Test hook (microbenchmark): `n` single-segment AQL packs of `bytes` from rotating HBM sources,
  * round robin over `queues` of the device's AQL queues with at most `depth` outstanding per
  * queue; mode 0 completes them with the in-kernel fill signal, 1 with the packet's completion

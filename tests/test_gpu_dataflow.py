@@ -669,6 +669,62 @@ def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
     assert stats["slots_created"] + stats["cache_hits"] == n_msgs
 
 
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_cp_signalled_mid_size_sends_bit_exact(launcher, tmp_path, mode):
+    """Mid-size single-segment packs sent alone are signalled by the command processor (the
+    packet's completion signal in the flag's CpSignal line, shm.h) instead of the in-kernel flag
+    store.  Sizes across the window (2 MiB, 4 MiB + 13, misaligned sources, 16 MB) and past it
+    (1 MB, 40.96 MB: in-kernel signals) interleave on the same slots' flags, so a flag goes from
+    one completion rule to the other and back: every delivered payload must match its own
+    checksum, and the sender must have used the CP path."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    sizes = [(2 << 20, 0), ((4 << 20) + 13, 3), (4096000, 0), (1 << 20, 0), (16 << 20, 7),
+             (6 << 20, 1), (40960000, 0), ((2 << 20) - 1, 0)]
+    nsrc = 6
+    stride = 41 << 20
+    s = device.Stream()
+    bufs = []
+    for k in range(nsrc):
+        b = device.DeviceBuffer(stride)
+        device.fill_splitmix(b.ptr, stride, 0xC0DE0000 + k, s)
+        bufs.append(b)
+    s.sync()
+    plan = []
+    n_msgs = 240
+    for k in range(n_msgs):
+        size, off = sizes[(k * 5 + k // len(sizes)) % len(sizes)]
+        src = bufs[k % nsrc]
+        plan.append((src.ptr + off, size, to_i64(device.csum64(src.ptr + off, size, s))))
+    s.close()
+    cp0 = device.aql_cp_signalled(0)
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(mode == "async")
+        for k, (ptr, size, csum) in enumerate(plan):
+            node.send_output_device_bytes("data", ptr, size,
+                                          {"seq": k, "csum": csum, "verify": True})
+        node.send_output("data", b"", {"seq": n_msgs, "ack": True})
+        node.wait_input("ack", "seq", n_msgs, 60.0)
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    cp = device.aql_cp_signalled(0) - cp0
+    for b in bufs:
+        b.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(x["verified"] for x in out["series"]) == n_msgs
+    assert sum(x["mismatches"] for x in out["series"]) == 0
+    in_window = sum(1 for _, size, _ in plan if (2 << 20) <= size < (32 << 20))
+    print(f"{mode}: {cp} of {in_window} in-window sends signalled by the command processor")
+    assert cp > 0
+
+
 class _StreamHandle:
     def __init__(self, h):
         self.handle = h
