@@ -552,7 +552,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // A lone mid-size single-segment pack signalled by the command processor (cp_signal_window):
   // no in-kernel flag, every wave waits for its own stores, the packet's completion signal is
   // the flag's CpSignal line (shm.h FillFlag)
-  const bool cp = !batch && it0.cp && it0.flag_host && (one || cp_multi());
+  bool cp = !batch && it0.cp && it0.flag_host && (one || cp_multi());
   int rc;
   if (batch) {
     BatchItem bi[kBatchMsgs];
@@ -569,6 +569,13 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll);
   } else {
     rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll, it0.dst_cap);
+  }
+  if (rc == DORA_OK && cp && it0.cp_stamps && grid > kCpStampWgs) {
+    // more workgroups than the stamp area holds: this one signals in-kernel
+    cp = false;
+    rc = one ? build_aql_args1(segs[0], dst, sig, args, &grid, &unroll)
+             : build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll,
+                              it0.dst_cap);
   }
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};

@@ -30,8 +30,10 @@ AqlQueue* aql_queue(int device);
 // `dst_cap`: bytes writable from `dst` (0: unknown; see launch_pack).
 // With `profile`, the packet carries a completion signal whose dispatch times
 // aql_profile_take() reports.  `profile` packs (a timed region's) are signalled by the command
-// processor only when `cp_stamps` (device memory, (1 + kMaxSignalWgs) zeroed words) takes their
-// stamps: [0] the first workgroup's start, [1 + k] workgroup k's completion (s_memrealtime).
+// processor only when `cp_stamps` (device memory, 1 + kCpStampWgs zeroed words) takes their
+// stamps: [0] the first workgroup's start, [1 + k] workgroup k's completion (s_memrealtime); a
+// pack of more workgroups then signals in-kernel.
+constexpr uint32_t kCpStampWgs = 1024;
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
              uint64_t* cp_stamps = nullptr);

@@ -673,9 +673,13 @@ struct dora_node {
   // kernel stamps (s_memrealtime ticks) of the region's packs, harvested from their flag lines
   uint64_t region_stamped = 0, region_unstamped = 0, region_tmin = 0, region_tmax = 0;
   std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
-  // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory,
-  // zeroed at region_begin, read back once at region_end
-  uint64_t* region_cp_stamps = nullptr;
+  // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory
+  // (stamps to host memory held every pack's end for their PCIe writes: C3 0.44-0.52 of HBM),
+  // the areas the last region used zeroed at region_begin, copied into pinned memory at
+  // region_end (a pageable copy preceded stalled sends, profiles/r03_cp_signal_ab.jsonl)
+  uint64_t* region_cp_stamps = nullptr;      // device
+  uint64_t* region_cp_host = nullptr;        // pinned copy
+  hipStream_t region_cp_stream = nullptr;    // their memset / copy (never the node stream)
   uint32_t region_cp_next = 0;
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
@@ -1495,7 +1499,7 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
 constexpr size_t kTimingPairs = 64;
 // Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k] workgroup k's end.
 constexpr uint32_t kRegionCpAreas = 256;
-constexpr size_t kCpAreaWords = 1 + kMaxSignalWgs;
+constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
 constexpr size_t kMaxIntervals = 1 << 16;  // stamped packs whose (start, stop) are kept
 
 void harvest(dora_node* n, TimingPair& p) {
@@ -2099,6 +2103,8 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   if (n->region_cp_stamps) {
     dora::aql_fence_all();  // no pack of this node may still write its stamps
     (void)hipFree(n->region_cp_stamps);
+    (void)hipHostFree(n->region_cp_host);
+    (void)hipStreamDestroy(n->region_cp_stream);
   }
   delete n;
 }
@@ -2465,16 +2471,27 @@ int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
   if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
-  // zeroed stamp areas for the region's CP-signalled packs (made once; re-zeroed per region,
-  // before its clock starts)
+  // zeroed stamp areas for the region's CP-signalled packs (made once; the areas the last region
+  // used re-zeroed, before its clock starts; every pack of that region has completed)
   const size_t cp_bytes = size_t(dora::kRegionCpAreas) * dora::kCpAreaWords * 8;
-  if (!n->region_cp_stamps && hipMalloc(&n->region_cp_stamps, cp_bytes) != hipSuccess) {
-    n->region_cp_stamps = nullptr;  // the region's packs then signal in-kernel
-    (void)hipGetLastError();
+  size_t zero = size_t(n->region_cp_next) * dora::kCpAreaWords * 8;
+  if (!n->region_cp_stamps) {
+    void* d = nullptr;
+    void* h = nullptr;
+    if (hipMalloc(&d, cp_bytes) == hipSuccess && hipHostMalloc(&h, cp_bytes) == hipSuccess &&
+        hipStreamCreateWithFlags(&n->region_cp_stream, hipStreamNonBlocking) == hipSuccess) {
+      n->region_cp_stamps = static_cast<uint64_t*>(d);
+      n->region_cp_host = static_cast<uint64_t*>(h);
+      zero = cp_bytes;
+    } else {  // the region's packs then signal in-kernel
+      if (d) (void)hipFree(d);
+      if (h) (void)hipHostFree(h);
+      (void)hipGetLastError();
+    }
   }
-  if (n->region_cp_stamps) {
-    DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, cp_bytes, n->core->stream));
-    DORA_HIP(hipStreamSynchronize(n->core->stream));
+  if (n->region_cp_stamps && zero) {
+    DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, zero, n->region_cp_stream));
+    DORA_HIP(hipStreamSynchronize(n->region_cp_stream));
   }
   n->region_cp_next = 0;
   n->region_cp_used.clear();
@@ -2532,10 +2549,12 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
     if (!n->region_cp_used.empty()) {
       // CP-signalled packs: their first workgroup's start and their last workgroup's end, from
       // the stamp areas (written through by the packs, all of which have completed)
-      std::vector<uint64_t> st(size_t(n->region_cp_next) * dora::kCpAreaWords);
-      DORA_HIP(hipMemcpy(st.data(), n->region_cp_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+      const size_t used = size_t(n->region_cp_next) * dora::kCpAreaWords * 8;
+      DORA_HIP(hipMemcpyAsync(n->region_cp_host, n->region_cp_stamps, used, hipMemcpyDeviceToHost,
+                              n->region_cp_stream));
+      DORA_HIP(hipStreamSynchronize(n->region_cp_stream));
       for (uint32_t area : n->region_cp_used) {
-        const uint64_t* w = st.data() + size_t(area) * dora::kCpAreaWords;
+        const uint64_t* w = n->region_cp_host + size_t(area) * dora::kCpAreaWords;
         const uint64_t a = w[0];
         const uint64_t b = *std::max_element(w + 1, w + dora::kCpAreaWords);
         if (!a || b < a) continue;

@@ -476,8 +476,8 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (args.epoch) {
         // a pack inside a timed region: `epoch` is its stamp area (device memory, zeroed by the
-        // host) — [0] the first workgroup's start, [1 + blk] the time workgroup blk's stores
-        // were all complete; written through, before the wave ends (so before the CP's signal)
+        // host, read once the region's packs have all completed) — [0] the first workgroup's
+        // start, [1 + blk] the time workgroup blk's stores were all complete; written through
         uint64_t* st = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(args.epoch));
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -485,7 +485,6 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
                              __HIP_MEMORY_SCOPE_SYSTEM);
           if (blk == 0)
             __hip_atomic_store(st, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
       }
     }

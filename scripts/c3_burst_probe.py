@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""The bench's C3 block alone (bench.run_c3_block: warm-up, 200-send steady region, 20-send
+burst) `--reps` times in one dataflow, printing per rep the burst's send-call times, pack starts
+and fraction of HBM; with DORA_GPU_SUBPHASES=1 the sender's host sub-phases follow at exit.
+Diagnoses the burst's host stall with CP-signalled multi-segment packs.
+
+    DORA_GPU_AQL_CP_MULTI=1 python scripts/c3_burst_probe.py --reps 3
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--steady", type=int, default=200)
+    a = ap.parse_args()
+    import bench
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    res = os.path.join(tempfile.mkdtemp(prefix="dora-c3-burst-"), "sink.json")
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["throughput"], "inputs": {"ack": "sink/ack"}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"throughput": {"source": "node/throughput", "queue_size": 10}},
+         "env": {"DORA_BENCH_RESULT": res}},
+    ]}
+    with Dataflow(desc) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        node.set_async_sends(True)
+        stream = device.Stream()
+        seq = 0
+
+        def wait_ack(s, timeout=60.0):
+            node.wait_input("ack", "seq", s, timeout)
+
+        for r in range(a.reps):
+            seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
+            print(json.dumps({"rep": r, "cp_multi": os.environ.get("DORA_GPU_AQL_CP_MULTI", "0"),
+                              "frac": c3["roofline"]["frac"],
+                              "steady_frac": (c3["steady"] or {}).get("frac"),
+                              "send_calls_us": c3["send_calls_us"],
+                              "pack_starts_us": [x for x, _ in c3["pack_intervals_us"]],
+                              "cp_signalled": device.aql_cp_signalled(0)}), flush=True)
+        stream.close()
+        node.close()
+        df.wait(60)
+
+
+if __name__ == "__main__":
+    main()
