@@ -877,10 +877,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.cp_stamps = cp_stamps;
   for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
   // inside a timed region only with a stamp area for the pack's own stamps
-  const auto cw = cp_signal_window();
-  p.cp = (!profile || cp_stamps) && flag_host &&
-         ((n == 1 && segs[0].dst_off == 0) || cp_multi()) && p.bytes >= cw.first &&
-         p.bytes < cw.second;
+  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n);
   std::lock_guard<std::mutex> g(a->mu);
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
@@ -915,6 +912,14 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
     a->cv.notify_one();
   }
   return DORA_OK;
+}
+
+bool aql_cp_candidate(const Segment* segs, size_t n) {
+  if (n == 0 || !((n == 1 && segs[0].dst_off == 0) || cp_multi())) return false;
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
+  const auto cw = cp_signal_window();
+  return bytes >= cw.first && bytes < cw.second;
 }
 
 int bar_alloc(int device, size_t bytes, void** out) {

@@ -34,6 +34,10 @@ AqlQueue* aql_queue(int device);
 // stamps: [0] the first workgroup's start, [1 + k] workgroup k's completion (s_memrealtime); a
 // pack of more workgroups then signals in-kernel.
 constexpr uint32_t kCpStampWgs = 1024;
+
+// Would a pack of these segments, sent alone, be signalled by the command processor
+// (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI)?
+bool aql_cp_candidate(const Segment* segs, size_t n);
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
              uint64_t* cp_stamps = nullptr);

@@ -675,11 +675,11 @@ struct dora_node {
   std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
   // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory
   // (stamps to host memory held every pack's end for their PCIe writes: C3 0.44-0.52 of HBM),
-  // the areas the last region used zeroed at region_begin, copied into pinned memory at
-  // region_end (a pageable copy preceded stalled sends, profiles/r03_cp_signal_ab.jsonl)
+  // made and zeroed when the node starts, copied into pinned memory and the used areas re-zeroed
+  // at region_end.  No HIP call in region_begin: a memset + synchronise there made the region's
+  // first send take 27-31 us instead of 4 (profiles/r03_cp_signal_ab.jsonl, first_send_ab).
   uint64_t* region_cp_stamps = nullptr;      // device
   uint64_t* region_cp_host = nullptr;        // pinned copy
-  hipStream_t region_cp_stream = nullptr;    // their memset / copy (never the node stream)
   uint32_t region_cp_next = 0;
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
@@ -1607,7 +1607,8 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       // a timed region's pack may be signalled by the command processor if it has a stamp area
       int area = -1;
       uint64_t* stamps = nullptr;
-      if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas) {
+      if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas &&
+          aql_cp_candidate(segs, nseg)) {
         area = int(n->region_cp_next++);
         stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
       }
@@ -2000,6 +2001,28 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   n->core = core;
   n->id = node_id;
   for (auto& o : dora::split(e.outputs, ',')) n->outputs.insert(o);
+  // stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed
+  // here, never inside or just before a region (DORA_GPU_REGION_CP_STAMPS=0: none, such packs
+  // then signal in-kernel inside regions)
+  static const bool cp_stamps_on = [] {
+    const char* v = std::getenv("DORA_GPU_REGION_CP_STAMPS");
+    return !(v && *v == '0');
+  }();
+  if (core->device >= 0 && !n->outputs.empty() && cp_stamps_on) {
+    const size_t cp_bytes = size_t(dora::kRegionCpAreas) * dora::kCpAreaWords * 8;
+    void* d = nullptr;
+    void* h = nullptr;
+    if (hipMalloc(&d, cp_bytes) == hipSuccess && hipHostMalloc(&h, cp_bytes) == hipSuccess &&
+        hipMemsetAsync(d, 0, cp_bytes, core->stream) == hipSuccess &&
+        hipStreamSynchronize(core->stream) == hipSuccess) {
+      n->region_cp_stamps = static_cast<uint64_t*>(d);
+      n->region_cp_host = static_cast<uint64_t*>(h);
+    } else {
+      if (d) (void)hipFree(d);
+      if (h) (void)hipHostFree(h);
+      (void)hipGetLastError();
+    }
+  }
   for (auto& kv : dora::split(e.inputs, ',')) {
     auto eq = kv.find('=');
     n->queue_size[kv.substr(0, eq)] = static_cast<uint32_t>(std::stoul(kv.substr(eq + 1)));
@@ -2104,7 +2127,6 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     dora::aql_fence_all();  // no pack of this node may still write its stamps
     (void)hipFree(n->region_cp_stamps);
     (void)hipHostFree(n->region_cp_host);
-    (void)hipStreamDestroy(n->region_cp_stream);
   }
   delete n;
 }
@@ -2471,29 +2493,9 @@ int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
   if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
-  // zeroed stamp areas for the region's CP-signalled packs (made once; the areas the last region
-  // used re-zeroed, before its clock starts; every pack of that region has completed)
-  const size_t cp_bytes = size_t(dora::kRegionCpAreas) * dora::kCpAreaWords * 8;
-  size_t zero = size_t(n->region_cp_next) * dora::kCpAreaWords * 8;
-  if (!n->region_cp_stamps) {
-    void* d = nullptr;
-    void* h = nullptr;
-    if (hipMalloc(&d, cp_bytes) == hipSuccess && hipHostMalloc(&h, cp_bytes) == hipSuccess &&
-        hipStreamCreateWithFlags(&n->region_cp_stream, hipStreamNonBlocking) == hipSuccess) {
-      n->region_cp_stamps = static_cast<uint64_t*>(d);
-      n->region_cp_host = static_cast<uint64_t*>(h);
-      zero = cp_bytes;
-    } else {  // the region's packs then signal in-kernel
-      if (d) (void)hipFree(d);
-      if (h) (void)hipHostFree(h);
-      (void)hipGetLastError();
-    }
-  }
-  if (n->region_cp_stamps && zero) {
-    DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, zero, n->region_cp_stream));
-    DORA_HIP(hipStreamSynchronize(n->region_cp_stream));
-  }
-  n->region_cp_next = 0;
+  // stamp areas still dirty (a region that did not reach its stamped end): none this region;
+  // the next stamped region_end zeroes them all
+  if (n->region_cp_next) n->region_cp_next = dora::kRegionCpAreas;
   n->region_cp_used.clear();
   n->region_armed = true;
   n->region_started = false;
@@ -2546,13 +2548,18 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
     for (dora::Slot* s : live)
       if (s->region_epoch && !dora::wait_slot_idle(n, s))
         return dora::fail(DORA_ERR_TIMEOUT, "a timed pack did not complete within 10 s");
-    if (!n->region_cp_used.empty()) {
+    if (n->region_cp_next) {
       // CP-signalled packs: their first workgroup's start and their last workgroup's end, from
-      // the stamp areas (written through by the packs, all of which have completed)
+      // the stamp areas (written through by the packs, all of which have completed); then the
+      // areas this region handed out are zeroed for the next one
       const size_t used = size_t(n->region_cp_next) * dora::kCpAreaWords * 8;
-      DORA_HIP(hipMemcpyAsync(n->region_cp_host, n->region_cp_stamps, used, hipMemcpyDeviceToHost,
-                              n->region_cp_stream));
-      DORA_HIP(hipStreamSynchronize(n->region_cp_stream));
+      hipStream_t st = n->core->stream;
+      if (!n->region_cp_used.empty())
+        DORA_HIP(hipMemcpyAsync(n->region_cp_host, n->region_cp_stamps, used,
+                                hipMemcpyDeviceToHost, st));
+      DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, used, st));
+      DORA_HIP(hipStreamSynchronize(st));
+      n->region_cp_next = 0;
       for (uint32_t area : n->region_cp_used) {
         const uint64_t* w = n->region_cp_host + size_t(area) * dora::kCpAreaWords;
         const uint64_t a = w[0];
