@@ -673,8 +673,8 @@ def test_queue_size_one_distinct_payloads_bit_exact(launcher, tmp_path):
 def test_cp_signalled_mid_size_sends_bit_exact(launcher, tmp_path, mode):
     """Mid-size single-segment packs sent alone are signalled by the command processor (the
     packet's completion signal in the flag's CpSignal line, shm.h) instead of the in-kernel flag
-    store.  Sizes across the window (2 MiB, 4 MiB + 13, misaligned sources, 16 MB) and past it
-    (1 MB, 40.96 MB: in-kernel signals) interleave on the same slots' flags, so a flag goes from
+    store.  Sizes across the window (1-32 MiB: 2 MiB, 4 MiB + 13, misaligned sources, 16 MB) and
+    past it (1 MiB - 16, 40.96 MB: in-kernel signals) interleave on the same slots' flags, so a flag goes from
     one completion rule to the other and back: every delivered payload must match its own
     checksum, and the sender must have used the CP path."""
     from dora_amd import device
@@ -682,7 +682,7 @@ def test_cp_signalled_mid_size_sends_bit_exact(launcher, tmp_path, mode):
     from dora_amd.node import Node
     from dora_amd.verify import to_i64
     res = str(tmp_path / "sink.json")
-    sizes = [(2 << 20, 0), ((4 << 20) + 13, 3), (4096000, 0), (1 << 20, 0), (16 << 20, 7),
+    sizes = [(2 << 20, 0), ((4 << 20) + 13, 3), (4096000, 0), ((1 << 20) - 16, 0), (16 << 20, 7),
              (6 << 20, 1), (40960000, 0), ((2 << 20) - 1, 0)]
     nsrc = 6
     stride = 41 << 20
@@ -720,9 +720,11 @@ def test_cp_signalled_mid_size_sends_bit_exact(launcher, tmp_path, mode):
     assert out["errors"] == 0
     assert sum(x["verified"] for x in out["series"]) == n_msgs
     assert sum(x["mismatches"] for x in out["series"]) == 0
-    in_window = sum(1 for _, size, _ in plan if (2 << 20) <= size < (32 << 20))
+    in_window = sum(1 for _, size, _ in plan if (1 << 20) <= size < (32 << 20))
     print(f"{mode}: {cp} of {in_window} in-window sends signalled by the command processor")
     assert cp > 0
+    if mode == "sync":  # one pack at a time: none waits in the backlog or goes out in a batch
+        assert cp == in_window, (cp, in_window)
 
 
 class _StreamHandle:
