@@ -673,13 +673,13 @@ struct dora_node {
   // kernel stamps (s_memrealtime ticks) of the region's packs, harvested from their flag lines
   uint64_t region_stamped = 0, region_unstamped = 0, region_tmin = 0, region_tmax = 0;
   std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
-  // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory
-  // (stamps to host memory held every pack's end for their PCIe writes: C3 0.44-0.52 of HBM),
-  // made and zeroed when the node starts, copied into pinned memory and the used areas re-zeroed
-  // at region_end.  No HIP call in region_begin: a memset + synchronise there made the region's
-  // first send take 27-31 us instead of 4 (profiles/r03_cp_signal_ab.jsonl, first_send_ab).
-  uint64_t* region_cp_stamps = nullptr;      // device
-  uint64_t* region_cp_host = nullptr;        // pinned copy
+  // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory the
+  // host reads through the BAR (stamps written to host memory held every pack's end for their
+  // PCIe writes: C3 0.44-0.52 of HBM), made and zeroed when the node starts.  No HIP work around a
+  // region: a memset or copy on a HIP stream right before a region made its first send take
+  // 25-45 us instead of 4 (profiles/r03_cp_signal_ab.jsonl, first_send_ab).  Areas are never
+  // re-zeroed: an area's stale words are an earlier pack's, older than the current pack's own.
+  uint64_t* region_cp_stamps = nullptr;  // coarse-grained device memory, host-mapped (aql.h bar_alloc)
   uint32_t region_cp_next = 0;
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
@@ -1434,6 +1434,34 @@ size_t in_transit(dora_node* n) {
 constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
 
 // `ext_len` > len: the slot also holds a validity tail (plans with in-sample bitmaps).
+// Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k] workgroup k's end.
+constexpr uint32_t kRegionCpAreas = 256;
+constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
+
+// Stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed with
+// the node's AQL queues at its first send, never inside or just before a region
+// (DORA_GPU_REGION_CP_STAMPS=0: none; such packs then signal in-kernel inside regions).
+void ensure_cp_stamps(dora_node* n) {
+  static const bool on = [] {
+    const char* v = std::getenv("DORA_GPU_REGION_CP_STAMPS");
+    return !(v && *v == '0');
+  }();
+  if (!on || n->region_cp_stamps || n->core->device < 0) return;
+  const size_t bytes = size_t(kRegionCpAreas) * kCpAreaWords * 8;
+  void* d = nullptr;
+  if (bar_alloc(n->core->device, bytes, &d) != DORA_OK) {
+    clear_error();
+    return;  // no large BAR: a region's packs signal in-kernel
+  }
+  const std::vector<uint8_t> zero(bytes, 0);
+  if (bar_write(n->core->device, d, zero.data(), bytes) != DORA_OK) {
+    bar_free(d);
+    clear_error();
+    return;
+  }
+  n->region_cp_stamps = static_cast<uint64_t*>(d);
+}
+
 int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
                  uint64_t ext_len = 0) {  // mod.rs:303-319
   if (n->core->device < 0) {
@@ -1459,7 +1487,7 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
       // pack code object (~20 ms), whatever its size: a later small send then finds them ready
       // instead of paying that inside its latency (nodes that never send data create none)
       n->aql_ready = true;
-      (void)aql_queue(n->core->device);
+      if (aql_queue(n->core->device)) ensure_cp_stamps(n);
     }
     SubSpan sp_tok(SP_ALLOC_TOKENS);
     handle_finished_drop_tokens(n);
@@ -1497,9 +1525,6 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
 }
 
 constexpr size_t kTimingPairs = 64;
-// Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k] workgroup k's end.
-constexpr uint32_t kRegionCpAreas = 256;
-constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
 constexpr size_t kMaxIntervals = 1 << 16;  // stamped packs whose (start, stop) are kept
 
 void harvest(dora_node* n, TimingPair& p) {
@@ -2001,28 +2026,6 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   n->core = core;
   n->id = node_id;
   for (auto& o : dora::split(e.outputs, ',')) n->outputs.insert(o);
-  // stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed
-  // here, never inside or just before a region (DORA_GPU_REGION_CP_STAMPS=0: none, such packs
-  // then signal in-kernel inside regions)
-  static const bool cp_stamps_on = [] {
-    const char* v = std::getenv("DORA_GPU_REGION_CP_STAMPS");
-    return !(v && *v == '0');
-  }();
-  if (core->device >= 0 && !n->outputs.empty() && cp_stamps_on) {
-    const size_t cp_bytes = size_t(dora::kRegionCpAreas) * dora::kCpAreaWords * 8;
-    void* d = nullptr;
-    void* h = nullptr;
-    if (hipMalloc(&d, cp_bytes) == hipSuccess && hipHostMalloc(&h, cp_bytes) == hipSuccess &&
-        hipMemsetAsync(d, 0, cp_bytes, core->stream) == hipSuccess &&
-        hipStreamSynchronize(core->stream) == hipSuccess) {
-      n->region_cp_stamps = static_cast<uint64_t*>(d);
-      n->region_cp_host = static_cast<uint64_t*>(h);
-    } else {
-      if (d) (void)hipFree(d);
-      if (h) (void)hipHostFree(h);
-      (void)hipGetLastError();
-    }
-  }
   for (auto& kv : dora::split(e.inputs, ',')) {
     auto eq = kv.find('=');
     n->queue_size[kv.substr(0, eq)] = static_cast<uint32_t>(std::stoul(kv.substr(eq + 1)));
@@ -2125,8 +2128,7 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   for (hipEvent_t e : n->region_stop) (void)hipEventDestroy(e);
   if (n->region_cp_stamps) {
     dora::aql_fence_all();  // no pack of this node may still write its stamps
-    (void)hipFree(n->region_cp_stamps);
-    (void)hipHostFree(n->region_cp_host);
+    dora::bar_free(n->region_cp_stamps);
   }
   delete n;
 }
@@ -2493,9 +2495,7 @@ int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
   if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
-  // stamp areas still dirty (a region that did not reach its stamped end): none this region;
-  // the next stamped region_end zeroes them all
-  if (n->region_cp_next) n->region_cp_next = dora::kRegionCpAreas;
+  n->region_cp_next = 0;
   n->region_cp_used.clear();
   n->region_armed = true;
   n->region_started = false;
@@ -2549,21 +2549,16 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
       if (s->region_epoch && !dora::wait_slot_idle(n, s))
         return dora::fail(DORA_ERR_TIMEOUT, "a timed pack did not complete within 10 s");
     if (n->region_cp_next) {
-      // CP-signalled packs: their first workgroup's start and their last workgroup's end, from
-      // the stamp areas (written through by the packs, all of which have completed); then the
-      // areas this region handed out are zeroed for the next one
-      const size_t used = size_t(n->region_cp_next) * dora::kCpAreaWords * 8;
-      hipStream_t st = n->core->stream;
-      if (!n->region_cp_used.empty())
-        DORA_HIP(hipMemcpyAsync(n->region_cp_host, n->region_cp_stamps, used,
-                                hipMemcpyDeviceToHost, st));
-      DORA_HIP(hipMemsetAsync(n->region_cp_stamps, 0, used, st));
-      DORA_HIP(hipStreamSynchronize(st));
+      // CP-signalled packs: their first workgroup's start and their last workgroup's end, read
+      // from the stamp areas through the BAR (written through by the packs, all of which have
+      // completed).  An area's other words are older packs' (earlier regions), never the max.
       n->region_cp_next = 0;
+      std::vector<uint64_t> w(dora::kCpAreaWords);
       for (uint32_t area : n->region_cp_used) {
-        const uint64_t* w = n->region_cp_host + size_t(area) * dora::kCpAreaWords;
+        std::memcpy(w.data(), n->region_cp_stamps + size_t(area) * dora::kCpAreaWords,
+                    dora::kCpAreaWords * 8);
         const uint64_t a = w[0];
-        const uint64_t b = *std::max_element(w + 1, w + dora::kCpAreaWords);
+        const uint64_t b = *std::max_element(w.begin() + 1, w.end());
         if (!a || b < a) continue;
         if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
         if (!n->region_stamped || b > n->region_tmax) n->region_tmax = b;
