@@ -675,7 +675,8 @@ struct dora_node {
   std::vector<uint64_t> region_ticks;  // (start, end) stamps of the region's packs
   // stamp areas of a region's CP-signalled packs (aql.h aql_pack `cp_stamps`): device memory the
   // host reads through the BAR (stamps written to host memory held every pack's end for their
-  // PCIe writes: C3 0.44-0.52 of HBM), made and zeroed when the node starts.  No HIP work around a
+  // PCIe writes: C3 0.44-0.52 of HBM), made and zeroed at the node's first send (ensure_cp_stamps).
+  // No HIP work around a
   // region: a memset or copy on a HIP stream right before a region made its first send take
   // 25-45 us instead of 4 (profiles/r03_cp_signal_ab.jsonl, first_send_ab).  Areas are never
   // re-zeroed: an area's stale words are an earlier pack's, older than the current pack's own.
