@@ -108,6 +108,8 @@ _SIGS = {
     "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
     "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
+    "dora_gpu_test_bcast_group": (c_int, [c_int, c_void_p, c_uint64, POINTER(c_int),
+                                          POINTER(c_int)]),
     "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
                                            POINTER(ctypes.c_double)]),
     "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
@@ -174,6 +176,7 @@ _SIGS = {
     "dora_node_pack_intervals": (c_int, [c_void_p, POINTER(c_double), c_size_t,
                                          POINTER(c_size_t)]),
     "dora_node_peer_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_node_bcast_ranks": (c_int, [c_void_p, POINTER(c_uint64)]),
     "dora_node_bcast_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64),
                                       POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
                                       POINTER(c_char_p)]),

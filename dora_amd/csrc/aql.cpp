@@ -133,6 +133,11 @@ struct AqlQueue {
   hsa_agent_t cpu{};
   hsa_amd_memory_pool_t coarse{};
   bool coarse_ok = false;
+  // HIP device of the queues, and the stream that takes sends a failed queue could not dispatch
+  // (fallback_locked)
+  int device = -1;
+  hipStream_t fallback = nullptr;
+  uint64_t fallbacks = 0;
 };
 
 namespace {
@@ -290,6 +295,7 @@ AqlQueue* create(int device) {
   if (!f.pool_ok) return note("device memory pool");
   auto* a = new AqlQueue();
   a->gpu = f.gpu;
+  a->device = device;
   hsa_amd_hdp_flush_t hdp{};
   if (hsa_agent_get_info(f.gpu, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_HDP_FLUSH),
                          &hdp) != HSA_STATUS_SUCCESS ||
@@ -459,6 +465,14 @@ void aql_forget_flags(int device, const void* base, size_t size) {
   drain_backlog(a, t0, std::chrono::seconds(2));
   std::lock_guard<std::mutex> g(a->mu);
   const auto* lo = static_cast<const uint8_t*>(base);
+  // sends still backlogged after the bound: never dispatched, and their flags are about to go
+  // away — drop them rather than let a later dispatch write into the unmapped region
+  std::deque<Pending> keep_backlog;
+  for (const Pending& p : a->backlog) {
+    const auto* f = reinterpret_cast<const uint8_t*>(p.flag_host);
+    if (f < lo || f >= lo + size) keep_backlog.push_back(p);
+  }
+  a->backlog.swap(keep_backlog);
   for (auto& o : a->outq) {  // outstanding entries pointing into the region go too
     std::deque<Use> keep;
     for (const Use& u : o) {
@@ -509,6 +523,24 @@ std::pair<uint64_t, uint64_t> cp_signal_window() {
       if (end && *end == ':') w = {lo, std::strtoull(end + 1, nullptr, 10)};
     }
     return w;
+  }();
+  return v;
+}
+
+// DORA_GPU_AQL_CP_LONE=0: a single-segment pack above the CP window stays in-kernel-signalled
+// even when it runs alone (sync sends, idle queues).  DORA_GPU_AQL_CP_BIG=1: such packs are
+// CP-signalled even when others run beside them (an A/B knob for the pipelined headline).
+bool cp_lone() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_CP_LONE");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+bool cp_big() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_CP_BIG");
+    return e && *e == '1';
   }();
   return v;
 }
@@ -569,13 +601,6 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll);
   } else {
     rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll, it0.dst_cap);
-  }
-  if (rc == DORA_OK && cp && it0.cp_stamps && grid > kCpStampWgs) {
-    // more workgroups than the stamp area holds: this one signals in-kernel
-    cp = false;
-    rc = one ? build_aql_args1(segs[0], dst, sig, args, &grid, &unroll)
-             : build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll,
-                              it0.dst_cap);
   }
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};
@@ -756,6 +781,16 @@ void prune(AqlQueue* a, int i) {
     o.pop_front();
 }
 
+// No queue has an outstanding packet (a pack dispatched now runs alone on the GPU).
+bool queues_idle(AqlQueue* a) {
+  if (!a->backlog.empty()) return false;
+  for (int i = 0; i < a->nq; ++i) {
+    prune(a, i);
+    if (!a->outq[i].empty()) return false;
+  }
+  return true;
+}
+
 // The queue with the fewest outstanding packets below the depth (ties: round robin) among the
 // first `nq` (0: all), or -1.
 int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
@@ -794,9 +829,43 @@ uint64_t batch_big_bytes() {
   return v;
 }
 
+// Sends that were accepted (aql_pack returned DORA_OK) but can no longer leave through the AQL
+// queues — a dispatch failed and the queues are marked failed — are launched through HIP on
+// the fallback stream instead, each signalling its own fill flag in-kernel (launch_pack), so
+// no sender or receiver waits out a timeout for a fill that was never dispatched (a->mu held).
+void fallback_locked(AqlQueue* a, const Pending* items, size_t n) {
+  if (!n) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != a->device) (void)hipSetDevice(a->device);
+  if (!a->fallback && hipStreamCreateWithFlags(&a->fallback, hipStreamNonBlocking) != hipSuccess) {
+    a->fallback = nullptr;
+    std::fprintf(stderr, "dora-gpu: AQL fallback stream: %s; %zu fills lost\n",
+                 hipGetErrorString(hipGetLastError()), n);
+  }
+  for (size_t k = 0; k < n && a->fallback; ++k) {
+    const Pending& p = items[k];
+    bool signalled = false;
+    if (launch_pack(p.segs, p.n, ARROW_DEVICE_ROCM, p.dst, a->fallback, nullptr, nullptr, &p.sig,
+                    &signalled, p.dst_cap) != DORA_OK ||
+        !signalled)
+      std::fprintf(stderr, "dora-gpu: AQL fallback launch failed: %s\n", dora_gpu_last_error());
+    else
+      ++a->fallbacks;
+  }
+  if (prev >= 0 && prev != a->device) (void)hipSetDevice(prev);
+}
+
+void fallback_backlog_locked(AqlQueue* a) {
+  std::vector<Pending> rest(a->backlog.begin(), a->backlog.end());
+  a->backlog.clear();
+  fallback_locked(a, rest.data(), rest.size());
+}
+
 // Dispatch the backlog into queues with room, as batches of consecutive sends that share a
 // chunk size (a->mu held).
 void pump_locked(AqlQueue* a) {
+  if (a->failed.load()) fallback_backlog_locked(a);
   while (!a->backlog.empty() && !a->failed.load()) {
     // the batch at the front of the backlog
     size_t n = 0, segs = 0;
@@ -820,8 +889,11 @@ void pump_locked(AqlQueue* a) {
       a->backlog.pop_front();
     }
     if (dispatch_locked(a, size_t(qi), batch, n, big) != DORA_OK) {
-      // the fills of these messages never signal: their receivers report them failed
+      // the queues are unusable from here on: these sends and the rest of the backlog leave
+      // through HIP instead
       a->failed.store(true);
+      fallback_locked(a, batch, n);
+      fallback_backlog_locked(a);
       return;
     }
   }
@@ -834,7 +906,7 @@ void dispatcher_main(AqlQueue* a) {
     a->cv.wait(lk, [a] { return !a->backlog.empty(); });
     pump_locked(a);
     if (a->backlog.empty() || a->failed.load()) {
-      if (a->failed.load()) a->backlog.clear();
+      if (a->failed.load()) fallback_backlog_locked(a);
       continue;
     }
     // every queue is full: wait (unlocked) for the oldest packet of any queue to complete
@@ -862,7 +934,7 @@ void dispatcher_main(AqlQueue* a) {
 
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
-             uint64_t* cp_stamps) {
+             uint64_t* cp_stamps, bool sync) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -876,9 +948,12 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.profile = profile;
   p.cp_stamps = cp_stamps;
   for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
-  // inside a timed region only with a stamp area for the pack's own stamps
-  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n);
   std::lock_guard<std::mutex> g(a->mu);
+  // Signalled by the command processor (inside a timed region only with a stamp area for the
+  // pack's own stamps): a pack in the window, and a single-segment pack above it that runs alone
+  // — sent synchronously, or finding every queue idle (aql.h).
+  p.cp = (!profile || cp_stamps) && flag_host &&
+         aql_cp_candidate(segs, n, cp_lone() && (sync || cp_big() || queues_idle(a)));
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
   // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
@@ -914,12 +989,15 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   return DORA_OK;
 }
 
-bool aql_cp_candidate(const Segment* segs, size_t n) {
-  if (n == 0 || !((n == 1 && segs[0].dst_off == 0) || cp_multi())) return false;
+bool aql_cp_candidate(const Segment* segs, size_t n, bool lone) {
+  if (n == 0) return false;
+  const bool single = n == 1 && segs[0].dst_off == 0;
+  if (!single && !cp_multi()) return false;
   uint64_t bytes = 0;
   for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
   const auto cw = cp_signal_window();
-  return bytes >= cw.first && bytes < cw.second;
+  if (cw.second == 0) return false;  // DORA_GPU_AQL_CP_SIGNAL=0
+  return bytes >= cw.first && (bytes < cw.second || (lone && single));
 }
 
 int bar_alloc(int device, size_t bytes, void** out) {

@@ -30,17 +30,21 @@ AqlQueue* aql_queue(int device);
 // `dst_cap`: bytes writable from `dst` (0: unknown; see launch_pack).
 // With `profile`, the packet carries a completion signal whose dispatch times
 // aql_profile_take() reports.  `profile` packs (a timed region's) are signalled by the command
-// processor only when `cp_stamps` (device memory, 1 + kCpStampWgs zeroed words) takes their
-// stamps: [0] the first workgroup's start, [1 + k] workgroup k's completion (s_memrealtime); a
-// pack of more workgroups then signals in-kernel.
-constexpr uint32_t kCpStampWgs = 1024;
-
-// Would a pack of these segments, sent alone, be signalled by the command processor
-// (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI)?
-bool aql_cp_candidate(const Segment* segs, size_t n);
+// processor only when `cp_stamps` (device memory, 1 + kCpStampWgs zeroed words, plan.h) takes
+// their stamps: [0] the first workgroup's start, [1 + k mod kCpStampWgs] the latest completion of
+// the workgroups k that map there (s_memrealtime, atomic max).
+//
+// `sync`: the caller waits for this pack before it does anything else (a synchronous send,
+// node.cpp wait_source_read).  A single-segment pack that is sent synchronously, or that finds
+// every queue idle, runs alone on the GPU: it is signalled by the command processor at any size
+// >= the CP window's lower bound, with a grid of up to cp_grid() workgroups (no done words to
+// poll, so no 1024-workgroup signalling cap).
+// Would a pack of these segments be signalled by the command processor when sent alone
+// (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI; `lone`: also a lone big pack)?
+bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
-             uint64_t* cp_stamps = nullptr);
+             uint64_t* cp_stamps = nullptr, bool sync = false);
 
 // Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
 // region about to be unmapped), after waiting (bounded) for those fills to signal.

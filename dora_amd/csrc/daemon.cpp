@@ -306,6 +306,10 @@ class Daemon {
             throw std::invalid_argument("bad remote input `" + ri + "` in: " + line);
           r.inputs.emplace_back(ri.substr(0, slash), ri.substr(slash + 1));
         }
+        // without its receivers' inputs the output's close could name nothing for the peer
+        // (InputsClosed), and the peer's proxies would never close
+        if (r.inputs.empty())
+          throw std::invalid_argument("remote line names no receiver/input: " + line);
         remote_lines.push_back(std::move(r));
       } else if (kw == "proxy") {  // proxy <node> <gpu>: a remote node feeding local inputs
         ProxySpec p;

@@ -217,6 +217,20 @@ bool Forwarder::stage(const ForwardJob& job, std::vector<uint8_t>* bytes,
   return true;
 }
 
+// Largest inter-daemon frame (DORA_GPU_MAX_FRAME_BYTES; default 64 GiB + 1 MiB of metadata,
+// above any sample a slot holds, so every output the local path delivers also crosses machines).
+// A gateway reading a longer length prefix takes the frame as corrupt or hostile and drops that
+// connection; a forwarder refuses to send one (that message only, with an error naming it), so
+// a message the peer would refuse never severs the link for the messages behind it.
+uint64_t max_frame_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_MAX_FRAME_BYTES");
+    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
+    return x ? x : (uint64_t(64) << 30) + (uint64_t(1) << 20);
+  }();
+  return v;
+}
+
 bool Forwarder::send_to(const std::string& machine, const std::vector<uint8_t>& frame) {
   auto p = peers_.find(machine);
   if (p == peers_.end()) {
@@ -316,6 +330,15 @@ void Forwarder::handle(ForwardJob& job) {
                  job.output_id.c_str(), ex.what());
     return;
   }
+  if (frame.size() > max_frame_bytes()) {
+    std::fprintf(stderr,
+                 "dora-gpu daemon: forwarding `%s/%s`: a %llu-byte frame exceeds the inter-daemon "
+                 "frame limit (%llu bytes, DORA_GPU_MAX_FRAME_BYTES); dropped\n",
+                 job.node_id.c_str(), job.output_id.c_str(),
+                 static_cast<unsigned long long>(frame.size()),
+                 static_cast<unsigned long long>(max_frame_bytes()));
+    return;
+  }
   for (const auto& m : job.machines) send_to(m, frame);
   forwarded_.fetch_add(1, std::memory_order_relaxed);
 }
@@ -400,17 +423,6 @@ void Gateway::accept_loop() {
     reader_fds_.push_back(fd);
     readers_.emplace_back([this, fd] { read_loop(fd); });
   }
-}
-
-// Largest inter-daemon frame accepted (DORA_GPU_MAX_FRAME_BYTES, default 4 GiB + 1 MiB of
-// metadata): a longer length prefix is a corrupt or hostile frame.
-uint64_t max_frame_bytes() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_MAX_FRAME_BYTES");
-    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
-    return x ? x : (uint64_t(4) << 30) + (uint64_t(1) << 20);
-  }();
-  return v;
 }
 
 void Gateway::read_loop(int fd) {

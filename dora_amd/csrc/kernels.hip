@@ -56,6 +56,8 @@ uint32_t env_u32(const char* name) {
 }
 // workgroups of a signalling launch (0: kSignalGrid; DORA_GPU_SIGNAL_GRID, dora_gpu_pack_tune)
 std::atomic<uint32_t> g_signal_grid{env_u32("DORA_GPU_SIGNAL_GRID")};
+// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 8192)
+std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 8192u};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
@@ -514,6 +516,18 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
   return DORA_OK;
 }
 
+// Workgroups of an AQL pack signalled as `sig` says.  In-kernel signals (a flag): the signalling
+// grid (kSignalGrid, or DORA_GPU_SIGNAL_GRID up to the kMaxSignalWgs done words).  Signalled by
+// the command processor (no flag): nothing to poll, so up to aql_cp_grid() workgroups — a lone
+// 40.96 MB pack capped at 1024 keeps 8 MiB in flight, half of what HBM needs.
+uint32_t aql_cp_grid() { return std::max<uint32_t>(1, g_cp_grid.load(std::memory_order_relaxed)); }
+
+uint64_t signal_grid_cap(const FillSignal& sig) {
+  if (!sig.flag) return aql_cp_grid();
+  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
+  return g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
+}
+
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
@@ -544,9 +558,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.nseg = static_cast<uint32_t>(n) | (line_chunks() ? 0u : kUnitChunks);
   a.edge_mask = edge_mask(segs, n, dst, dst_cap);
   a.n_chunks = static_cast<uint32_t>(chunks);
-  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
-  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
   a.flag = sig.flag;
   a.done = sig.done;
   a.epoch = sig.epoch;
@@ -570,9 +582,7 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
   const uint64_t chunks =
       segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
-  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
-  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
   const uint64_t words[6] = {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(sg.src),
                              sg.len, reinterpret_cast<uintptr_t>(sig.flag),
                              reinterpret_cast<uintptr_t>(sig.done), sig.epoch};

@@ -726,12 +726,6 @@ struct dora_node {
 namespace dora {
 namespace {
 
-// A returned drop token does not prove that the slot's last fill has completed: the daemon
-// returns the token at once for an output without receivers, a receiver's drop-oldest queue
-// releases inputs it never waited on, and a finished receiver's tokens are released for it.
-// Before a slot is refilled or freed, wait for its last fill (normally long complete: one load).
-// False when the fill did not complete within `timeout_ns` — the slot must then be neither
-// reused nor freed (a kernel may still write it).
 // The stamps of a timed region's pack, read from its flag line before the slot's next fill
 // overwrites them (the flag must already show the pack's epoch).
 void harvest_region_stamp(dora_node* n, Slot* s) {
@@ -756,6 +750,12 @@ void harvest_region_stamp(dora_node* n, Slot* s) {
   s->region_cp_area = -1;
 }
 
+// A returned drop token does not prove that the slot's last fill has completed: the daemon
+// returns the token at once for an output without receivers, a receiver's drop-oldest queue
+// releases inputs it never waited on, and a finished receiver's tokens are released for it.
+// Before a slot is refilled or freed, wait for its last fill (normally long complete: one load).
+// False when the fill did not complete within `timeout_ns` — the slot must then be neither
+// reused nor freed (a kernel may still write it).
 bool wait_slot_idle(dora_node* n, Slot* s, uint64_t timeout_ns = 10000000000ull) {
   const uint64_t t0 = mono_ns();
   if (s->flag >= 0 && s->fill_epoch) {
@@ -1135,12 +1135,16 @@ void finish_input(dora_node* n, dora_event* ev) {
     }
     add_fill_wait_ns(mono_ns() - t0);
     if (trace_enabled()) {
-      // the pack's own stamps (s_memrealtime), for the GPU side of a message's latency; the
-      // line may already carry a later fill's stamps if the slot was refilled meanwhile
+      // the pack's own stamps (s_memrealtime), for the GPU side of a message's latency: only an
+      // in-kernel-signalled fill of exactly this epoch writes them (a CP-signalled fill writes
+      // none, and the line may already carry a later fill's stamps if the slot was refilled)
       const FillFlag& ff = h->nodes[d.flag_node].fill[d.flag_index];
-      const double ns_per_tick = 1e9 / kRealtimeHz;
-      trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
-      trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
+      if (ff.epoch.load(std::memory_order_acquire) == d.epoch &&
+          ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) {
+        const double ns_per_tick = 1e9 / kRealtimeHz;
+        trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
+        trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
+      }
     }
   } else if (d.fill == FILL_EVENT) {
     // the producer's fill completes when its interprocess event fires
@@ -1605,7 +1609,7 @@ bool kernel_signal() {
 // completion signal.
 int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
                 ArrowDeviceType dev, hipStream_t st, hipEvent_t t_start, hipEvent_t t_stop,
-                bool signal = true) {
+                bool signal = true, bool sync = false) {
   if (!signal) {
     // the caller orders what follows on `st` (a broadcast-group send): no fill flag
     ++n->hip_packs;
@@ -1634,13 +1638,13 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       int area = -1;
       uint64_t* stamps = nullptr;
       if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas &&
-          aql_cp_candidate(segs, nseg)) {
+          aql_cp_candidate(segs, nseg, /*lone=*/true)) {
         area = int(n->region_cp_next++);
         stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
       }
       s->slot->region_cp_area = area;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap), stamps) == DORA_OK) {
+                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -1885,8 +1889,10 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     }
     // a broadcast-group output packs on the node stream, where its broadcast follows
     const bool bcast = n->bcast_out.count(output_id) > 0;
+    const bool sync = plan->dev == ARROW_DEVICE_ROCM &&
+                      !((flags & DORA_SEND_ASYNC) || n->async_default);
     rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
-                     bcast ? n->core->stream : nullptr, t_start, t_stop, !bcast);
+                     bcast ? n->core->stream : nullptr, t_start, t_stop, !bcast, sync);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
@@ -2637,6 +2643,14 @@ int dora_node_bcast_stats(dora_node* n, uint64_t* groups_out, uint64_t* groups_i
   if (received) *received = n->core->bcast_recvs;
   if (received_bytes) *received_bytes = n->core->bcast_bytes;
   if (error) *error = n->core->bcast_error.c_str();
+  return DORA_OK;
+}
+
+int dora_node_bcast_ranks(dora_node* n, uint64_t* max_ranks) {
+  if (!n || !max_ranks) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *max_ranks = 0;
+  for (const auto& kv : n->bcast_out)
+    *max_ranks = std::max<uint64_t>(*max_ranks, uint64_t(dora::bcast_nranks(kv.second)));
   return DORA_OK;
 }
 

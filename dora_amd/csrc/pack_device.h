@@ -27,7 +27,8 @@ constexpr int kThreads = 256;
 constexpr int kMaxSegs = 32;       // segments of a HIP-launched pack
 constexpr int kMaxAqlSegs = 8;     // segments of an AQL-dispatched pack (smaller kernargs)
 // Workgroups of a signalling pack (r01 sweep, profiles/r01_signal_sweep.jsonl: 1024 beats 512
-// and 2048-4096 at 16-40 MB, flat at 4 MB).
+// and 2048-4096 at 16-40 MB, flat at 4 MB).  Packs signalled by the command processor have no
+// done words to poll and take up to cp_grid() workgroups instead (aql.cpp).
 constexpr uint32_t kSignalGrid = 1024;
 // Chunk windows start on a cache line: a segment's body is cut into chunks from the 128-byte
 // line holding its first aligned unit, so every wave's 1 KiB store covers whole lines (64-byte
@@ -477,12 +478,14 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
       if (args.epoch) {
         // a pack inside a timed region: `epoch` is its stamp area (device memory, zeroed by the
         // host, read once the region's packs have all completed) — [0] the first workgroup's
-        // start, [1 + blk] the time workgroup blk's stores were all complete; written through
+        // start, [1 + blk mod kCpStampWgs] the latest time a workgroup mapping there had all its
+        // stores complete (system-scope atomic max: performed past the L2s, where the host's BAR
+        // read finds it; a grid of any size fits the area)
         uint64_t* st = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(args.epoch));
         __syncthreads();
         if (threadIdx.x == 0) {
-          __hip_atomic_store(st + 1 + blk, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_max(st + 1 + (blk % kCpStampWgs), __builtin_amdgcn_s_memrealtime(),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (blk == 0)
             __hip_atomic_store(st, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

@@ -84,6 +84,9 @@ struct FillSignal {
   uint32_t* done;
 };
 constexpr uint32_t kMaxSignalWgs = 4096;
+// Completion-stamp words of a CP-signalled pack inside a timed region (aql.h): workgroup k
+// raises word 1 + (k mod kCpStampWgs) to its end time (atomic max), so a grid of any size fits.
+constexpr uint32_t kCpStampWgs = 1024;
 
 // One message of a batch pack (aql.cpp): its copy segments, slot, fill signal, writable bytes.
 struct BatchItem {

@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include "aql.h"
+#include "bcast.h"
 #include "shm.h"
 #include "common.h"
 
@@ -123,6 +124,32 @@ int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_ms
 }
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
+
+int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank) {
+  if (!buf || !nranks || !rank) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  DORA_GUARD_BEGIN
+  DORA_HIP(hipSetDevice(device));
+  uint8_t uid[dora::kBcastIdBytes];
+  int rc = dora::bcast_unique_id(uid);
+  if (rc != DORA_OK) return rc;
+  dora::BcastComm* c = nullptr;
+  rc = dora::bcast_join(uid, 1, 0, 30000, &c);
+  if (rc != DORA_OK) return rc;
+  *nranks = dora::bcast_nranks(c);
+  *rank = dora::bcast_rank(c);
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    dora::bcast_close(c, nullptr, 0);
+    return dora::fail(DORA_ERR_HIP, "hipStreamCreate");
+  }
+  rc = dora::bcast_enqueue(c, buf, bytes, st);
+  if (rc == DORA_OK && hipStreamSynchronize(st) != hipSuccess)
+    rc = dora::fail(DORA_ERR_HIP, "broadcast stream: %s", hipGetErrorString(hipGetLastError()));
+  dora::bcast_close(c, st, 10000);
+  (void)hipStreamDestroy(st);
+  return rc;
+  DORA_GUARD_END
+}
 
 int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
                                double* us_per_msg) {

@@ -222,6 +222,8 @@ int main() {
   uint64_t bgroups = 0, bsent = 0;
   const char* berr = "";
   dora_node_bcast_stats(node, &bgroups, nullptr, &bsent, nullptr, nullptr, &berr);
+  uint64_t branks = 0;
+  dora_node_bcast_ranks(node, &branks);
   FILE* f = out_path ? std::fopen(out_path, "w") : stdout;
   const double delivered = double(tp_size) * double(tp_n) * double(acks);
   std::fprintf(f,
@@ -229,13 +231,15 @@ int main() {
                "\"tp_seconds\": %.6f, \"tp_delivered_GBps\": %.3f, \"tp_per_receiver_GBps\": %.3f, "
                "\"send_phase_us\": {\"alloc_us\": %.2f, \"launch_us\": %.2f, \"fill_us\": %.2f, "
                "\"send_us\": %.2f}, \"slots_created\": %llu, \"cache_hits\": %llu, "
-               "\"bcast_groups\": %llu, \"bcast_sent\": %llu, \"bcast_error\": \"%s\", "
+               "\"bcast_groups\": %llu, \"bcast_ranks\": %llu, \"bcast_sent\": %llu, "
+               "\"bcast_error\": \"%s\", "
                "\"tp_busy_us_per_msg\": %.3f, \"aql_batches\": %llu, \"aql_batched_msgs\": %llu}\n",
                errors, ok ? "true" : "false", acks, (unsigned long long)tp_size, tp_n, tp_s,
                tp_s > 0 ? delivered / tp_s / 1e9 : 0.0,
                tp_s > 0 ? double(tp_size) * double(tp_n) / tp_s / 1e9 : 0.0, phase[0], phase[1],
                phase[2], phase[3], (unsigned long long)slots, (unsigned long long)hits,
-               (unsigned long long)bgroups, (unsigned long long)bsent, json_safe(berr).c_str(),
+               (unsigned long long)bgroups, (unsigned long long)branks, (unsigned long long)bsent,
+               json_safe(berr).c_str(),
                tp_n > 0 ? (tp_s * 1e9 - double(idle1 - idle0)) / 1e3 / double(tp_n) : 0.0,
                (unsigned long long)batches, (unsigned long long)batched);
   if (f != stdout) std::fclose(f);

@@ -261,6 +261,11 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch);
 int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
                                double* us_per_msg);
 void dora_gpu_test_bar_free(void* ptr);
+/* Test hook (RCCL path of the fan-out): form a broadcast group of one rank on
+ * `device` (unique id -> join(nranks 1) -> ncclBroadcast of `bytes` at `buf` in place on a fresh
+ * stream -> close), reporting the rank count and rank the communicator holds.  The one-GPU
+ * exercise of bcast_unique_id / bcast_join / bcast_enqueue / bcast_close. */
+int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank);
 /* Test hooks of the inter-daemon wire, bincode of Timestamped<InterDaemonEvent> (replaces
  * bincode::serialize in binaries/daemon/src/inter_daemon.rs:66 and its deserialize at :156;
  * layouts in csrc/bincode.h): an Output event built from this library's type-info and parameter
@@ -429,6 +434,9 @@ int dora_node_peer_stats(dora_node* node, uint64_t* copies, uint64_t* bytes);
 int dora_node_bcast_stats(dora_node* node, uint64_t* groups_out, uint64_t* groups_in,
                           uint64_t* sent, uint64_t* received, uint64_t* received_bytes,
                           const char** error);
+/* Ranks of this node's broadcast groups as RCCL formed them: the largest group's rank count
+ * (producer included; 0 without a group). */
+int dora_node_bcast_ranks(dora_node* node, uint64_t* max_ranks);
 /* Pack-kernel timing: hipExtLaunchKernel start/stop stamps of every n-th pack launch
  * (dora_node_set_timing_period; 0 = DORA_GPU_TIMING_SAMPLE, default 8). */
 int dora_node_set_profiling(dora_node* node, int enable);

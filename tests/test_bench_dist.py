@@ -153,3 +153,30 @@ def test_aql_kernel_name_follows_the_coherent_knob(monkeypatch):
     monkeypatch.setenv("DORA_GPU_PACK_VARIANT", "u8nt")
     monkeypatch.delenv("DORA_GPU_AQL_COHERENT")
     assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u8 (AQL)"
+
+
+def test_compact_line_fits_the_driver_tail():
+    """The stdout line keeps the contract's keys and the north_star summaries (latency p50/p99 at
+    4 KB / 4 MiB / 40.96 MB, sync send, mid-size, C3, drops) within a 2000-character log tail
+    (verdict r03 item 4), from a full r03 line with every ladder filled in."""
+    import json
+    import os
+
+    import bench
+    full = json.load(open(os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                       "r03_final_bench_1.json")))
+    full["sink_dropped_by_phase"] = {"warmup": 0, "latency_ladder": 2, "timed_region": 0}
+    full["sync_send_headline"].update({"hbm_frac_2S": 0.19, "pack_own_us": 17.9,
+                                       "pack_own_frac": 0.57, "gap_us_median": 6.3})
+    c = bench.compact_line(full, os.path.join(bench.ROOT, "gpurun_out", "bench_detail.json"))
+    text = json.dumps(c)
+    assert len(text) < 1900, len(text)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in c, k
+    assert list(c)[-1] == "cpu_baseline"
+    assert set(c["latency_summary"]) == {"4096", "4194304", "40960000"}
+    assert c["roofline"]["frac"] == full["roofline"]["frac"]
+    assert c["sink_dropped"]["by_phase"] == {"latency_ladder": 2}
+    assert c["c3"]["frac"] == full["c3"]["roofline"]["frac"]

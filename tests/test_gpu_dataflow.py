@@ -519,6 +519,32 @@ def test_cross_gpu_bench_runs_on_one_gpu(launcher):
     assert rc["pulls"] > 0
 
 
+@pytest.mark.gpu
+def test_rccl_group_of_one_rank_broadcasts_in_place():
+    """The RCCL fan-out path on one GPU (verdict r03 item 5): a broadcast group of one rank is
+    formed (ncclGetUniqueId -> ncclCommInitRankConfig, non-blocking), one ncclBroadcast runs in
+    place on a stream and the group is closed, all through the C ABI; the buffer's bytes are
+    unchanged (the root's own data) and the communicator reports 1 rank, rank 0."""
+    from ctypes import byref, c_int
+
+    from dora_amd import device
+    from dora_amd._lib import call
+    from dora_amd.workloads import payload_seed
+    size = 6220800  # one C4 frame (1920 x 1080 x 3)
+    s = device.Stream()
+    b = device.DeviceBuffer(size)
+    try:
+        device.fill_splitmix(b.ptr, size, payload_seed(size), s)
+        s.sync()
+        before = device.csum64(b.ptr, size, s)
+        nranks, rank = c_int(-1), c_int(-1)
+        call("dora_gpu_test_bcast_group", 0, b.ptr, size, byref(nranks), byref(rank))
+        assert (nranks.value, rank.value) == (1, 0)
+        assert device.csum64(b.ptr, size, s) == before
+    finally:
+        b.free()
+
+
 def _distinct_sources(n, size):
     """n device buffers with distinct splitmix64 payloads and their checksums."""
     from dora_amd import device

@@ -188,3 +188,49 @@ def test_crashed_peer_daemon_closes_remote_inputs(tmp_path, monkeypatch):
         a.stop()
         b.stop()
     assert "gone; closing its outputs" in b.log("_daemon")
+
+
+def test_oversized_frame_is_refused_per_message(tmp_path, monkeypatch):
+    """A message whose frame exceeds the inter-daemon limit (DORA_GPU_MAX_FRAME_BYTES, lowered
+    here to 2048 B) is refused by the forwarder with an error naming it: the link
+    stays up, so the messages behind it and the InputsClosed still arrive."""
+    monkeypatch.setenv("DORA_GPU_MAX_FRAME_BYTES", "2048")
+    desc = _desc(1)
+    b = Dataflow(desc, machine="B", machines={"B": ("127.0.0.1", 0), "A": ("127.0.0.1", 1)},
+                 dataflow_id="df-big", log_dir=str(tmp_path / "B")).start()
+    a = Dataflow(desc, machine="A",
+                 machines={"A": ("127.0.0.1", 0), "B": ("127.0.0.1", b.listen_port)},
+                 dataflow_id="df-big", log_dir=str(tmp_path / "A")).start()
+    try:
+        box = {}
+        lt = threading.Thread(target=lambda: box.update(local=_open(a, "local")))
+        lt.start()
+        rt = threading.Thread(target=lambda: box.update(dst=_open(b, "dst0")))
+        rt.start()
+        src = _open(a, "src")
+        lt.join(30)
+        rt.join(30)
+        src.send_output("data", b"a" * 100, {"seq": 0})
+        src.send_output("data", b"b" * 3000, {"seq": 1})   # frame > 2048 B: refused
+        src.send_output("data", b"c" * 100, {"seq": 2})
+        src.close()
+        box["local"].close()
+        dst = box["dst"]
+        seqs, closed = [], set()
+        while True:
+            ev = dst.next(timeout=30)
+            if ev is None:
+                break
+            if ev["type"] == "INPUT":
+                seqs.append(ev["metadata"]["seq"])
+            elif ev["type"] == "INPUT_CLOSED":
+                closed.add(ev["id"])
+        dst.close()
+        codes = {"A": a.wait(30), "B": b.wait(30)}
+    finally:
+        a.stop()
+        b.stop()
+    assert seqs == [0, 2] and closed == {"data", "side"}
+    assert codes["A"]["_daemon"] == 0 and codes["B"]["_daemon"] == 0, codes
+    assert "exceeds the inter-daemon frame limit" in a.log("_daemon")
+    assert "refused" not in b.log("_daemon")
