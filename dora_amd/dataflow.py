@@ -101,6 +101,75 @@ def _runtime_node(n: dict, base: str) -> dict:
     return r
 
 
+def dataflow_uuid(dataflow_id: str) -> str:
+    """The dataflow's `DataflowId` (uuid::Uuid): the id itself when it is a UUID, else the
+    name-derived UUID the daemon puts on the inter-daemon wire (csrc/bincode.cpp dataflow_uuid:
+    two FNV-1a-64 passes, version 8 / RFC 4122 variant bits)."""
+    import uuid
+    try:
+        return str(uuid.UUID(dataflow_id)) if len(dataflow_id) == 36 else _fnv_uuid(dataflow_id)
+    except ValueError:
+        return _fnv_uuid(dataflow_id)
+
+
+def _fnv_uuid(name: str) -> str:
+    import uuid
+    m = (1 << 64) - 1
+    h1, h2 = 0xcbf29ce484222325, 0x84222325cbf29ce4
+    for c in name.encode():
+        h1 = ((h1 ^ c) * 0x100000001b3) & m
+        h2 = ((h2 ^ c) * 0x100000001b3) & m
+    u = bytearray(h1.to_bytes(8, "little") + h2.to_bytes(8, "little"))
+    u[6] = (u[6] & 0x0F) | 0x80
+    u[8] = (u[8] & 0x3F) | 0x80
+    return str(uuid.UUID(bytes=bytes(u)))
+
+
+def node_config(nodes: List[NodeSpec], node_id: str, dataflow_id: str, shm: str) -> dict:
+    """The reference's `NodeConfig` (libraries/message/src/daemon_to_node.rs:20-27) of one node,
+    as `dora start` hands it over in DORA_NODE_CONFIG (apis/rust/node/src/node/mod.rs:65-76):
+    the Rust facade's `DoraNode::init_from_env` / `init(NodeConfig)` (integration/rust) read it.
+    `daemon_communication` is the `Shmem` variant naming this data plane's control region (one
+    region carries the control, drop and event channels); the descriptor is restated in the
+    reference's schema (descriptor/mod.rs:25-200) — `_unstable_deploy` keeps `machine` only,
+    since the reference's `Deploy` denies unknown fields; the GPU ordinal travels in
+    DORA_GPU_DEVICE."""
+    def inputs(n):
+        return {k: {"source": f"{src}/{out}", "queue_size": q}
+                for k, (src, out, q) in n.inputs.items()}
+
+    def desc_node(n):
+        d = {"id": n.id, "inputs": inputs(n), "outputs": list(n.outputs)}
+        if n.path != "dynamic":
+            d["path"] = n.path
+            if n.args:
+                d["args"] = " ".join(shlex.quote(a) for a in n.args)
+        else:
+            d["path"] = "dynamic"
+        env = {k: v for k, v in n.env.items() if k != "DORA_GPU_SEND_STDOUT_AS"}
+        if env:
+            d["env"] = env
+        if n.env.get("DORA_GPU_SEND_STDOUT_AS"):
+            d["send_stdout_as"] = n.env["DORA_GPU_SEND_STDOUT_AS"]
+        if n.machine:
+            d["_unstable_deploy"] = {"machine": n.machine}
+        return d
+    me = next(x for x in nodes if x.id == node_id)
+    return {"dataflow_id": dataflow_uuid(dataflow_id), "node_id": node_id,
+            "run_config": {"inputs": inputs(me), "outputs": list(me.outputs)},
+            "daemon_communication": {"Shmem": {"daemon_control_region_id": shm,
+                                               "daemon_drop_region_id": shm,
+                                               "daemon_events_region_id": shm,
+                                               "daemon_events_close_region_id": shm}},
+            "dataflow_descriptor": {"nodes": [desc_node(n) for n in nodes]},
+            "dynamic": me.path == "dynamic"}
+
+
+def node_config_yaml(nodes: List[NodeSpec], node_id: str, dataflow_id: str, shm: str) -> str:
+    import yaml
+    return yaml.safe_dump(node_config(nodes, node_id, dataflow_id, shm), sort_keys=False)
+
+
 def parse_descriptor(desc) -> List[NodeSpec]:
     base = os.getcwd()
     if isinstance(desc, str):
@@ -261,7 +330,9 @@ class Dataflow:
         """Environment a node runs with (set it before Node() for `path: dynamic` nodes)."""
         n = next(x for x in self.nodes if x.id == node_id)
         return {"DORA_GPU_DATAFLOW": self.shm, "DORA_NODE_ID": n.id,
-                "DORA_GPU_DEVICE": str(n.gpu)}
+                "DORA_GPU_DEVICE": str(n.gpu),
+                "DORA_NODE_CONFIG": node_config_yaml(self.all_nodes, n.id, self.dataflow_id,
+                                                     self.shm)}
 
     @staticmethod
     def _ready_port(log: str) -> Optional[int]:

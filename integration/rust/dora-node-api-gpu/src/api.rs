@@ -9,18 +9,24 @@
 //! token returned at once.  A consumer that can use HBM directly takes
 //! `EventStream::recv_device` (zero-copy `DeviceInput`).  `send_output*` return once the sample
 //! no longer needs the caller's data, as the reference's.
-use std::future::Future;
+use std::collections::{BTreeMap, BTreeSet, VecDeque};
 use std::pin::Pin;
-use std::task::{Context, Poll};
+use std::sync::{Arc, Condvar, Mutex};
+use std::task::{Context, Poll, Waker};
+use std::thread::JoinHandle;
 use std::time::{Duration, Instant};
 
 use arrow::array::{make_array, new_empty_array, Array};
 use dora_arrow_convert::ArrowData;
-use dora_core::config::{DataId, NodeId, OperatorId};
+use dora_core::config::{DataId, NodeId, NodeRunConfig, OperatorId};
+use dora_core::descriptor::Descriptor;
 use dora_core::uhlc;
+use dora_message::daemon_to_node::{DaemonCommunication, NodeConfig};
 use dora_message::metadata::{ArrowTypeInfo, Metadata, MetadataParameters};
+use dora_message::DataflowId;
 use dora_gpu_sys as sys;
 use eyre::{bail, Result, WrapErr};
+use futures::Stream;
 
 use crate::check;
 use crate::node::{self, DeviceInput, GpuEvent, GpuNode, SharedNode};
@@ -29,7 +35,10 @@ use crate::node::{self, DeviceInput, GpuEvent, GpuNode, SharedNode};
 pub struct DoraNode {
     inner: GpuNode,
     id: NodeId,
-    clock: std::sync::Arc<uhlc::HLC>,
+    dataflow_id: DataflowId,
+    node_config: NodeRunConfig,
+    dataflow_descriptor: Descriptor,
+    clock: Arc<uhlc::HLC>,
 }
 
 /// A sample from `allocate_data_sample` (mod.rs:303-346, 434-503): host bytes the caller fills
@@ -71,44 +80,105 @@ pub enum Event {
 /// `EventStream` (event_stream/mod.rs:27): receives this node's events.
 pub struct EventStream {
     node: SharedNode,
-    clock: std::sync::Arc<uhlc::HLC>,
+    clock: Arc<uhlc::HLC>,
+    // async readers (`recv_async*`, `Stream`): a thread that waits for events so the task
+    // parks instead of spinning; started on the first async poll
+    pump: Option<Pump>,
+}
+
+/// The GPU ordinal of this node: DORA_GPU_DEVICE, set by the launcher from the descriptor's
+/// `_unstable_deploy.gpu` (default 0).
+fn device_from_env() -> i32 {
+    std::env::var("DORA_GPU_DEVICE").ok().and_then(|d| d.parse().ok()).unwrap_or(0)
 }
 
 impl DoraNode {
-    fn wrap(inner: GpuNode, id: NodeId) -> (Self, EventStream) {
-        let clock = std::sync::Arc::new(uhlc::HLC::default());
-        let events = EventStream { node: inner.shared(), clock: clock.clone() };
-        (DoraNode { inner, id, clock }, events)
+    fn wrap(inner: GpuNode, config: NodeConfig) -> (Self, EventStream) {
+        let clock = Arc::new(uhlc::HLC::default());
+        let events = EventStream { node: inner.shared(), clock: clock.clone(), pump: None };
+        let node = DoraNode {
+            inner,
+            id: config.node_id,
+            dataflow_id: config.dataflow_id,
+            node_config: config.run_config,
+            dataflow_descriptor: config.dataflow_descriptor,
+            clock,
+        };
+        (node, events)
     }
 
-    /// `init_from_env` (mod.rs:65-76).  The launcher of this data plane sets DORA_GPU_DATAFLOW
-    /// (the dataflow's control region), DORA_NODE_ID and DORA_GPU_DEVICE instead of
-    /// DORA_NODE_CONFIG.
+    /// `init_from_env` (mod.rs:65-76): the `NodeConfig` in DORA_NODE_CONFIG, as the reference.
+    /// This data plane's launcher (dora_amd/dataflow.py `node_config`) writes it in the
+    /// reference's schema, naming its control region as the `Shmem` daemon communication.
     pub fn init_from_env() -> Result<(Self, EventStream)> {
-        let id = std::env::var("DORA_NODE_ID")
-            .wrap_err("env variable DORA_NODE_ID must be set. Are you sure you started the dataflow?")?;
-        let inner = GpuNode::init_from_env().wrap_err("failed to init node")?;
-        Ok(Self::wrap(inner, NodeId::from(id)))
+        let node_config: NodeConfig = {
+            let raw = std::env::var("DORA_NODE_CONFIG").wrap_err(
+                "env variable DORA_NODE_CONFIG must be set. Are you sure your using `dora start`?",
+            )?;
+            serde_yaml::from_str(&raw).context("failed to deserialize operator config")?
+        };
+        Self::init(node_config)
     }
 
     /// `init_from_node_id` (mod.rs:87-110): a dynamic node (`path: dynamic`) of the running
-    /// dataflow named by DORA_GPU_DATAFLOW, on DORA_GPU_DEVICE (default 0).
+    /// dataflow.  The reference asks the local daemon for the node's `NodeConfig` over TCP; this
+    /// data plane's launcher hands it over in DORA_NODE_CONFIG for dynamic nodes too
+    /// (`Dataflow.dynamic_env`), and without it the node attaches to the control region named
+    /// by DORA_GPU_DATAFLOW with an empty run config.
     pub fn init_from_node_id(node_id: NodeId) -> Result<(Self, EventStream)> {
+        if let Ok(raw) = std::env::var("DORA_NODE_CONFIG") {
+            let config: NodeConfig =
+                serde_yaml::from_str(&raw).context("failed to deserialize node config")?;
+            if config.node_id == node_id {
+                return Self::init(config);
+            }
+        }
         let dataflow = std::env::var("DORA_GPU_DATAFLOW")
-            .wrap_err("env variable DORA_GPU_DATAFLOW must name the running dataflow")?;
-        let device = std::env::var("DORA_GPU_DEVICE").ok().and_then(|d| d.parse().ok()).unwrap_or(0);
-        let inner = GpuNode::init(&dataflow, node_id.as_ref(), device)
+            .wrap_err("failed to get node config from daemon: DORA_GPU_DATAFLOW is not set")?;
+        let inner = GpuNode::init(&dataflow, node_id.as_ref(), device_from_env())
             .wrap_err_with(|| format!("Could not init node {node_id}"))?;
-        Ok(Self::wrap(inner, node_id))
+        let config = NodeConfig {
+            dataflow_id: DataflowId::nil(),
+            node_id,
+            run_config: NodeRunConfig { inputs: BTreeMap::new(), outputs: BTreeSet::new() },
+            daemon_communication: DaemonCommunication::Shmem {
+                daemon_control_region_id: dataflow.clone(),
+                daemon_drop_region_id: dataflow.clone(),
+                daemon_events_region_id: dataflow.clone(),
+                daemon_events_close_region_id: dataflow,
+            },
+            dataflow_descriptor: serde_yaml::from_str("nodes: []")
+                .context("empty dataflow descriptor")?,
+            dynamic: true,
+        };
+        Ok(Self::wrap(inner, config))
     }
 
     /// `init_flexible` (mod.rs:112-119).
     pub fn init_flexible(node_id: NodeId) -> Result<(Self, EventStream)> {
-        if std::env::var("DORA_NODE_ID").is_ok() {
+        if std::env::var("DORA_NODE_CONFIG").is_ok() {
             Self::init_from_env()
         } else {
             Self::init_from_node_id(node_id)
         }
+    }
+
+    /// `init` (mod.rs:122-156): attach to the dataflow the config names.  This data plane's
+    /// daemon speaks over one shared-memory control region (requests, events and drop tokens
+    /// in rings), named by the `Shmem` variant; the node's GPU is DORA_GPU_DEVICE.
+    pub fn init(node_config: NodeConfig) -> eyre::Result<(Self, EventStream)> {
+        let region = match &node_config.daemon_communication {
+            DaemonCommunication::Shmem { daemon_control_region_id, .. } => {
+                daemon_control_region_id.clone()
+            }
+            _ => bail!(
+                "the device data plane's daemon is reached through a shared-memory control \
+                 region (DaemonCommunication::Shmem)"
+            ),
+        };
+        let inner = GpuNode::init(&region, node_config.node_id.as_ref(), device_from_env())
+            .wrap_err("failed to init event stream")?;
+        Ok(Self::wrap(inner, node_config))
     }
 
     /// `send_output_raw` (mod.rs:180-196).
@@ -211,6 +281,21 @@ impl DoraNode {
         &self.id
     }
 
+    /// `dataflow_id` (mod.rs:295).
+    pub fn dataflow_id(&self) -> &DataflowId {
+        &self.dataflow_id
+    }
+
+    /// `node_config` (mod.rs:299): this node's inputs and outputs.
+    pub fn node_config(&self) -> &NodeRunConfig {
+        &self.node_config
+    }
+
+    /// `dataflow_descriptor` (mod.rs:376): the descriptor of the dataflow this node is part of.
+    pub fn dataflow_descriptor(&self) -> &Descriptor {
+        &self.dataflow_descriptor
+    }
+
     /// `allocate_data_sample` (mod.rs:303): host bytes, uploaded by `send_output_sample`.
     pub fn allocate_data_sample(&mut self, data_len: usize) -> Result<DataSample> {
         Ok(DataSample { buf: vec![0u8; data_len] })
@@ -260,6 +345,13 @@ impl EventStream {
         node::next_event(&self.node, slice.as_micros() as i64).map_err(|_| ())
     }
 
+    /// The next device event for an async reader: one queued by the pump, else the waker is
+    /// registered and the pump asked for an event (woken also at `deadline`).
+    fn poll_device(&mut self, cx: &Context<'_>, deadline: Option<Instant>) -> Poll<Option<GpuEvent>> {
+        let node = self.node.clone();
+        self.pump.get_or_insert_with(|| Pump::start(node)).poll(cx.waker(), deadline)
+    }
+
     /// `recv` (event_stream/mod.rs:121-124): the next event, None at the end of the stream.
     pub fn recv(&mut self) -> Option<Event> {
         self.recv_device().map(|e| self.convert(e))
@@ -274,32 +366,33 @@ impl EventStream {
         }
     }
 
-    /// `recv_async` (event_stream/mod.rs:130-132).
+    /// `recv_async` (event_stream/mod.rs:130-132): parks the task until an event arrives (the
+    /// pump thread waits for it and wakes the task), as the reference's awaited channel.
     pub async fn recv_async(&mut self) -> Option<Event> {
-        loop {
-            match self.poll(Duration::ZERO) {
-                Ok(e) => return e.map(|e| self.convert(e)),
-                Err(()) => YieldNow(false).await,
-            }
-        }
+        let e = futures::future::poll_fn(|cx| self.poll_device(cx, None)).await;
+        e.map(|e| self.convert(e))
     }
 
     /// `recv_async_timeout` (event_stream/mod.rs:134-147).
     pub async fn recv_async_timeout(&mut self, dur: Duration) -> Option<Event> {
-        let t0 = Instant::now();
-        loop {
-            match self.poll(Duration::ZERO) {
-                Ok(e) => return e.map(|e| self.convert(e)),
-                Err(()) if t0.elapsed() >= dur => {
-                    return Some(Event::Error("Receiver timed out".to_string()))
-                }
-                Err(()) => YieldNow(false).await,
-            }
+        let deadline = Instant::now() + dur;
+        let e = futures::future::poll_fn(|cx| match self.poll_device(cx, Some(deadline)) {
+            Poll::Ready(e) => Poll::Ready(Ok(e)),
+            Poll::Pending if Instant::now() >= deadline => Poll::Ready(Err(())),
+            Poll::Pending => Poll::Pending,
+        })
+        .await;
+        match e {
+            Ok(e) => e.map(|e| self.convert(e)),
+            Err(()) => Some(Event::Error("Receiver timed out".to_string())),
         }
     }
 
     /// Extension: the next event with its input left in HBM (zero-copy `DeviceInput`).
     pub fn recv_device(&mut self) -> Option<GpuEvent> {
+        if let Some(p) = &self.pump {
+            return p.wait(None).unwrap_or(None);  // keeps the order of events the pump holds
+        }
         loop {
             if let Ok(e) = self.poll(Duration::from_millis(1)) {
                 return e;
@@ -310,6 +403,9 @@ impl EventStream {
     /// Extension: `recv_device` bounded by `dur` (Err on a timeout).
     pub fn recv_device_timeout(&mut self, dur: Duration) -> Result<Option<GpuEvent>, ()> {
         let t0 = Instant::now();
+        if let Some(p) = &self.pump {
+            return p.wait(Some(t0 + dur));
+        }
         loop {
             let left = dur.saturating_sub(t0.elapsed());
             match self.poll(left.min(Duration::from_millis(1))) {
@@ -317,6 +413,145 @@ impl EventStream {
                 Err(()) if t0.elapsed() >= dur => return Err(()),
                 Err(()) => {}
             }
+        }
+    }
+}
+
+/// `impl Stream for EventStream` (event_stream/mod.rs:201-214): `while let Some(event) =
+/// events.next().await` works as with the reference.
+impl Stream for EventStream {
+    type Item = Event;
+
+    fn poll_next(mut self: Pin<&mut Self>, cx: &mut Context<'_>) -> Poll<Option<Self::Item>> {
+        let this = &mut *self;
+        match this.poll_device(cx, None) {
+            Poll::Ready(e) => Poll::Ready(e.map(|e| this.convert(e))),
+            Poll::Pending => Poll::Pending,
+        }
+    }
+}
+
+impl Drop for EventStream {
+    fn drop(&mut self) {
+        if let Some(p) = self.pump.take() {
+            p.stop();
+        }
+    }
+}
+
+/// Events fetched by the pump thread for async readers, and the reader it wakes.
+#[derive(Default)]
+struct PumpState {
+    events: VecDeque<GpuEvent>,
+    ended: bool,              // the stream ended (None was returned)
+    wanted: bool,             // a reader waits: fetch an event
+    waker: Option<Waker>,
+    deadline: Option<Instant>, // wake the reader then even without an event (recv_async_timeout)
+    stop: bool,
+}
+
+/// A thread that calls `dora_node_next_event` in 1 ms slices (the node's lock is free between
+/// them, so sends on other threads proceed) while a reader wants an event, queues what it gets
+/// and wakes the reader's task; it sleeps on a condition variable otherwise.  This replaces the
+/// reference's event-stream thread + flume channel (event_stream/thread.rs) for async readers.
+struct Pump {
+    state: Arc<(Mutex<PumpState>, Condvar)>,
+    thread: Option<JoinHandle<()>>,
+}
+
+impl Pump {
+    fn start(node: SharedNode) -> Pump {
+        let state = Arc::new((Mutex::new(PumpState::default()), Condvar::new()));
+        let st = state.clone();
+        let thread = std::thread::Builder::new()
+            .name("dora-event-pump".into())
+            .spawn(move || {
+                let (m, cv) = &*st;
+                loop {
+                    {
+                        let mut g = m.lock().unwrap();
+                        while !g.stop && (!g.wanted || !g.events.is_empty() || g.ended) {
+                            g = cv.wait(g).unwrap();
+                        }
+                        if g.stop {
+                            return;
+                        }
+                    }
+                    let got = node::next_event(&node, 1000);
+                    let mut g = m.lock().unwrap();
+                    match got {
+                        Ok(Some(e)) => g.events.push_back(e),
+                        Ok(None) => g.ended = true,
+                        Err(_) => {
+                            // no event in this slice: only a passed deadline wakes the reader
+                            if !g.deadline.map_or(false, |d| Instant::now() >= d) {
+                                continue;
+                            }
+                            g.deadline = None;
+                        }
+                    }
+                    g.wanted = false;
+                    if let Some(w) = g.waker.take() {
+                        w.wake();
+                    }
+                    cv.notify_all();
+                }
+            })
+            .expect("failed to spawn the event pump thread");
+        Pump { state, thread: Some(thread) }
+    }
+
+    fn poll(&self, waker: &Waker, deadline: Option<Instant>) -> Poll<Option<GpuEvent>> {
+        let (m, cv) = &*self.state;
+        let mut g = m.lock().unwrap();
+        if let Some(e) = g.events.pop_front() {
+            return Poll::Ready(Some(e));
+        }
+        if g.ended {
+            return Poll::Ready(None);
+        }
+        g.waker = Some(waker.clone());
+        g.deadline = deadline;
+        g.wanted = true;
+        cv.notify_all();
+        Poll::Pending
+    }
+
+    /// A blocking read through the pump (a synchronous `recv` after async ones): Err at
+    /// `deadline`.
+    fn wait(&self, deadline: Option<Instant>) -> Result<Option<GpuEvent>, ()> {
+        let (m, cv) = &*self.state;
+        let mut g = m.lock().unwrap();
+        loop {
+            if let Some(e) = g.events.pop_front() {
+                return Ok(Some(e));
+            }
+            if g.ended {
+                return Ok(None);
+            }
+            g.wanted = true;
+            cv.notify_all();
+            g = match deadline {
+                None => cv.wait(g).unwrap(),
+                Some(d) => {
+                    let now = Instant::now();
+                    if now >= d {
+                        return Err(());
+                    }
+                    cv.wait_timeout(g, d - now).unwrap().0
+                }
+            };
+        }
+    }
+
+    fn stop(mut self) {
+        {
+            let (m, cv) = &*self.state;
+            m.lock().unwrap().stop = true;
+            cv.notify_all();
+        }
+        if let Some(t) = self.thread.take() {
+            let _ = t.join();
         }
     }
 }
@@ -334,17 +569,3 @@ fn host_input(data: &DeviceInput) -> Result<(ArrowTypeInfo, arrow::array::ArrayR
     Ok((type_info, array))
 }
 
-/// Yield once to the executor (the C event call above never blocks in async mode).
-struct YieldNow(bool);
-
-impl Future for YieldNow {
-    type Output = ();
-    fn poll(mut self: Pin<&mut Self>, cx: &mut Context<'_>) -> Poll<()> {
-        if self.0 {
-            return Poll::Ready(());
-        }
-        self.0 = true;
-        cx.waker().wake_by_ref();
-        Poll::Pending
-    }
-}

@@ -453,9 +453,22 @@ impl GpuNode {
     }
 
     /// EventStream::recv / recv_timeout (event_stream/mod.rs:121-140) with device-resident
-    /// inputs; None once the stream ended or on a timeout.
+    /// inputs; None once the stream ended or on a timeout.  Waits in 1 ms slices, releasing the
+    /// node's lock between them: a `DeviceInput` dropped on another thread (its drop token)
+    /// or a send there never waits for the next event to arrive.
     pub fn recv(&mut self, timeout: Option<Duration>) -> Option<GpuEvent> {
-        let t = timeout.map(|d| d.as_micros() as i64).unwrap_or(-1);
-        next_event(&self.node, t).ok().flatten()
+        let t0 = std::time::Instant::now();
+        let slice = Duration::from_millis(1);
+        loop {
+            let wait = match timeout {
+                None => slice,
+                Some(d) => d.saturating_sub(t0.elapsed()).min(slice),
+            };
+            match next_event(&self.node, wait.as_micros() as i64) {
+                Ok(e) => return e,
+                Err(_) if timeout.map_or(false, |d| t0.elapsed() >= d) => return None,
+                Err(_) => {}
+            }
+        }
     }
 }

@@ -165,3 +165,46 @@ def test_busy_stats_count_blocked_time():
         pass
     dst.close()
     d.join()
+
+
+def test_node_config_in_the_reference_schema():
+    """DORA_NODE_CONFIG (the Rust facade's init_from_env / init(NodeConfig)) is the reference's
+    NodeConfig (libraries/message/src/daemon_to_node.rs:20-27): run_config inputs/outputs, the
+    Shmem daemon communication naming the control region, a descriptor whose nodes carry only
+    fields the reference's `Node` accepts (descriptor/mod.rs:164-200, deny_unknown_fields;
+    `_unstable_deploy` with `machine` only), and the dataflow UUID the daemon's wire uses."""
+    import uuid
+
+    import yaml
+
+    from dora_amd.dataflow import Dataflow, dataflow_uuid, node_config_yaml, parse_descriptor
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["data"], "_unstable_deploy": {"gpu": 1}},
+        {"id": "dst", "path": "/bin/true", "args": "-x 'a b'", "env": {"K": 3},
+         "inputs": {"in": {"source": "src/data", "queue_size": 4}, "in2": "src/data"},
+         "outputs": ["o"], "_unstable_deploy": {"machine": "B", "gpu": 2}}]}
+    nodes = parse_descriptor(desc)
+    c = yaml.safe_load(node_config_yaml(nodes, "dst", "df-test", "/dora-gpu-x"))
+    assert set(c) == {"dataflow_id", "node_id", "run_config", "daemon_communication",
+                      "dataflow_descriptor", "dynamic"}
+    assert c["dataflow_id"] == dataflow_uuid("df-test") and uuid.UUID(c["dataflow_id"])
+    assert c["node_id"] == "dst" and c["dynamic"] is False
+    assert c["run_config"] == {"inputs": {"in": {"source": "src/data", "queue_size": 4},
+                                          "in2": {"source": "src/data", "queue_size": 10}},
+                               "outputs": ["o"]}
+    assert c["daemon_communication"] == {"Shmem": {k: "/dora-gpu-x" for k in (
+        "daemon_control_region_id", "daemon_drop_region_id", "daemon_events_region_id",
+        "daemon_events_close_region_id")}}
+    allowed = {"id", "name", "description", "env", "_unstable_deploy", "operators", "custom",
+               "operator", "path", "args", "build", "send_stdout_as", "inputs", "outputs"}
+    for n in c["dataflow_descriptor"]["nodes"]:
+        assert set(n) <= allowed, n
+        assert set(n.get("_unstable_deploy", {})) <= {"machine"}
+    dst = c["dataflow_descriptor"]["nodes"][1]
+    assert dst["args"] == "-x 'a b'" and dst["env"] == {"K": "3"}
+    assert dst["_unstable_deploy"] == {"machine": "B"}
+    # a UUID id is kept as it is; every node the launcher starts gets its config
+    u = str(uuid.uuid4())
+    assert dataflow_uuid(u) == u
+    df = Dataflow(desc, machine=None)
+    assert yaml.safe_load(df.dynamic_env("src")["DORA_NODE_CONFIG"])["dynamic"] is True
