@@ -63,6 +63,7 @@ constexpr uint32_t kProfilePrealloc = 2048;  // created when profiling is first 
 struct Use {
   const std::atomic<uint64_t>* flag = nullptr;
   uint64_t epoch = 0;
+  uint64_t seq = 0;  // the dispatch's number (AqlQueue::next when it was written)
 };
 
 constexpr size_t kMaxItemSegs = 8;   // segments of one message the AQL path takes
@@ -422,6 +423,8 @@ AqlQueue* aql_queue(int device) {
   return (q && !q->failed.load()) ? q : nullptr;
 }
 
+bool aql_usable(const AqlQueue* q) { return q && !q->failed.load(std::memory_order_relaxed); }
+
 size_t aql_max_segments() { return 8; }
 
 namespace {
@@ -553,6 +556,14 @@ uint64_t barrier_bytes() {
   return v;
 }
 
+// The number of the oldest dispatch still in an outstanding list (a->next when none is).
+uint64_t oldest_outstanding(const AqlQueue* a) {
+  uint64_t m = a->next;
+  for (int i = 0; i < a->nq; ++i)
+    if (!a->outq[i].empty()) m = std::min(m, a->outq[i].front().seq);
+  return m;
+}
+
 // Write and ring one packet on queue `qi` (a->mu held): one message with the single- or
 // multi-segment kernels, or a batch of `n` > 1 messages with dora_aql_packb_u4.
 int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big) {
@@ -561,10 +572,13 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   uint8_t* const dst = it0.dst;
   const FillSignal& sig = it0.sig;
   const bool profile = std::any_of(items, items + n, [](const Pending& x) { return x.profile; });
-  // the argument slot of the dispatch kRingSlots back must have completed
+  // the argument slot of the dispatch kRingSlots back must have completed.  Every dispatch
+  // sits in its queue's outstanding list until seen complete (prune) and the lists hold
+  // dispatches in order, so one older than every list's front is complete: no load of its flag
+  // line (which the GPU has written since: a cache miss per send)
   const uint64_t r = a->next % kRingSlots;
   Use& u = a->uses[r];
-  if (u.flag && !fill_reached(u.flag, u.epoch)) {
+  if (u.flag && u.seq >= oldest_outstanding(a) && !fill_reached(u.flag, u.epoch)) {
     const auto t0 = std::chrono::steady_clock::now();
     while (!fill_reached(u.flag, u.epoch)) {
       __builtin_ia32_pause();
@@ -731,6 +745,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // every message of a batch signals at its end: the last one's flag stands for the packet
   u.flag = items[n - 1].flag_host;
   u.epoch = items[n - 1].sig.epoch;
+  u.seq = a->next;
   a->outq[qi].push_back(u);
   ++a->next;
   ++a->dispatched[k];
@@ -791,22 +806,20 @@ bool queues_idle(AqlQueue* a) {
   return true;
 }
 
-// The queue with the fewest outstanding packets below the depth (ties: round robin) among the
-// first `nq` (0: all), or -1.
+// The first queue in round-robin order, among the first `nq` (0: all), with fewer than `depth`
+// outstanding packets, or -1.  An idle queue is taken without loading anything; a busy one is
+// pruned first (one load of its oldest packet's flag line, which the GPU has written since: a
+// cache miss), and only as far as needed — r03 pruned all four queues on every send.
 int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
   if (a->hold) return -1;
   if (nq <= 0 || nq > a->nq) nq = a->nq;
-  int best = -1;
-  size_t best_n = depth ? depth : queue_depth();
+  const size_t d = depth ? depth : queue_depth();
   for (int j = 0; j < nq; ++j) {
     const int i = int((a->next + uint64_t(j)) % uint64_t(nq));
-    prune(a, i);
-    if (a->outq[i].size() < best_n) {
-      best = i;
-      best_n = a->outq[i].size();
-    }
+    if (a->outq[i].size() >= d) prune(a, i);
+    if (a->outq[i].size() < d) return i;
   }
-  return best;
+  return -1;
 }
 
 // Bytes a batch may carry (DORA_GPU_AQL_BATCH_BYTES, default the barrier size), and the size from

@@ -23,6 +23,9 @@ struct AqlQueue;
 // The process's AQL queue for HIP device `device`, created on first use; nullptr when HSA or
 // the code object cannot be set up (callers then launch through HIP).  DORA_GPU_AQL=0 disables.
 AqlQueue* aql_queue(int device);
+// A queue aql_queue returned is still usable (not marked failed): callers may keep the pointer
+// (queues are never freed) instead of looking it up under the global lock on every send.
+bool aql_usable(const AqlQueue* q);
 
 // Dispatch one signalling pack of `n` (<= 8) device-source copy segments into `dst`; the launch
 // stores `sig.epoch` into `sig.flag` when the sample is complete.  `flag_host` is the host view
@@ -37,7 +40,7 @@ AqlQueue* aql_queue(int device);
 // `sync`: the caller waits for this pack before it does anything else (a synchronous send,
 // node.cpp wait_source_read).  A single-segment pack that is sent synchronously, or that finds
 // every queue idle, runs alone on the GPU: it is signalled by the command processor at any size
-// >= the CP window's lower bound, with a grid of up to cp_grid() workgroups (no done words to
+// >= the CP window's lower bound, with a grid of up to DORA_GPU_CP_GRID workgroups (no done words to
 // poll, so no 1024-workgroup signalling cap).
 // Would a pack of these segments be signalled by the command processor when sent alone
 // (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI; `lone`: also a lone big pack)?

@@ -395,6 +395,8 @@ struct NodeCore {
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
   uint32_t* fill_done = nullptr;  // device: per fill flag, kMaxSignalWgs workgroup done words
+  dora::AqlQueue* aql = nullptr;  // this process's AQL queues of `device` (fill_sample)
+  bool aql_tried = false;
   std::vector<uint32_t> free_flags;
   uint64_t epoch = 0;
 
@@ -1632,7 +1634,11 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
         return hipStreamQuery(n->core->stream) != hipErrorNotReady;
       }()) {
     // host-bound size: one raw AQL packet instead of hipLaunchKernel (aql.h)
-    if (AqlQueue* q = aql_queue(n->core->device)) {
+    if (!n->core->aql_tried) {  // looked up once (a global lock), then kept
+      n->core->aql_tried = true;
+      n->core->aql = aql_queue(n->core->device);
+    }
+    if (AqlQueue* q = aql_usable(n->core->aql) ? n->core->aql : nullptr) {
       const std::atomic<uint64_t>* fh = n->core->flag_host(s->slot->flag);
       // a timed region's pack may be signalled by the command processor if it has a stamp area
       int area = -1;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Verdict r03 item 2 (C3 burst): the bench's C3 block (200-send steady region + 20-send burst)
+# under dispatch variants, interleaved.  usage: bash scripts/c3_ab.sh <out dir> [rounds]
+set -euo pipefail
+out=${1:?out dir}; rounds=${2:-2}
+mkdir -p "$out"
+export TMPDIR=/tmp
+run() {  # name, env...
+  local name=$1; shift
+  env "$@" timeout -k 10 120 python -u scripts/c3_burst_probe.py --reps 2 \
+    > "$out/$name.jsonl" 2> "$out/$name.err"
+  sed "s/^{/{\"run\": \"$name\", /" "$out/$name.jsonl" >> "$out/summary.jsonl"
+}
+for r in $(seq 1 "$rounds"); do
+  run "r${r}_default"
+  run "r${r}_cpmulti" DORA_GPU_AQL_CP_MULTI=1
+  run "r${r}_grid2048" DORA_GPU_SIGNAL_GRID=2048
+  run "r${r}_cpmulti_sub" DORA_GPU_AQL_CP_MULTI=1 DORA_GPU_SUBPHASES=1
+done
+echo done

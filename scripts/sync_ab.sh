@@ -25,5 +25,7 @@ for r in $(seq 1 "$rounds"); do
   run "r${r}_grid4096" DORA_GPU_CP_GRID=4096
   run "r${r}_grid2048" DORA_GPU_CP_GRID=2048
   run "r${r}_cpbig" DORA_GPU_AQL_CP_BIG=1
+  run "r${r}_chunk16k" DORA_GPU_PACK_CHUNK=16384
+  run "r${r}_u8" DORA_GPU_PACK_VARIANT=u8
 done
 echo done
