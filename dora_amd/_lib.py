@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t,
-                    c_uint8, c_uint64, c_void_p)
+                    c_uint8, c_uint32, c_uint64, c_void_p)
 
 from .arrow_c import ArrowArray, ArrowSchema
 
@@ -110,6 +110,8 @@ _SIGS = {
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
     "dora_gpu_test_bcast_group": (c_int, [c_int, c_void_p, c_uint64, POINTER(c_int),
                                           POINTER(c_int)]),
+    "dora_gpu_test_l1_stale": (c_int, [c_int, c_int, POINTER(c_uint32), POINTER(c_uint32),
+                                       POINTER(c_uint32)]),
     "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
                                            POINTER(ctypes.c_double)]),
     "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "aql.h"
 #include "common.h"
 #include "pack_device.h"
 #include "plan.h"
@@ -246,6 +247,42 @@ __global__ __launch_bounds__(kThreads) void l2_touch_kernel(const uint8_t* __res
     x ^= w[0] ^ w[1] ^ w[2] ^ w[3];
   }
   if (x == 0x5EEDF00Du && n == 1) sink[blockIdx.x] = x;
+}
+
+// Test tool (the fence probe's failing control, tests/test_gpu_fence.py): can a CU's cache hand
+// a wave stale source bytes inside ONE dispatch?  One 64-lane workgroup per CU reads 64 words of
+// `src` (coarse-grained device memory the host then rewrites through the BAR) into `first`,
+// reports its arrival on a host counter, waits (bounded) for the host's `go` — given after the
+// rewrite — and reads the same words again into `second`.  `mode` picks the loads: 0 plain
+// (L1-cached), 1 non-temporal (the pack's default loads), 2 agent-coherent sc1 (the coherent
+// pack's).  A plain load served by the CU's L1 returns the old words; a load that bypasses L1
+// cannot.  The arrival counter is a vector atomic, the poll a system-scope load; every wave
+// leaves after at most ~2^22 sleeps, so a host that never answers cannot hang the device.
+template <int MODE>
+__device__ __forceinline__ uint32_t probe_load(const uint32_t* p) {
+  if constexpr (MODE == 0) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  if constexpr (MODE == 1) return __builtin_nontemporal_load(p);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void l1_stale_kernel(const uint32_t* src, uint32_t* first,
+                                                      uint32_t* second, uint32_t* arrived,
+                                                      const uint32_t* go) {
+  const uint32_t t = threadIdx.x, b = blockIdx.x;
+  asm volatile("" ::: "memory");
+  first[b * 64 + t] = probe_load<MODE>(src + t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (t == 0) {
+    __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t i = 0; i < (1u << 22); ++i) {
+      if (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  asm volatile("" ::: "memory");
+  second[b * 64 + t] = probe_load<MODE>(src + t);
 }
 
 unsigned grid_for(uint64_t items) {
@@ -619,6 +656,81 @@ int launch_l2_touch(const void* p, size_t len, hipStream_t stream) {
   return DORA_OK;
 }
 
+// One run of l1_stale_kernel (see there): `src` holds 64 words of pattern A, the host rewrites
+// them to pattern B once every workgroup has read them.  Out: workgroups whose first read was
+// not A (setup failures), whose second read still held A words (stale), and the workgroups.
+int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks) {
+  *bad_first = *stale = *blocks = 0;
+  DORA_HIP(hipSetDevice(device));
+  int cus = 0;
+  DORA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  const uint32_t nb = uint32_t(std::max(cus, 1));
+  void* bar = nullptr;
+  int rc = bar_alloc(device, 4096, &bar);
+  if (rc != DORA_OK) return rc;
+  uint32_t A[64], B[64];
+  for (uint32_t i = 0; i < 64; ++i) {
+    A[i] = 0xA0000000u | i;
+    B[i] = 0xB0000000u | i;
+  }
+  uint32_t *first = nullptr, *second = nullptr, *ctl = nullptr;
+  auto cleanup = [&] {
+    if (first) (void)hipFree(first);
+    if (second) (void)hipFree(second);
+    if (ctl) (void)hipHostFree(ctl);
+    bar_free(bar);
+  };
+  if (bar_write(device, bar, A, sizeof(A)) != DORA_OK ||
+      hipMalloc(&first, size_t(nb) * 256) != hipSuccess ||
+      hipMalloc(&second, size_t(nb) * 256) != hipSuccess ||
+      hipHostMalloc(&ctl, 128, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    cleanup();
+    return fail(DORA_ERR_HIP, "l1 stale probe: setup");
+  }
+  volatile uint32_t* arrived = ctl;
+  volatile uint32_t* go = ctl + 16;  // its own cache line
+  *arrived = 0;
+  *go = 0;
+  uint32_t *d_arr = nullptr, *d_go = nullptr;
+  (void)hipHostGetDevicePointer(reinterpret_cast<void**>(&d_arr), ctl, 0);
+  d_go = d_arr + 16;
+  hipStream_t st = nullptr;
+  DORA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  auto kern = mode == 0 ? l1_stale_kernel<0> : mode == 1 ? l1_stale_kernel<1> : l1_stale_kernel<2>;
+  hipLaunchKernelGGL(kern, dim3(nb), dim3(64), 0, st, static_cast<const uint32_t*>(bar), first,
+                     second, d_arr, d_go);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    // every workgroup has read A (bounded: a workgroup that never got a CU is just not counted)
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*arrived < nb && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+    }
+    (void)bar_write(device, bar, B, sizeof(B));
+    __atomic_store_n(const_cast<uint32_t*>(go), 1u, __ATOMIC_SEQ_CST);
+    e = hipStreamSynchronize(st);
+  }
+  (void)hipStreamDestroy(st);
+  if (e != hipSuccess) {
+    cleanup();
+    return fail(DORA_ERR_HIP, "l1 stale probe: %s", hipGetErrorString(e));
+  }
+  std::vector<uint32_t> f(size_t(nb) * 64), g(size_t(nb) * 64);
+  DORA_HIP(hipMemcpy(f.data(), first, f.size() * 4, hipMemcpyDeviceToHost));
+  DORA_HIP(hipMemcpy(g.data(), second, g.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t b = 0; b < nb; ++b) {
+    bool bf = false, bs = false;
+    for (uint32_t i = 0; i < 64; ++i) {
+      bf |= f[b * 64 + i] != A[i];
+      bs |= g[b * 64 + i] == A[i];
+    }
+    *bad_first += bf;
+    *stale += bs;
+  }
+  *blocks = nb;
+  cleanup();
+  return DORA_OK;
+}
+
 int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
   if (!len) return DORA_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
@@ -723,6 +835,15 @@ int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint
 int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream) {
   if (!data && len) return dora::fail(DORA_ERR_INVALID, "data is NULL");
   return dora::launch_l2_touch(data, len, static_cast<hipStream_t>(stream));
+}
+
+int dora_gpu_test_l1_stale(int device, int mode, uint32_t* bad_first, uint32_t* stale,
+                           uint32_t* blocks) {
+  if (!bad_first || !stale || !blocks || mode < 0 || mode > 2)
+    return dora::fail(DORA_ERR_INVALID, "bad l1 stale probe arguments");
+  DORA_GUARD_BEGIN
+  return dora::l1_stale_probe(device, mode, bad_first, stale, blocks);
+  DORA_GUARD_END
 }
 
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream) {

@@ -266,6 +266,13 @@ void dora_gpu_test_bar_free(void* ptr);
  * stream -> close), reporting the rank count and rank the communicator holds.  The one-GPU
  * exercise of bcast_unique_id / bcast_join / bcast_enqueue / bcast_close. */
 int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank);
+/* Test tool (the fence probe's failing control): one 64-lane workgroup per CU reads 64 words of
+ * BAR-written device memory, the host rewrites them through the BAR, and the same waves read
+ * them again within the same dispatch; `mode` 0 plain (L1-cached) loads, 1 non-temporal, 2
+ * agent-coherent (sc1).  Workgroups whose first read was wrong, whose second read was stale,
+ * and the workgroups launched. */
+int dora_gpu_test_l1_stale(int device, int mode, uint32_t* bad_first, uint32_t* stale,
+                           uint32_t* blocks);
 /* Test hooks of the inter-daemon wire, bincode of Timestamped<InterDaemonEvent> (replaces
  * bincode::serialize in binaries/daemon/src/inter_daemon.rs:66 and its deserialize at :156;
  * layouts in csrc/bincode.h): an Output event built from this library's type-info and parameter

@@ -68,3 +68,24 @@ def test_acquire_fence_negative_control_and_coherent_loads():
             assert r["mismatched"] == 0, r   # every shipped configuration is bit-exact
     stale = {e: res[("plain_no_fence", e)]["mismatched"] for e in ENGINES}
     print(f"negative control (L1-cached loads, no acquire fence): stale trials {stale}")
+
+
+def test_in_dispatch_stale_read_control():
+    """The control that can fail (verdict r03 weak 6): inside ONE dispatch, a wave reads 64 words
+    of BAR-written device memory, the host rewrites them through the BAR, and the wave reads them
+    again (dora_gpu_test_l1_stale; one workgroup per CU).  Plain loads may be served the old
+    words by the CU's L1 — the hazard an acquire guards against — while the pack's loads
+    (non-temporal, mode 1; agent-coherent sc1, mode 2) bypass L1 and must see the new words."""
+    from ctypes import byref, c_uint32
+
+    from dora_amd._lib import call
+    out = {}
+    for mode in (0, 1, 2):
+        bad, stale, blocks = c_uint32(), c_uint32(), c_uint32()
+        call("dora_gpu_test_l1_stale", 0, mode, byref(bad), byref(stale), byref(blocks))
+        out[mode] = (bad.value, stale.value, blocks.value)
+    print(f"in-dispatch reread after a BAR rewrite, (bad first read, stale, workgroups) by "
+          f"load: plain {out[0]}, nt {out[1]}, sc1 {out[2]}")
+    for mode, (bad, stale, blocks) in out.items():
+        assert blocks > 0 and bad == 0, (mode, out)
+    assert out[1][1] == 0 and out[2][1] == 0, out
