@@ -565,6 +565,26 @@ uint64_t signal_grid_cap(const FillSignal& sig) {
   return g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
 }
 
+// DORA_GPU_BALANCED_CHUNKS=1: when a pack has more chunks than workgroups (a C3 cloud: 1,587
+// chunks of 8 KiB over 1,024 workgroups, so 563 workgroups copy two chunks and the rest one),
+// the chunk grows in whole lines until every workgroup copies at most one (13 MB: ~12.5 KiB
+// each, 4 loads in flight per lane over ~1 pass).  `count(c)` = the pack's chunks at size c.
+bool balanced_chunks() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_BALANCED_CHUNKS");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
+template <class F>
+uint32_t balance_chunk(uint32_t chunk, uint64_t body, uint64_t grid_cap, F count) {
+  if (!balanced_chunks() || count(chunk) <= grid_cap) return chunk;
+  uint64_t c = ((body + grid_cap - 1) / grid_cap + kLine - 1) / kLine * kLine;
+  for (int i = 0; i < 64 && count(c) > grid_cap; ++i) c += kLine * uint64_t(i + 1);
+  return c <= (uint64_t(1) << 30) && count(c) <= grid_cap ? uint32_t(c) : chunk;
+}
+
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
@@ -583,8 +603,14 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   Variant var = pack_variant();
   if (var.unroll == 0) var.unroll = default_unroll(body);
   a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
-  uint64_t chunks = 0;
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  a.chunk_bytes = balance_chunk(a.chunk_bytes, body, signal_grid_cap(sig), [&](uint64_t c) {
+    uint64_t t = 0;
+    for (size_t k = 0; k < n; ++k)
+      t += segment_chunks(base, segs[k].dst_off, segs[k].len, c, line_chunks());
+    return t;
+  });
+  uint64_t chunks = 0;
   for (size_t k = 0; k < n; ++k) {
     const Segment& s = segs[k];
     a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
@@ -615,9 +641,11 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
                 (unsigned long long)sg.dst_off);
   Variant var = pack_variant();
   if (var.unroll == 0) var.unroll = default_unroll(sg.len);
-  const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, var.unroll);
-  const uint64_t chunks =
-      segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, sg.len, chunk_bytes);
+  const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  const uint32_t chunk_bytes =
+      balance_chunk(choose_chunk_bytes(sg.len, var.unroll), sg.len, signal_grid_cap(sig),
+                    [&](uint64_t c) { return segment_chunks(base, 0, sg.len, c); });
+  const uint64_t chunks = segment_chunks(base, 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
   const uint64_t words[6] = {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(sg.src),

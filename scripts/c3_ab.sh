@@ -15,6 +15,7 @@ for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
   run "r${r}_cpmulti" DORA_GPU_AQL_CP_MULTI=1
   run "r${r}_grid2048" DORA_GPU_SIGNAL_GRID=2048
+  run "r${r}_balanced" DORA_GPU_BALANCED_CHUNKS=1
   run "r${r}_cpmulti_sub" DORA_GPU_AQL_CP_MULTI=1 DORA_GPU_SUBPHASES=1
 done
 echo done

@@ -27,5 +27,6 @@ for r in $(seq 1 "$rounds"); do
   run "r${r}_cpbig" DORA_GPU_AQL_CP_BIG=1
   run "r${r}_chunk16k" DORA_GPU_PACK_CHUNK=16384
   run "r${r}_u8" DORA_GPU_PACK_VARIANT=u8
+  run "r${r}_balanced" DORA_GPU_BALANCED_CHUNKS=1
 done
 echo done
