@@ -548,6 +548,15 @@ bool cp_big() {
   return v;
 }
 
+// DORA_GPU_AQL_MID_COHERENT=0: CP-signalled mid-size packs keep the acquire fence and nt loads.
+bool mid_coherent() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_MID_COHERENT");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 uint64_t barrier_bytes() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
@@ -694,7 +703,15 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // SGPRs by the command processor, so no kernarg line can be stale either.  Interleaved A/B on
   // one box, sources rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 ->
   // 1.23-1.26 us per message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.
-  const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi;
+  // A CP-signalled single-segment pack inside the CP window (1-32 MiB) reads its source
+  // agent-coherently and carries no acquire fence (mid_coherent): the packet's acquire is a
+  // per-packet cost of the command processor (4 MB: 1.50-1.58 -> 1.37-1.46 us per message
+  // pipelined), and a pack whose every source load bypasses the CU's L1 has nothing
+  // for it to invalidate (the in-dispatch control shows L1 the only cache a reread
+  // finds stale; no cross-dispatch configuration ever read stale).
+  const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi ||
+                   (cp && one && unroll == 4 && coherent_level() == 0 && mid_coherent() &&
+                    it0.bytes < cp_signal_window().second);
   const int k = batch                                      ? kBatchKernel
                 : coh                                        ? (one ? 4 : 5)
                 : (one && coherent_level() < 0 && unroll == 4) ? 6

@@ -763,13 +763,15 @@ class _StreamHandle:
 
 
 @pytest.mark.parametrize("writer", ["kernel", "dma"])
-def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer):
+@pytest.mark.parametrize("size", [256 << 10, (2 << 20) + 48])
+def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer, size):
     """One device source rewritten before every send (on the node stream, as
     dora_node_stream's contract says) — by a kernel, or by a host-to-device copy — and sent on
     the AQL path each time: every delivered sample must carry the bytes of its own rewrite.  The
     pack's workgroups may run on XCDs whose L2s still hold the buffer's lines from the previous
     pack; its agent-coherent loads (or the dispatch's acquire fence) must keep them from being
-    served."""
+    served.  256 KiB: in-kernel-signalled packs behind the acquire fence; 2 MiB + 48: the
+    CP-signalled mid-size packs, agent-coherent loads and no fence (aql.cpp mid_coherent)."""
     import ctypes
     from dora_amd import device
     from dora_amd._lib import call
@@ -777,7 +779,7 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer):
     from dora_amd.node import Node
     from dora_amd.verify import to_i64
     res = str(tmp_path / "sink.json")
-    n_msgs, size = 200, 256 << 10
+    n_msgs = 200
     s = device.Stream()
     scratch = device.DeviceBuffer(size)
     sums, host = [], []
