@@ -180,3 +180,28 @@ def test_compact_line_fits_the_driver_tail():
     assert c["roofline"]["frac"] == full["roofline"]["frac"]
     assert c["sink_dropped"]["by_phase"] == {"latency_ladder": 2}
     assert c["c3"]["frac"] == full["c3"]["roofline"]["frac"]
+
+
+def test_compact_line_with_cross_gpu_block():
+    """N > 1: the compact line carries one short entry per cross-GPU configuration (link GB/s,
+    xGMI fraction, RCCL groups and the ranks RCCL formed) and still fits the driver's tail."""
+    import json
+
+    import bench
+    cross = {"c4_fanout_kernel": {"ok": True, "per_link_GBps": 120.5,
+                                  "roofline": {"frac": 0.7876}, "bcast": {"groups": 0, "ranks": 0}},
+             "c4_fanout_rccl": {"ok": True, "per_link_GBps": 98.1, "roofline": {"frac": 0.641},
+                                "bcast": {"groups": 1, "ranks": 8}},
+             "c5_chain_kernel": {"error": "RuntimeError('daemon failed to start: ...')" * 3}}
+    full = {"metric": "m", "value": 1.0, "unit": "GB/s", "n_gpus": 8, "steps": 20, "warmup": 5,
+            "ms_per_step": 0.1, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic", "config": {"workload": "C2", "msg_bytes": 1,
+                                                           "parallelism": "dp8"},
+            "roofline": {"bound": "hbm", "frac": 0.8, "kernel": "dora_aql_pack1_u4 (AQL)"},
+            "parity": {"verified_msgs": 3, "mismatches": 0}, "latency_us": {},
+            "cross_gpu": cross, "sink_dropped_inputs": 0}
+    c = bench.compact_line(full, None)
+    assert c["cross_gpu"]["c4_fanout_rccl"] == {"ok": True, "link_GBps": 98.1, "xgmi_frac": 0.641,
+                                                "bcast": [1, 8]}
+    assert len(c["cross_gpu"]["c5_chain_kernel"]["error"]) <= 60
+    assert len(json.dumps(c)) < 1900
