@@ -1060,8 +1060,9 @@ def main():
         "cold_start_send_us": round(cold_send_us, 1),
         "timed_region": region_setup,
         "sink_us": {"next_event": sink.get("next_event_us"), "free": sink.get("free_us")},
-        # inputs the sink's queue (queue_size 10, the reference default) dropped, all phases:
-        # non-zero would mean the throughput ladders counted undelivered messages
+        # inputs the sink's queue (queue_size 10, the reference default) dropped, all phases;
+        # `sink_dropped_by_phase` (added below) splits them.  The throughput ladders count only
+        # delivered messages (their own `dropped`), and the timed region must show none
         "sink_dropped_inputs": sink.get("dropped_inputs"),
         "node_stats": stats, "exit_codes": codes,
     }
