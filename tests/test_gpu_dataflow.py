@@ -11,6 +11,7 @@ receiver node processes, with IPC-mapped HBM slots, drop-token recycling and bit
 import json
 import os
 import sys
+import threading
 import time
 
 import pytest
@@ -1233,8 +1234,14 @@ def test_full_size_samples_byte_identical_to_the_oracle(launcher, mode):
         return out.raw[:ev["data_len"]]
     try:
         with Dataflow(desc, launcher=launcher) as df:
-            tx = Node("src", dataflow=df.shm, device=0)
-            rx = Node("dst", dataflow=df.shm, device=0)
+            nodes = {}
+
+            def mk(i):  # both dynamic nodes subscribe before either sees AllNodesReady
+                nodes[i] = Node(i, dataflow=df.shm, device=0)
+            ts = [threading.Thread(target=mk, args=(i,)) for i in ("src", "dst")]
+            [t.start() for t in ts]
+            [t.join(90) for t in ts]
+            tx, rx = nodes["src"], nodes["dst"]
             tx.set_async_sends(mode == "async")
             got = []
             for off in (0, 3):
