@@ -475,6 +475,14 @@ def run_sync_leg(node, send, wait_ack, seq, S, n_sync):
     stamps, and the host time between one pack's end and the next one's start."""
     from dora_amd import device
     node.set_async_sends(False)
+    # the sink checksums the timed region's late messages after acking it: one ack round trip
+    # first, so the GPU is idle, then two untimed synchronous sends (this path's first use)
+    node.send_output("throughput", b"", {"seq": seq, "ack": True})
+    wait_ack(seq)
+    seq += 1
+    for k in range(2):
+        send(k, {"seq": seq})
+        seq += 1
     node.set_profiling(False)  # resets the send-phase timers: they cover these sends
     cp0 = device.aql_cp_signalled(node.device)
     node.region_begin()

@@ -533,10 +533,14 @@ std::pair<uint64_t, uint64_t> cp_signal_window() {
 // DORA_GPU_AQL_CP_LONE=0: a single-segment pack above the CP window stays in-kernel-signalled
 // even when it runs alone (sync sends, idle queues).  DORA_GPU_AQL_CP_BIG=1: such packs are
 // CP-signalled even when others run beside them (an A/B knob for the pipelined headline).
-bool cp_lone() {
-  static const bool v = [] {
+// DORA_GPU_AQL_CP_LONE=sync: only synchronous sends count as lone (not a pack that merely
+// finds the queues idle).
+int cp_lone_mode() {
+  static const int v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_CP_LONE");
-    return !(e && *e == '0');
+    if (e && *e == '0') return 0;
+    if (e && std::string(e) == "sync") return 1;
+    return 2;
   }();
   return v;
 }
@@ -983,7 +987,9 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // pack's own stamps): a pack in the window, and a single-segment pack above it that runs alone
   // — sent synchronously, or finding every queue idle (aql.h).
   p.cp = (!profile || cp_stamps) && flag_host &&
-         aql_cp_candidate(segs, n, cp_lone() && (sync || cp_big() || queues_idle(a)));
+         aql_cp_candidate(segs, n,
+                          cp_lone_mode() > 0 &&
+                              (sync || cp_big() || (cp_lone_mode() == 2 && queues_idle(a))));
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
   // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
