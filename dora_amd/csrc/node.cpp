@@ -1441,9 +1441,11 @@ size_t in_transit(dora_node* n) {
 constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
 
 // `ext_len` > len: the slot also holds a validity tail (plans with in-sample bitmaps).
-// Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k] workgroup k's end.
+// Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k mod kCpStampWgs] the
+// latest end of the workgroups k mapping there.
 constexpr uint32_t kRegionCpAreas = 256;
-constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
+constexpr size_t kCpAreaWords = 32;  // 1 + kCpStampWgs words, padded to 256 B
+static_assert(1 + kCpStampWgs <= kCpAreaWords, "stamp area");
 
 // Stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed with
 // the node's AQL queues at its first send, never inside or just before a region
@@ -2566,10 +2568,10 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
       // from the stamp areas through the BAR (written through by the packs, all of which have
       // completed).  An area's other words are older packs' (earlier regions), never the max.
       n->region_cp_next = 0;
-      std::vector<uint64_t> w(dora::kCpAreaWords);
+      std::vector<uint64_t> w(1 + dora::kCpStampWgs);
       for (uint32_t area : n->region_cp_used) {
         std::memcpy(w.data(), n->region_cp_stamps + size_t(area) * dora::kCpAreaWords,
-                    dora::kCpAreaWords * 8);
+                    w.size() * 8);
         const uint64_t a = w[0];
         const uint64_t b = *std::max_element(w.begin() + 1, w.end());
         if (!a || b < a) continue;

@@ -14,8 +14,7 @@ run() {  # name, env...
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
   run "r${r}_cpmulti" DORA_GPU_AQL_CP_MULTI=1
-  run "r${r}_grid2048" DORA_GPU_SIGNAL_GRID=2048
-  run "r${r}_balanced" DORA_GPU_BALANCED_CHUNKS=1
-  run "r${r}_cpmulti_sub" DORA_GPU_AQL_CP_MULTI=1 DORA_GPU_SUBPHASES=1
+  run "r${r}_inflight11" DORA_GPU_MAX_IN_FLIGHT=11
+  run "r${r}_cpmulti_inflight11" DORA_GPU_AQL_CP_MULTI=1 DORA_GPU_MAX_IN_FLIGHT=11
 done
 echo done
