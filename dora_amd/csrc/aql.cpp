@@ -89,12 +89,15 @@ struct Pending {
 constexpr int kMaxQueues = 8;
 
 // The kernels of the embedded code object, in AqlQueue::kobj order.
-constexpr int kKernels = 8;
+constexpr int kKernels = 9;
 constexpr int kBatchKernel = 7;
+constexpr int kReduceKernel = 8;
+constexpr uint32_t kReduceArgsBytes = 32;  // base, areas, out, n, area_words
 constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4",   "dora_aql_pack_u8",
                                                 "dora_aql_pack1_u4",  "dora_aql_pack1_u8",
                                                 "dora_aql_pack1c_u4", "dora_aql_packc_u4",
-                                                "dora_aql_pack1p_u4", "dora_aql_packb_u4"};
+                                                "dora_aql_pack1p_u4", "dora_aql_packb_u4",
+                                                "dora_aql_stamp_reduce"};
 
 struct AqlQueue {
   std::mutex mu;
@@ -139,6 +142,7 @@ struct AqlQueue {
   int device = -1;
   hipStream_t fallback = nullptr;
   uint64_t fallbacks = 0;
+  hsa_signal_t reduce_sig{0};  // completion of aql_stamp_reduce's dispatch
 };
 
 namespace {
@@ -335,6 +339,7 @@ AqlQueue* create(int device) {
             HSA_STATUS_SUCCESS ||
         ka != (k < 2                  ? aql_args_size()
                : k == kBatchKernel    ? aql_batch_args_size()
+               : k == kReduceKernel   ? size_t(kReduceArgsBytes)
                : k == 5               ? sizeof(void*)
                                       : size_t(kArgs1Bytes)) ||
         ka > kSlotBytes) {
@@ -1260,6 +1265,75 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
     (void)hipHostFree(flags);
   }  // else: a pack may still run, leak its buffers rather than free them under it
   return rc;
+}
+
+int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
+                     const uint32_t* areas, uint32_t n, uint64_t* out) {
+  AqlQueue* a = aql_queue(device);
+  if (!a || !a->hring) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue / host argument ring");
+  if (n == 0) return DORA_OK;
+  std::lock_guard<std::mutex> g(a->mu);
+  if (!a->reduce_sig.handle && hsa_signal_create(1, 0, nullptr, &a->reduce_sig) != HSA_STATUS_SUCCESS) {
+    a->reduce_sig.handle = 0;
+    return fail(DORA_ERR_HIP, "hsa_signal_create");
+  }
+  // the host argument slot of the dispatch kRingSlots back must be free (as in dispatch_locked)
+  const uint64_t r = a->next % kRingSlots;
+  Use& u = a->uses[r];
+  const auto t0 = std::chrono::steady_clock::now();
+  while (u.flag && u.seq >= oldest_outstanding(a) && !fill_reached(u.flag, u.epoch)) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      return fail(DORA_ERR_TIMEOUT, "AQL argument slot still in use after 5 s");
+    __builtin_ia32_pause();
+  }
+  uint8_t* slot = a->hring + r * kHostSlotBytes;
+  const uint64_t w[3] = {reinterpret_cast<uintptr_t>(base), reinterpret_cast<uintptr_t>(areas),
+                         reinterpret_cast<uintptr_t>(out)};
+  std::memcpy(slot, w, sizeof(w));
+  std::memcpy(slot + 24, &n, 4);
+  std::memcpy(slot + 28, &area_words, 4);
+  u = Use{nullptr, 0, a->next};
+  ++a->next;
+  hsa_signal_store_relaxed(a->reduce_sig, 1);
+  hsa_queue_t* const q = a->qs[0];
+  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+  while (idx - (a->rd[0] = hsa_queue_load_read_index_scacquire(q)) >= q->size) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      return fail(DORA_ERR_TIMEOUT, "AQL queue full for 5 s");
+    __builtin_ia32_pause();
+  }
+  hsa_queue_store_write_index_relaxed(q, idx + 1);
+  auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  const int k = kReduceKernel;
+  p->workgroup_size_x = 256;
+  p->workgroup_size_y = 1;
+  p->workgroup_size_z = 1;
+  p->reserved0 = 0;
+  p->grid_size_x = n * 256u;
+  p->grid_size_y = 1;
+  p->grid_size_z = 1;
+  p->private_segment_size = a->priv[k];
+  p->group_segment_size = a->group[k];
+  p->kernel_object = a->kobj[k];
+  p->kernarg_address = slot;
+  p->reserved2 = 0;
+  p->completion_signal = a->reduce_sig;
+  // barrier: after every packet of the queue; system-scope release: the host reads `out`
+  const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                          (1 << HSA_PACKET_HEADER_BARRIER) |
+                          (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                          (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
+                   __ATOMIC_RELEASE);
+  hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+  ++a->dispatched[k];
+  if (hsa_signal_wait_scacquire(a->reduce_sig, HSA_SIGNAL_CONDITION_LT, 1,
+                                uint64_t(5) * 1000000000ull, HSA_WAIT_STATE_ACTIVE) != 0) {
+    a->failed.store(true);  // a reduction that never completes: stop using these queues
+    return fail(DORA_ERR_TIMEOUT, "stamp reduction did not complete in 5 s");
+  }
+  return DORA_OK;
 }
 
 int aql_profile_enable(AqlQueue* a, bool on) {

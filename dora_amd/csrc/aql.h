@@ -82,6 +82,12 @@ int bar_alloc(int device, size_t bytes, void** out);
 int bar_write(int device, void* dst, const void* src, size_t bytes);
 void bar_free(void* p);
 
+// Region-end reduction of stamp areas (node.cpp): one dispatch of dora_aql_stamp_reduce over
+// `n` areas of `area_words` words each at `base` (device memory), area indices in `areas`, writing
+// (start, latest end) pairs to `out` (host memory the GPU can write); waits for it (bounded).
+int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
+                     const uint32_t* areas, uint32_t n, uint64_t* out);
+
 // Segments one AQL dispatch takes.
 size_t aql_max_segments();
 

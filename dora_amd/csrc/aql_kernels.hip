@@ -96,3 +96,32 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1p_u4(
     uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
   pack1<4, dora::pack::kPlainSrc>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
+
+// Region-end reduction of CP-signalled packs' stamp areas (aql.cpp aql_stamp_reduce, node.cpp
+// dora_node_region_end): workgroup i reads area `areas[i]` of `base` (area_words words: [0] the
+// first workgroup's start, then the end stamps of pack_body's CP branch) and writes (start,
+// latest end) to out[2i], out[2i + 1] in host memory.  The words were written by system-scope
+// atomics (performed in memory); system-scope loads read them there.
+extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_stamp_reduce(
+    const uint64_t* base, const uint32_t* areas, uint64_t* out, uint32_t n, uint32_t area_words) {
+  const uint32_t i = __builtin_amdgcn_workgroup_id_x(), t = threadIdx.x;
+  if (i >= n) return;
+  const uint64_t* a = base + uint64_t(areas[i]) * area_words;
+  uint64_t m = 0;
+  for (uint32_t w = 1 + t; w < area_words; w += kThreads) {
+    const uint64_t v = __hip_atomic_load(a + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    m = v > m ? v : m;
+  }
+  __shared__ uint64_t red[kThreads];
+  red[t] = m;
+  __syncthreads();
+  for (uint32_t k = kThreads / 2; k > 0; k >>= 1) {
+    if (t < k && red[t + k] > red[t]) red[t] = red[t + k];
+    __syncthreads();
+  }
+  if (t == 0) {
+    __hip_atomic_store(out + 2 * i, __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + 2 * i + 1, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}

@@ -683,6 +683,10 @@ struct dora_node {
   // 25-45 us instead of 4 (profiles/r03_cp_signal_ab.jsonl, first_send_ab).  Areas are never
   // re-zeroed: an area's stale words are an earlier pack's, older than the current pack's own.
   uint64_t* region_cp_stamps = nullptr;  // coarse-grained device memory, host-mapped (aql.h bar_alloc)
+  // region end: the used areas' indices and their (start, end) pairs, pinned host memory the
+  // stamp reduction (aql_stamp_reduce) reads and writes
+  uint32_t* region_reduce_idx = nullptr;
+  uint64_t* region_reduce_out = nullptr;
   uint32_t region_cp_next = 0;
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
@@ -1444,8 +1448,7 @@ constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
 // Stamp areas of a timed region's CP-signalled packs: [0] start, [1 + k mod kCpStampWgs] the
 // latest end of the workgroups k mapping there.
 constexpr uint32_t kRegionCpAreas = 256;
-constexpr size_t kCpAreaWords = 32;  // 1 + kCpStampWgs words, padded to 256 B
-static_assert(1 + kCpStampWgs <= kCpAreaWords, "stamp area");
+constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
 
 // Stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed with
 // the node's AQL queues at its first send, never inside or just before a region
@@ -1469,6 +1472,16 @@ void ensure_cp_stamps(dora_node* n) {
     return;
   }
   n->region_cp_stamps = static_cast<uint64_t*>(d);
+  void* idx = nullptr;
+  void* out = nullptr;
+  if (hipHostMalloc(&idx, kRegionCpAreas * 4, hipHostMallocCoherent) == hipSuccess &&
+      hipHostMalloc(&out, kRegionCpAreas * 16, hipHostMallocCoherent) == hipSuccess) {
+    n->region_reduce_idx = static_cast<uint32_t*>(idx);
+    n->region_reduce_out = static_cast<uint64_t*>(out);
+  } else {
+    (void)hipGetLastError();  // region ends read the areas through the BAR
+    if (idx) (void)hipHostFree(idx);
+  }
 }
 
 int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
@@ -2145,6 +2158,8 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     dora::aql_fence_all();  // no pack of this node may still write its stamps
     dora::bar_free(n->region_cp_stamps);
   }
+  if (n->region_reduce_idx) (void)hipHostFree(n->region_reduce_idx);
+  if (n->region_reduce_out) (void)hipHostFree(n->region_reduce_out);
   delete n;
 }
 
@@ -2568,12 +2583,31 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
       // from the stamp areas through the BAR (written through by the packs, all of which have
       // completed).  An area's other words are older packs' (earlier regions), never the max.
       n->region_cp_next = 0;
+      // one AQL dispatch reduces every used area to (start, latest end) in host memory; the
+      // BAR read is the fallback (~0.3 ms of uncached reads per area)
+      const uint32_t na = uint32_t(std::min<size_t>(n->region_cp_used.size(), dora::kRegionCpAreas));
+      bool reduced = false;
+      if (na && n->region_reduce_idx) {
+        std::copy(n->region_cp_used.begin(), n->region_cp_used.begin() + na, n->region_reduce_idx);
+        std::fill(n->region_reduce_out, n->region_reduce_out + 2 * na, uint64_t(0));
+        reduced = dora::aql_stamp_reduce(n->core->device, n->region_cp_stamps,
+                                         uint32_t(dora::kCpAreaWords), n->region_reduce_idx, na,
+                                         n->region_reduce_out) == DORA_OK;
+        if (!reduced) dora::clear_error();
+      }
       std::vector<uint64_t> w(1 + dora::kCpStampWgs);
-      for (uint32_t area : n->region_cp_used) {
-        std::memcpy(w.data(), n->region_cp_stamps + size_t(area) * dora::kCpAreaWords,
-                    w.size() * 8);
-        const uint64_t a = w[0];
-        const uint64_t b = *std::max_element(w.begin() + 1, w.end());
+      for (uint32_t j = 0; j < n->region_cp_used.size(); ++j) {
+        const uint32_t area = n->region_cp_used[j];
+        uint64_t a, b;
+        if (reduced && j < na) {
+          a = __atomic_load_n(n->region_reduce_out + 2 * j, __ATOMIC_ACQUIRE);
+          b = __atomic_load_n(n->region_reduce_out + 2 * j + 1, __ATOMIC_ACQUIRE);
+        } else {
+          std::memcpy(w.data(), n->region_cp_stamps + size_t(area) * dora::kCpAreaWords,
+                      w.size() * 8);
+          a = w[0];
+          b = *std::max_element(w.begin() + 1, w.end());
+        }
         if (!a || b < a) continue;
         if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
         if (!n->region_stamped || b > n->region_tmax) n->region_tmax = b;

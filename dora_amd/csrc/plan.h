@@ -86,11 +86,11 @@ struct FillSignal {
 constexpr uint32_t kMaxSignalWgs = 4096;
 // Completion-stamp words of a CP-signalled pack inside a timed region (aql.h): workgroup k
 // raises word 1 + (k mod kCpStampWgs) to its end time (atomic max), so a grid of any size fits.
-// 16 words: ~100-300 arrivals per word spread over a pack (no contention worth a nanosecond),
-// and the host reads 17 words per pack through the BAR at region end instead of 1,025 (r03:
-// ~8 KiB of uncached reads per pack, milliseconds for a 200-send region — long enough for the
-// daemon and the receiver to fall asleep before the next burst, r04 trace).
-constexpr uint32_t kCpStampWgs = 16;
+// 1024 words: a few arrivals per word.  (16 words made every 40.96 MB pack of 5,000 workgroups
+// take 33 instead of 15 us: ~300 system-scope atomics per address serialise at ~60 ns each.)
+// The host does not read the words through the BAR (8 KiB of uncached reads per pack, ~57 ms
+// for a 200-send region, r04 trace): one AQL dispatch reduces them (aql_stamp_reduce).
+constexpr uint32_t kCpStampWgs = 1024;
 
 // One message of a batch pack (aql.cpp): its copy segments, slot, fill signal, writable bytes.
 struct BatchItem {
