@@ -44,7 +44,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
                    uint8_t* out, size_t cap, uint32_t* grid, int* unroll, uint64_t dst_cap);
 size_t aql_args_size();
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
-                    uint32_t* grid, int* unroll);
+                    uint32_t* grid, int* unroll, uint64_t grid_cap = 0);
 size_t aql_batch_args_size();
 uint32_t aql_chunk_bytes(const Segment* segs, size_t n);
 int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t cap,
@@ -81,6 +81,7 @@ struct Pending {
   uint32_t chunk = 0;
   bool profile = false;
   bool cp = false;  // may be signalled by the command processor (cp_signal_window) when alone
+  bool lone = false;  // runs alone on the GPU (a synchronous send, or every queue idle)
   uint64_t* cp_stamps = nullptr;  // CP-signalled: the timed region's stamp area (device), or none
 };
 
@@ -508,15 +509,18 @@ namespace {
 // the CP's completion signal instead, consecutive packets of a queue overlap.
 // DESIGN §9 (profiles/r03_aql_pipeline_probe.jsonl, mode 5): 4 MB packs over 4 queues
 // 1.95 -> 1.59-1.64 us each, 1 MB 1.38-1.42 -> 1.51 (so not below 2 MiB), 16 / 40.96 MB flat.
-// DORA_GPU_AQL_CP_MULTI=1: multi-segment packs (C3's point clouds) in the window too.  Opt-in:
-// C3's 200-send steady state gains (0.71-0.73 -> 0.75-0.78 of HBM), but its 20-send burst lost
-// (0.68-0.70 -> 0.35-0.63): the burst's first sends stall on the host (the first send call
-// 34-43 us instead of 4, then ~5 us per call instead of 2), which is not explained yet
-// (profiles/r03_cp_signal_ab.jsonl).
+// Multi-segment packs (C3's point clouds) in the window too (r04 default; DORA_GPU_AQL_CP_MULTI=0:
+// in-kernel signals).  r03 kept them opt-in: the 20-send burst lost (0.68-0.70 -> 0.35-0.63)
+// to host stalls at its first sends.  The r04 trace found the stall: the region before the
+// burst read its CP packs' stamp areas through the BAR (~57 ms of uncached reads), long enough
+// for the daemon and the receiver to fall asleep, and the burst's first messages waited 16 us
+// for the daemon's routing, the sender at its in-flight cap behind them.  With the stamps
+// reduced on the GPU (aql_stamp_reduce), 4 interleaved runs of the C3 block: burst 0.70-0.72 vs
+// 0.66-0.71 in-kernel, steady 0.73-0.76 vs 0.71-0.75 (profiles/r04_c3_ab.jsonl).
 bool cp_multi() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_CP_MULTI");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return v;
 }
@@ -546,6 +550,13 @@ int cp_lone_mode() {
     if (e && *e == '0') return 0;
     if (e && std::string(e) == "sync") return 1;
     return 2;
+  }();
+  return v;
+}
+bool lone_kernel_signal() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_LONE_SIGNAL");
+    return e && std::string(e) == "kernel";
   }();
   return v;
 }
@@ -617,6 +628,12 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // no in-kernel flag, every wave waits for its own stores, the packet's completion signal is
   // the flag's CpSignal line (shm.h FillFlag)
   bool cp = !batch && it0.cp && it0.flag_host && (one || cp_multi());
+  // DORA_GPU_AQL_LONE_SIGNAL=kernel: a lone single-segment pack keeps the in-kernel signal (its
+  // round trip is ~1.5 us shorter than the command processor's: 4 KB packs 7.0-7.2 vs 8.5-8.7 us,
+  // profiles/r04_lone_latency.jsonl) with up to kMaxSignalWgs workgroups instead of 1024
+  const bool lone_kernel = !batch && one && it0.lone && lone_kernel_signal() &&
+                           segs[0].len >= cp_signal_window().first;
+  if (lone_kernel) cp = false;
   int rc;
   if (batch) {
     BatchItem bi[kBatchMsgs];
@@ -630,7 +647,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
              : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, &unroll,
                               it0.dst_cap);
   } else if (one) {
-    rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll);
+    rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll, lone_kernel ? kMaxSignalWgs : 0);
   } else {
     rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll, it0.dst_cap);
   }
@@ -991,10 +1008,8 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // Signalled by the command processor (inside a timed region only with a stamp area for the
   // pack's own stamps): a pack in the window, and a single-segment pack above it that runs alone
   // — sent synchronously, or finding every queue idle (aql.h).
-  p.cp = (!profile || cp_stamps) && flag_host &&
-         aql_cp_candidate(segs, n,
-                          cp_lone_mode() > 0 &&
-                              (sync || cp_big() || (cp_lone_mode() == 2 && queues_idle(a))));
+  p.lone = cp_lone_mode() > 0 && (sync || (cp_lone_mode() == 2 && queues_idle(a)));
+  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, p.lone || cp_big());
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
   // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without

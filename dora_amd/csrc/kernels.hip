@@ -635,19 +635,22 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
 // dst, src, len, flag, done, epoch, chunk_bytes, grid — 56 bytes, the same chunk shape and grid
 // build_aql_args chooses for one segment at sample offset 0.
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
-                    uint32_t* grid_out, int* unroll_out) {
+                    uint32_t* grid_out, int* unroll_out, uint64_t grid_cap) {
   if (sg.op != SEG_COPY || sg.dst_off != 0)
     return fail(DORA_ERR_INVALID, "AQL single-segment pack: segment at offset %llu",
                 (unsigned long long)sg.dst_off);
   Variant var = pack_variant();
   if (var.unroll == 0) var.unroll = default_unroll(sg.len);
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
+  // a caller's cap (a lone in-kernel-signalled pack: up to the kMaxSignalWgs done words)
+  const uint64_t cap = grid_cap ? std::min<uint64_t>(grid_cap, sig.flag ? kMaxSignalWgs : grid_cap)
+                                : signal_grid_cap(sig);
   const uint32_t chunk_bytes =
-      balance_chunk(choose_chunk_bytes(sg.len, var.unroll), sg.len, signal_grid_cap(sig),
+      balance_chunk(choose_chunk_bytes(sg.len, var.unroll), sg.len, cap,
                     [&](uint64_t c) { return segment_chunks(base, 0, sg.len, c); });
   const uint64_t chunks = segment_chunks(base, 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
-  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap));
   const uint64_t words[6] = {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(sg.src),
                              sg.len, reinterpret_cast<uintptr_t>(sig.flag),
                              reinterpret_cast<uintptr_t>(sig.done), sig.epoch};

@@ -13,8 +13,6 @@ run() {  # name, env...
 }
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
-  run "r${r}_cpmulti" DORA_GPU_AQL_CP_MULTI=1
-  run "r${r}_inflight11" DORA_GPU_MAX_IN_FLIGHT=11
-  run "r${r}_cpmulti_inflight11" DORA_GPU_AQL_CP_MULTI=1 DORA_GPU_MAX_IN_FLIGHT=11
+  run "r${r}_inkernel" DORA_GPU_AQL_CP_MULTI=0
 done
 echo done
