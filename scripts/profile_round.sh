@@ -11,6 +11,10 @@ mkdir -p "$out"
 B="python bench.py --no-ladder --no-cpu-baseline --no-c3"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c2_trace" -o run -- \
   $B --steps 200 --warmup 20 > "$out/c2_trace_bench.json" 2> "$out/c2_trace_bench.err"
+# the default (synchronous) send: every timed step waits for its own pack (a lone pack)
+DORA_BENCH_SYNC_SENDS=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv \
+  -d "$out/c2_sync_trace" -o run -- $B --steps 200 --warmup 20 --sync-n 0 \
+  > "$out/c2_sync_trace_bench.json" 2> "$out/c2_sync_trace_bench.err"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/c2_fetch" -o run -- \
   $B --steps 50 --warmup 5 > "$out/c2_fetch_bench.json" 2> "$out/c2_fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/c2_write" -o run -- \

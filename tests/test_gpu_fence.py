@@ -88,4 +88,6 @@ def test_in_dispatch_stale_read_control():
           f"load: plain {out[0]}, nt {out[1]}, sc1 {out[2]}")
     for mode, (bad, stale, blocks) in out.items():
         assert blocks > 0 and bad == 0, (mode, out)
+    # the control fails: L1-cached loads read the old words (r04: 256 of 256 workgroups, twice)
+    assert out[0][1] > 0, out
     assert out[1][1] == 0 and out[2][1] == 0, out
