@@ -21,12 +21,9 @@ PY
 }
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
-  run "r${r}_lone_off" DORA_GPU_AQL_CP_LONE=0
-  run "r${r}_grid4096" DORA_GPU_CP_GRID=4096
-  run "r${r}_grid2048" DORA_GPU_CP_GRID=2048
-  run "r${r}_cpbig" DORA_GPU_AQL_CP_BIG=1
-  run "r${r}_chunk16k" DORA_GPU_PACK_CHUNK=16384
-  run "r${r}_u8" DORA_GPU_PACK_VARIANT=u8
-  run "r${r}_balanced" DORA_GPU_BALANCED_CHUNKS=1
+  run "r${r}_g2048_bal" DORA_GPU_CP_GRID=2048 DORA_GPU_BALANCED_CHUNKS=1
+  run "r${r}_g4096_bal" DORA_GPU_CP_GRID=4096 DORA_GPU_BALANCED_CHUNKS=1
+  run "r${r}_g2048" DORA_GPU_CP_GRID=2048
+  run "r${r}_g6144_bal" DORA_GPU_CP_GRID=6144 DORA_GPU_BALANCED_CHUNKS=1
 done
 echo done
