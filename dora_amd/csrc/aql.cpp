@@ -82,6 +82,7 @@ struct Pending {
   bool profile = false;
   bool cp = false;  // may be signalled by the command processor (cp_signal_window) when alone
   bool lone = false;  // runs alone on the GPU (a synchronous send, or every queue idle)
+  bool read_signal = false;  // CP-signalled, and workgroup 0 stores the flag's read_epoch
   uint64_t* cp_stamps = nullptr;  // CP-signalled: the timed region's stamp area (device), or none
 };
 
@@ -640,6 +641,12 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     for (size_t m = 0; m < n; ++m)
       bi[m] = {items[m].segs, items[m].n, items[m].dst, items[m].sig, items[m].dst_cap};
     rc = build_aql_batch_args(bi, n, args, sizeof(args), &grid);
+  } else if (cp && one && it0.read_signal) {
+    // a synchronous send: workgroup 0 tells the sender when the source has been read (the flag
+    // tagged with bit 0, pack_device.h signal_read); the command processor reports the fill
+    const FillSignal rs{reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(sig.flag) | 1),
+                        sig.epoch, sig.done};
+    rc = build_aql_args1(segs[0], dst, rs, args, &grid, &unroll, kMaxSignalWgs);
   } else if (cp) {
     // no flag, done words non-null: per-wave store waits; `epoch` carries the stamp area
     const FillSignal per_wave{nullptr, reinterpret_cast<uintptr_t>(it0.cp_stamps), sig.done};
@@ -988,9 +995,18 @@ void dispatcher_main(AqlQueue* a) {
 
 }  // namespace
 
+bool aql_read_signal_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_READ_SIGNAL");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
-             uint64_t* cp_stamps, bool sync) {
+             uint64_t* cp_stamps, bool sync, bool* read_signal) {
+  if (read_signal) *read_signal = false;
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -1010,6 +1026,10 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // — sent synchronously, or finding every queue idle (aql.h).
   p.lone = cp_lone_mode() > 0 && (sync || (cp_lone_mode() == 2 && queues_idle(a)));
   p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, p.lone || cp_big());
+  // a synchronous single-segment send returns on its pack's read signal (DORA_GPU_AQL_READ_SIGNAL=0:
+  // on the fill), when the pack leaves at once (not from the backlog or in a batch)
+  p.read_signal = sync && p.cp && n == 1 && segs[0].dst_off == 0 && !cp_stamps && read_signal &&
+                  aql_read_signal_enabled() && a->hring;
   // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
   // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
   // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
@@ -1020,6 +1040,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
                           : size_t(a->next % uint64_t(a->nq));
     const int rc = dispatch_locked(a, qi, &p, 1, big);
     prune(a, int(qi));
+    if (rc == DORA_OK && read_signal) *read_signal = p.read_signal;
     return rc;
   }
   // Below that, a queue holds at most queue_depth() packets (one running, one ready): the
@@ -1030,8 +1051,13 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.chunk = aql_chunk_bytes(segs, n);
   if (a->backlog.empty()) {
     const int qi = pick_queue(a, 0, p.cp ? cp_queue_depth() : 0);
-    if (qi >= 0) return dispatch_locked(a, size_t(qi), &p, 1, false);
+    if (qi >= 0) {
+      const int rc = dispatch_locked(a, size_t(qi), &p, 1, false);
+      if (rc == DORA_OK && read_signal) *read_signal = p.read_signal;
+      return rc;
+    }
   }
+  p.read_signal = false;  // a backlogged send may leave in a batch pack
   a->backlog.push_back(p);
   ++a->backlogged;
   pump_locked(a);

@@ -45,9 +45,13 @@ bool aql_usable(const AqlQueue* q);
 // Would a pack of these segments be signalled by the command processor when sent alone
 // (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI; `lone`: also a lone big pack)?
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
+//
+// `read_signal` (sync sends): set when the pack stores the epoch into the flag's read_epoch once
+// it has read its whole source (before its fill completes): the sender may return on that.
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
-             uint64_t* cp_stamps = nullptr, bool sync = false);
+             uint64_t* cp_stamps = nullptr, bool sync = false, bool* read_signal = nullptr);
+bool aql_read_signal_enabled();
 
 // Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
 // region about to be unmapped), after waiting (bounded) for those fills to signal.

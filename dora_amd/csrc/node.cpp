@@ -614,6 +614,7 @@ struct dora_sample {
   uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
   uint64_t epoch = 0;
   bool stamped = false;  // the pack kernel stamps its start / signal time into the flag line
+  bool read_signal = false;  // the pack stores read_epoch once it has read its source (aql.h)
 };
 
 namespace dora {
@@ -740,7 +741,9 @@ void harvest_region_stamp(dora_node* n, Slot* s) {
   if (s->region_cp_area >= 0 && ff.epoch.load(std::memory_order_acquire) != s->region_epoch &&
       ff.cp_epoch.load(std::memory_order_acquire) == s->region_epoch) {
     n->region_cp_used.push_back(uint32_t(s->region_cp_area));  // resolved at region_end
-  } else if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch) {
+  } else if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch ||
+             ff.read_epoch.load(std::memory_order_acquire) == s->region_epoch) {
+    // an in-kernel-signalled fill, or a read-signalled one (its workgroup 0 stamps the line)
     const uint64_t a = ff.t_start, b = ff.t_end;
     if (b >= a && a) {
       if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
@@ -1145,8 +1148,9 @@ void finish_input(dora_node* n, dora_event* ev) {
       // in-kernel-signalled fill of exactly this epoch writes them (a CP-signalled fill writes
       // none, and the line may already carry a later fill's stamps if the slot was refilled)
       const FillFlag& ff = h->nodes[d.flag_node].fill[d.flag_index];
-      if (ff.epoch.load(std::memory_order_acquire) == d.epoch &&
-          ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) {
+      if ((ff.epoch.load(std::memory_order_acquire) == d.epoch &&
+           ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) ||
+          ff.read_epoch.load(std::memory_order_acquire) == d.epoch) {
         const double ns_per_tick = 1e9 / kRealtimeHz;
         trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
         trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
@@ -1658,14 +1662,17 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       // a timed region's pack may be signalled by the command processor if it has a stamp area
       int area = -1;
       uint64_t* stamps = nullptr;
+      // (a synchronous send's read-signalled pack stamps the flag line instead)
       if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas &&
-          aql_cp_candidate(segs, nseg, /*lone=*/true)) {
+          aql_cp_candidate(segs, nseg, /*lone=*/true) && !(sync && aql_read_signal_enabled())) {
         area = int(n->region_cp_next++);
         stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
       }
       s->slot->region_cp_area = area;
+      bool read_sig = false;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync) == DORA_OK) {
+                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync, &read_sig) == DORA_OK) {
+        s->read_signal = read_sig;
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -1843,6 +1850,7 @@ void form_bcast_groups(dora_node* n) {
 struct SourceWait {
   uint8_t kind = FILL_DONE;  // FILL_FLAG: flag >= epoch; FILL_EVENT: event; FILL_BCAST: stream
   const std::atomic<uint64_t>* flag = nullptr;
+  const std::atomic<uint64_t>* read = nullptr;  // the flag's read_epoch, if the pack stores it
   uint64_t epoch = 0;
   hipEvent_t event = nullptr;
 };
@@ -1856,7 +1864,9 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
   if (w.kind == FILL_FLAG && w.flag) {
     const uint64_t t0 = mono_ns();
     uint32_t spins = 0;
-    while (!fill_reached(w.flag, w.epoch)) {
+    // the pack's read signal (its workgroup 0 saw every workgroup's loads return), or the fill
+    while (!(w.read && w.read->load(std::memory_order_acquire) >= w.epoch) &&
+           !fill_reached(w.flag, w.epoch)) {
       if (++spins < 4096) {
         __builtin_ia32_pause();
         continue;
@@ -1942,6 +1952,8 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     wait.kind = n->bcast_out.count(output_id) ? uint8_t(FILL_BCAST) : s->fill;
     wait.epoch = s->epoch;
     if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
+    if (s->fill == FILL_FLAG && s->read_signal)
+      wait.read = &reinterpret_cast<const FillFlag*>(wait.flag)->read_epoch;
     if (s->fill == FILL_EVENT) wait.event = s->slot->done;
   }
   rc = send_sample(n, output_id, ti, params, params_len, s, &tok);

@@ -458,6 +458,55 @@ __device__ __forceinline__ void signal_batch(const AqlBatchArgs& a, uint32_t blk
   }
 }
 
+// Read signal of a synchronous send (aql.cpp read_signal; `flag` tagged with bit 0): the
+// command processor's completion signal reports the fill to receivers, and workgroup 0 tells
+// the sender as soon as every workgroup's stores — so every load of the source — are complete:
+// it polls the workgroups' done words (as signal_fill does) and stores the epoch into the flag
+// line's read_epoch (word 4, system scope), then stamps the fill's start and end (words 1, 2).
+// The sender returns on it without waiting for the end of the dispatch, the command
+// processor's end-of-pipe event and its signal write (the reference's send_output returns once
+// its copy has read the caller's buffer, arrow_utils.rs:48).  (A "loads returned" word
+// published before the store wait did not compile into one: the wait-count pass puts a
+// vmcnt(0) — every store of the wave complete — in front of any store after the copy loop.)
+template <class A>
+__device__ __forceinline__ void signal_read(const A& a, uint32_t blk, uint32_t nblk,
+                                            uint64_t t_start) {
+  uint64_t* const flag =
+      reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(a.flag) & ~uintptr_t(1));
+  const uint32_t e = static_cast<uint32_t>(a.epoch);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are complete
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(a.done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blk != 0) return;
+  constexpr int kPer = kMaxSignalWgs / kThreads;
+  __shared__ uint32_t missing;
+  for (uint32_t round = 0; round < (1u << 22); ++round) {
+    if (threadIdx.x == 0) missing = 0;
+    __syncthreads();
+    bool mine = true;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = threadIdx.x + k * kThreads;
+      if (i < nblk)
+        mine &= __hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e;
+    }
+    if (!mine) missing = 1;
+    __syncthreads();
+    const bool all = missing == 0;
+    __syncthreads();
+    if (all) {
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(flag + 4, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        stamp_fill(flag, t_start);
+      }
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // a lost workgroup: no read signal; the command processor's signal still reports the fill
+}
+
 // A pack launch: its workgroups stride over the chunks; a signalling launch (NT >= 2) then
 // signals the fill flag.
 template <int U, int NT, class A>
@@ -469,8 +518,12 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
   for (uint32_t c = blk; c < args.n_chunks; c += nblk) pack_chunk<U, NT>(args, c);
   if constexpr (NT >= 2) {
     if (args.flag) {  // all-zero arguments are a no-op
-      if constexpr (__is_same(A, AqlBatchArgs)) signal_batch(args, blk, nblk, t_start);
-      else signal_fill(args, blk, nblk, t_start);
+      if constexpr (__is_same(A, AqlBatchArgs)) {
+        signal_batch(args, blk, nblk, t_start);
+      } else {
+        if (reinterpret_cast<uintptr_t>(args.flag) & 1) signal_read(args, blk, nblk, t_start);
+        else signal_fill(args, blk, nblk, t_start);
+      }
     } else if (args.done) {
       // done words but no flag: the dispatch's completion signal reports the fill (the command
       // processor's, aql.cpp cp_signal_window); every wave's stores are complete before it ends

@@ -66,6 +66,10 @@ struct FillFlag {
   alignas(64) std::atomic<uint64_t> epoch;
   uint64_t t_start, t_end;
   std::atomic<uint64_t> cp_epoch;  // epoch of the CP-signalled fill `cp` reports
+  // a synchronous send's pack has READ its whole source (aql.cpp read_signal): the epoch, stored
+  // by the pack's workgroup 0 before the fill completes; the sender may return on it
+  std::atomic<uint64_t> read_epoch;
+  uint64_t pad_[3];
   CpSignal cp;
 };
 static_assert(offsetof(FillFlag, cp) == 64 && sizeof(FillFlag) == 128, "FillFlag layout");

@@ -22,7 +22,7 @@ PY
 }
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
-  run "r${r}_lone_kernel" DORA_GPU_AQL_LONE_SIGNAL=kernel
+  run "r${r}_read_off" DORA_GPU_AQL_READ_SIGNAL=0
   run "r${r}_lone_off" DORA_GPU_AQL_CP_LONE=0
 done
 echo done
