@@ -995,10 +995,16 @@ void dispatcher_main(AqlQueue* a) {
 
 }  // namespace
 
+// DORA_GPU_AQL_READ_SIGNAL=1 (opt-in): synchronous single-segment sends return on their pack's
+// read signal (pack_device.h signal_read) instead of the command processor's fill signal.  Not
+// the default: the host saw the signal 1.9 us sooner (gap 6.8-7.2 vs 8.6-9.1 us), but the
+// in-kernel completion (done words, workgroup 0's poll, a 4096-workgroup cap) made each 40.96 MB
+// pack 2.8 us longer (17.5-17.7 vs 14.7-14.8 us): 24.8-25.7 vs 23.9-24.4 us per synchronous send
+// over three interleaved rounds (profiles/r04_headline_ab.jsonl, read_off = the default).
 bool aql_read_signal_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_READ_SIGNAL");
-    return !(e && *e == '0');
+    return e && *e == '1';
   }();
   return v;
 }
