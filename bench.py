@@ -824,6 +824,7 @@ def main():
             phase_drops("throughput_ladder_warm")
             d0 = node.dataflow_counters("sink")["dropped_inputs"]
             bs0 = device.aql_batch_stats(local_rank)
+            cp0 = device.aql_cp_signalled(local_rank)
             st0 = node.stats()
             node.set_profiling(False)  # resets the send-phase counters for this size
             # small sizes run ~1-2 us per message: >= 2000 of them, so a host hiccup does not
@@ -854,6 +855,8 @@ def main():
                                     # sends that left in batch packs (aql.cpp), and batches
                                     "batched_msgs": bs1["batched_msgs"] - bs0["batched_msgs"],
                                     "batches": bs1["batches"] - bs0["batches"],
+                                    # packs the command processor signalled (CP window, lone)
+                                    "cp_signalled": device.aql_cp_signalled(local_rank) - cp0,
                                     # where a send's host time goes, and whether its slots
                                     # came from the cache (verdict r02: the bimodal 40.96 MB
                                     # Python ladder)
