@@ -685,6 +685,8 @@ def main():
     from dora_amd.workloads import payload_seed
 
     node = Node("node", dataflow=df.shm, device=local_rank)
+    # the CPUs this process may run on once the node has placed itself (DORA_GPU_PIN)
+    affinity_after_init = sorted(os.sched_getaffinity(0))
     # the benchmark node never rewrites its sources: every send returns as soon as its pack is
     # queued (DORA_SEND_ASYNC), so packs overlap; the default synchronous send is measured
     # beside it (sync_send_headline)
@@ -1099,6 +1101,8 @@ def main():
                            for s in base["series"] if s["mode"] == "latency"},
             "wall_s": base["wall_s"], "nproc": base["nproc"], "cores_used": base["cores"]}
     line["sink_dropped_by_phase"] = drops
+    line["affinity_after_init"] = affinity_after_init
+    line["affinity_at_start"] = affinity
     if args.detail:
         try:
             os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)

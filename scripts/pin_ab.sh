@@ -18,11 +18,13 @@ print(json.dumps({"run": sys.argv[2], "value": d["value"], "frac": d["roofline"]
                   "py40": t["40960000"]["us_per_msg"], "py4": t["4194304"]["us_per_msg"],
                   "sync": d["sync_send_headline"]["us_per_msg"],
                   "lat4k": d["latency_us"]["4096"]["p50_us"], "drops": d["sink_dropped_by_phase"],
-                  "load": d["cpu_share"].get("loadavg_1m")}))
+                  "load": d["cpu_share"].get("loadavg_1m"),
+                  "affinity_after_init": d.get("affinity_after_init")}))
 PY
 }
 for r in $(seq 1 "$rounds"); do
   run "r${r}_pin"
+  run "r${r}_numa_only" DORA_GPU_PIN_L3=0
   run "r${r}_nopin" DORA_GPU_PIN=0
 done
 echo done
