@@ -74,12 +74,37 @@ void parse_cpulist(const char* path, cpu_set_t* out) {
   }
 }
 
-bool l3_placement() {
-  static const bool v = [] {
+// DORA_GPU_PIN_L3: 0 = NUMA node only; "fixed" = the domain by GPU ordinal (r03); default = the
+// least busy domain.
+int l3_placement_mode() {
+  static const int v = [] {
     const char* e = std::getenv("DORA_GPU_PIN_L3");
-    return !(e && *e == '0');
+    if (e && *e == '0') return 0;
+    if (e && std::strcmp(e, "fixed") == 0) return 1;
+    return 2;
   }();
   return v;
+}
+bool l3_placement() { return l3_placement_mode() > 0; }
+
+// Busy and total jiffies per CPU from /proc/stat.
+void cpu_times(std::vector<std::pair<uint64_t, uint64_t>>* out) {
+  out->assign(CPU_SETSIZE, {0, 0});
+  FILE* f = std::fopen("/proc/stat", "r");
+  if (!f) return;
+  char line[512];
+  while (std::fgets(line, sizeof(line), f)) {
+    int cpu = -1;
+    unsigned long long v[10] = {};
+    if (std::sscanf(line, "cpu%d %llu %llu %llu %llu %llu %llu %llu %llu", &cpu, &v[0], &v[1],
+                    &v[2], &v[3], &v[4], &v[5], &v[6], &v[7]) < 5 ||
+        cpu < 0 || cpu >= CPU_SETSIZE)
+      continue;
+    const uint64_t idle = v[3] + v[4];
+    const uint64_t total = v[0] + v[1] + v[2] + v[3] + v[4] + v[5] + v[6] + v[7];
+    (*out)[size_t(cpu)] = {total - idle, total};
+  }
+  std::fclose(f);
 }
 
 }  // namespace
@@ -119,6 +144,31 @@ bool pin_to_numa(int numa, int device, std::atomic<int32_t>* l3_cpu, int procs) 
       if (hint < CPU_SETSIZE && CPU_ISSET(hint, &groups[i])) pick = int(i);
     if (pick < 0 && groups.size() > 1) {
       pick = device >= 0 ? device % int(groups.size()) : 0;
+      if (l3_placement_mode() == 2) {
+        // the domain whose CPUs were idlest over 20 ms (ties: the ordinal's): the dataflow's
+        // processes spin, and a domain shared with busy threads of other processes left r04's
+        // sender or sink off-CPU for tens of microseconds mid-burst (C3 bursts at 0.40-0.66)
+        std::vector<std::pair<uint64_t, uint64_t>> t0, t1;
+        cpu_times(&t0);
+        usleep(20000);
+        cpu_times(&t1);
+        std::vector<double> idle(groups.size(), -1.0);  // idle CPUs per eligible domain
+        int best = -1;
+        for (size_t i = 0; i < groups.size(); ++i) {
+          if (CPU_COUNT(&groups[i]) < 2 * procs) continue;
+          idle[i] = 0;
+          for (int c = 0; c < CPU_SETSIZE; ++c) {
+            if (!CPU_ISSET(c, &groups[i])) continue;
+            const uint64_t dt = t1[size_t(c)].second - t0[size_t(c)].second;
+            const uint64_t db = t1[size_t(c)].first - t0[size_t(c)].first;
+            idle[i] += dt ? 1.0 - double(db) / double(dt) : 1.0;
+          }
+          if (best < 0 || idle[i] > idle[size_t(best)]) best = int(i);
+        }
+        // the ordinal's domain unless another has at least half a CPU more idle
+        if (best >= 0 && !(idle[size_t(pick)] >= 0 && idle[size_t(pick)] + 0.5 > idle[size_t(best)]))
+          pick = best;
+      }
       int first = 0;
       while (!CPU_ISSET(first, &groups[size_t(pick)])) ++first;
       int32_t none = -1;

@@ -24,7 +24,7 @@ PY
 }
 for r in $(seq 1 "$rounds"); do
   run "r${r}_pin"
-  run "r${r}_numa_only" DORA_GPU_PIN_L3=0
+  run "r${r}_pin_fixed" DORA_GPU_PIN_L3=fixed
   run "r${r}_nopin" DORA_GPU_PIN=0
 done
 echo done
