@@ -569,6 +569,14 @@ bool cp_big() {
   return v;
 }
 
+bool lone_dev_args() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_LONE_DEV_ARGS");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // DORA_GPU_AQL_MID_COHERENT=0: CP-signalled mid-size packs keep the acquire fence and nt loads.
 bool mid_coherent() {
   static const bool v = [] {
@@ -581,9 +589,21 @@ bool mid_coherent() {
 uint64_t barrier_bytes() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(32) << 20;
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(8) << 20;
   }();
   return v;
+}
+
+// Queues the barrier-bit packs of `bytes` spread over: three from 32 MiB (three concurrent 40 MB
+// copies saturate HBM: 12.9-13.0 us per pack on three queues vs 13.2 on four,
+// profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
+// the 20-cloud burst, profiles/r04_full_ab.jsonl).  DORA_GPU_AQL_BIG_QUEUES=N: N for every size.
+int big_queues(int nq, uint64_t bytes) {
+  static const int v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_BIG_QUEUES");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return std::min(nq, v ? v : bytes >= (uint64_t(32) << 20) ? 3 : 4);
 }
 
 // The number of the oldest dispatch still in an outstanding list (a->next when none is).
@@ -688,13 +708,19 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // its arguments from the device-ring slot through a pointer preloaded from the host ring.
   const bool coh_multi = coherent_level() >= 2 && !one && !batch && unroll == 4 && a->hring;
   uint8_t* slot;
-  if (one) {
+  // A lone single-segment pack (nothing to overlap its dispatch with) takes its arguments from
+  // the device ring like a multi-segment one: the command processor's preload then reads HBM, not
+  // host memory over PCIe — 0.6-0.7 us less from doorbell to completion at any size
+  // (aql_pipeline_bench modes 5 vs 7, profiles/r04_lone_dispatch_ab.jsonl; DORA_GPU_AQL_LONE_DEV_ARGS=0:
+  // host memory).  Pipelined packs keep the host ring: no HDP flush per send.
+  const bool dev_args1 = one && it0.lone && lone_dev_args();
+  if (one && !dev_args1) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
     slot = a->hring + r * kHostSlotBytes;
     std::memcpy(slot, args, kArgs1Bytes);
   } else {
     slot = a->ring + r * kSlotBytes;
-    std::memcpy(slot, args, batch ? aql_batch_args_size() : aql_args_size());
+    std::memcpy(slot, args, one ? kArgs1Bytes : batch ? aql_batch_args_size() : aql_args_size());
     // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both
     // are posted writes ordered before the doorbell
     __builtin_ia32_sfence();
@@ -705,10 +731,8 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
       std::memcpy(slot, &dev_slot, sizeof(dev_slot));
     }
   }
-  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
-  // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
-  // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
-  // the barrier; profiles/r02_aql_big_ab.jsonl).  Smaller packs overlap freely on all queues.
+  // HBM-bound packs (>= barrier_bytes) run in order per queue (barrier bit) over at most three
+  // queues (aql_pack).  Smaller packs overlap freely on all queues.
   sp_args.stop();
   SubSpan sp_disp(SP_AQL_DISPATCH);
   hsa_queue_t* const q = a->qs[qi];
@@ -872,14 +896,14 @@ int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
   return -1;
 }
 
-// Bytes a batch may carry (DORA_GPU_AQL_BATCH_BYTES, default the barrier size), and the size from
+// Bytes a batch may carry (DORA_GPU_AQL_BATCH_BYTES, default 32 MiB), and the size from
 // which a batch runs like a big pack — barrier bit, at most three queues — instead of
 // overlapping on all four (DORA_GPU_AQL_BATCH_BIG_BYTES, default: never).
 uint64_t batch_bytes() {
   static const uint64_t v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_BATCH_BYTES");
     const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
-    return x ? x : barrier_bytes();
+    return x ? x : uint64_t(32) << 20;
   }();
   return v;
 }
@@ -943,7 +967,7 @@ void pump_locked(AqlQueue* a) {
       ++n;
     }
     const bool big = n > 1 && bytes >= batch_big_bytes();
-    const int qi = pick_queue(a, big ? 3 : 0,
+    const int qi = pick_queue(a, big ? big_queues(a->nq, bytes) : 0,
                               n == 1 && a->backlog.front().cp ? cp_queue_depth() : 0);
     if (qi < 0) return;
     Pending batch[kBatchMsgs];
@@ -1036,13 +1060,16 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // on the fill), when the pack leaves at once (not from the backlog or in a batch)
   p.read_signal = sync && p.cp && n == 1 && segs[0].dst_off == 0 && !cp_stamps && read_signal &&
                   aql_read_signal_enabled() && a->hring;
-  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 32 MiB) run in order per queue
-  // (barrier bit) over at most three queues: three concurrent 40 MB copies saturate HBM, more
-  // only contend (40.96 MB: 12.9-13.0 us per pack on three vs 13.2 on four, 14.1-14.5 without
-  // the barrier; profiles/r02_aql_big_ab.jsonl).
+  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 8 MiB) run in order per queue
+  // (barrier bit) over at most three (four below 32 MiB) queues, big_queues: more concurrent
+  // 40 MB copies only contend (14.1-14.5 us per pack without the barrier, 12.9-13.0 with it;
+  // profiles/r02_aql_big_ab.jsonl).  r04 lowered the size from 32 to 8 MiB (the
+  // in-flight cap's boundary): C3's 13 MB clouds 0.68-0.70 -> 0.72-0.75 of HBM over the 20-cloud
+  // burst, 16 MB native sends 5.36-5.55 -> 5.20-5.25 us, over three interleaved full runs each
+  // (profiles/r04_full_ab.jsonl).
   const bool big = barrier_bytes() && p.bytes >= barrier_bytes();
   if (big || !batching_enabled()) {
-    const size_t qi = big ? size_t(a->next_big++ % uint64_t(std::min(a->nq, 3)))
+    const size_t qi = big ? size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)))
                           : size_t(a->next % uint64_t(a->nq));
     const int rc = dispatch_locked(a, qi, &p, 1, big);
     prune(a, int(qi));
@@ -1183,10 +1210,15 @@ uint64_t aql_dispatched(int device, size_t k) {
 // the last wave ended, follows every store of the pack without relying on a release fence).
 int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
                        double* us_per_msg) {
-  const bool no_acquire = mode == 3 || mode == 4;
-  const bool wave_wait = mode == 5;
+  // 6: as 5 with the coherent kernel and no acquire fence (dora_aql_pack1c_u4); 7: as 5 with the
+  // arguments in the device ring (write-combined stores + HDP flush) instead of host memory;
+  // 8: 6 and 7 together — the latency of a lone pack's dispatch
+  const bool coherent = mode == 6 || mode == 8;
+  const bool dev_args = mode == 7 || mode == 8;
+  const bool no_acquire = mode == 3 || mode == 4 || coherent;
+  const bool wave_wait = mode >= 5;
   if (mode == 3) mode = 0;
-  if (mode == 4 || mode == 5) mode = 1;
+  if (mode >= 4) mode = 1;
   AqlQueue* a = aql_queue(device);
   if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
   if (!a->hring) return fail(DORA_ERR_UNSUPPORTED, "no host argument ring");
@@ -1255,15 +1287,19 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
       if (build_aql_args1(sg, dst + b * stride, fs, args, &grid, &unroll) != DORA_OK)
         return DORA_ERR_INVALID;
       const uint64_t r = a->next++ % kRingSlots;
-      uint8_t* slot = a->hring + r * kHostSlotBytes;
+      uint8_t* slot = (dev_args ? a->ring + r * kSlotBytes : a->hring + r * kHostSlotBytes);
       std::memcpy(slot, args, kArgs1Bytes);
+      if (dev_args) {
+        __builtin_ia32_sfence();
+        *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
+      }
       if (mode != 0) hsa_signal_store_relaxed(sigs[size_t(sl)], 1);
       hsa_queue_t* const q = a->qs[qi];
       const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
       while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) __builtin_ia32_pause();
       hsa_queue_store_write_index_relaxed(q, idx + 1);
       auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-      const int k = 2;  // dora_aql_pack1_u4
+      const int k = coherent ? 4 : 2;  // dora_aql_pack1c_u4 / dora_aql_pack1_u4
       p->workgroup_size_x = 256;
       p->workgroup_size_y = 1;
       p->workgroup_size_z = 1;

@@ -145,19 +145,26 @@ constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
 // Samples a sender may have in flight (sent, token not back) before it waits for a returned
 // slot.  Below 8 MiB a message's life is dominated by the dispatch-to-fill-flag latency
 // (~5-8 us for a 4 KB-4 MB pack over the AQL queues, scripts/trace_report.py), so the pipeline
-// depth sets the rate: 11 there, 8 for larger samples, which are HBM-bound and lose to more
-// concurrent packs (C3, 13 MB: -20 % at 12).  11 = the reference's default queue_size (10) + the
-// input a receiver holds: a receiver that pauses (a checksum, a host hiccup) then finds at most
-// 10 ready inputs queued and drops none (12 dropped one per pause; in-flight 12 vs 16-24 made
-// no difference to the 4 MB rate, profiles/r02_sweep_4mb_*.jsonl).  DORA_GPU_MAX_IN_FLIGHT sets
-// both.
+// depth sets the rate: 10 there, 8 for larger samples, which are HBM-bound and lose to more
+// concurrent packs (C3, 13 MB: -20 % at 12).  10 = the reference's default queue_size: every
+// input queued at a receiver is in flight, so a receiver with the default queue never holds more
+// than it keeps, whenever it pauses, and drops nothing.  (r02-r03 used 11, counting on the
+// receiver holding one input while its queue fills; a receiver that pauses between releasing
+// one input and taking the next then had 11 ready and dropped one: 0-5 per bench run in the
+// throughput ladders, none at 10 over three full runs with the same rates,
+// profiles/r04_full_ab.jsonl.)  DORA_GPU_MAX_IN_FLIGHT=N sets both, `S:L` each.
 size_t max_in_flight(uint64_t len) {
-  static const long env = [] {
+  static const std::pair<long, long> env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
-    return e ? std::atol(e) : 0L;
+    if (!e) return std::make_pair(0L, 0L);
+    char* end = nullptr;
+    const long a = std::strtol(e, &end, 10);
+    const long b = (end && *end == ':') ? std::atol(end + 1) : a;
+    return std::make_pair(a, b);
   }();
-  if (env > 0) return static_cast<size_t>(env);
-  return len < kSmallInFlightBytes ? 11 : 8;
+  const long v = len < kSmallInFlightBytes ? env.first : env.second;
+  if (v > 0) return static_cast<size_t>(v);
+  return len < kSmallInFlightBytes ? 10 : 8;
 }
 
 // Opt-in (DORA_GPU_SPLIT_IN_FLIGHT=1): the cap above bounds only the samples whose fill has

@@ -11,8 +11,17 @@ run() {  # name, env...
     > "$out/$name.jsonl" 2> "$out/$name.err"
   sed "s/^{/{\"run\": \"$name\", /" "$out/$name.jsonl" >> "$out/summary.jsonl"
 }
+# variants: `inkernel` (r03's in-kernel-signalled multi-segment packs), `barrier` (13 MB clouds
+# run one at a time per queue over three queues, as the headline's >= 32 MiB packs), `depth2`
+variants=${C3_AB_VARIANTS:-inkernel}
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
-  run "r${r}_inkernel" DORA_GPU_AQL_CP_MULTI=0
+  for v in $variants; do
+    case $v in
+      inkernel) run "r${r}_inkernel" DORA_GPU_AQL_CP_MULTI=0 ;;
+      barrier) run "r${r}_barrier" DORA_GPU_AQL_BARRIER_BYTES=12000000 ;;
+      depth2) run "r${r}_depth2" DORA_GPU_AQL_CP_DEPTH=2 ;;
+    esac
+  done
 done
 echo done

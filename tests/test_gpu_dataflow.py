@@ -626,9 +626,10 @@ def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
 
 def test_default_queue_keeps_up_with_async_burst(launcher, tmp_path):
     """A receiver with the reference's default queue_size (10) that keeps up with a back-to-back
-    burst drops nothing, although the sender keeps up to 12 samples in flight: inputs whose
-    fill is still running are not yet queued for the drop policy (the reference fills before
-    the message leaves the sender).  Every input is verified bit-exact."""
+    burst drops nothing: the sender keeps at most 10 samples in flight below 8 MiB (node.cpp
+    max_in_flight), and inputs whose fill is still running are not yet queued for the drop
+    policy (the reference fills before the message leaves the sender).  Every 50th input is
+    checksummed against its source."""
     from dora_amd.dataflow import Dataflow
     from dora_amd.node import Node
     res = str(tmp_path / "sink.json")
