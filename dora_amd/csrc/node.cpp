@@ -145,14 +145,15 @@ constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
 // Samples a sender may have in flight (sent, token not back) before it waits for a returned
 // slot.  Below 8 MiB a message's life is dominated by the dispatch-to-fill-flag latency
 // (~5-8 us for a 4 KB-4 MB pack over the AQL queues, scripts/trace_report.py), so the pipeline
-// depth sets the rate: 10 there, 8 for larger samples, which are HBM-bound and lose to more
-// concurrent packs (C3, 13 MB: -20 % at 12).  10 = the reference's default queue_size: every
-// input queued at a receiver is in flight, so a receiver with the default queue never holds more
-// than it keeps, whenever it pauses, and drops nothing.  (r02-r03 used 11, counting on the
-// receiver holding one input while its queue fills; a receiver that pauses between releasing
-// one input and taking the next then had 11 ready and dropped one: 0-5 per bench run in the
-// throughput ladders, none at 10 over three full runs with the same rates,
-// profiles/r04_full_ab.jsonl.)  DORA_GPU_MAX_IN_FLIGHT=N sets both, `S:L` each.
+// depth sets the rate: 11 there, 8 for larger samples, which are HBM-bound and lose to more
+// concurrent packs (C3, 13 MB: -20 % at 12).  11 = the reference's default queue_size (10) + the
+// input a receiver is handed: every input queued at a receiver is in flight, and the drop-oldest
+// policy runs after next_event has taken its event (dora_node_next_event), so a default receiver
+// drops nothing whenever it pauses.  (r03 applied the policy before taking the event: a
+// receiver that paused between releasing one input and taking the next then had 11 ready and
+// dropped one, 0-5 per bench run in the throughput ladders.  A cap of 10 instead cost 4 MB
+// sends ~6 %: 1.56-1.63 vs 1.41-1.50 us, profiles/r04_cap_ab.jsonl.)  DORA_GPU_MAX_IN_FLIGHT=N
+// sets both, `S:L` each.
 size_t max_in_flight(uint64_t len) {
   static const std::pair<long, long> env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
@@ -164,7 +165,7 @@ size_t max_in_flight(uint64_t len) {
   }();
   const long v = len < kSmallInFlightBytes ? env.first : env.second;
   if (v > 0) return static_cast<size_t>(v);
-  return len < kSmallInFlightBytes ? 10 : 8;
+  return len < kSmallInFlightBytes ? 11 : 8;
 }
 
 // Opt-in (DORA_GPU_SPLIT_IN_FLIGHT=1): the cap above bounds only the samples whose fill has
@@ -1324,7 +1325,8 @@ void drop_oldest_inputs(dora_node* n) {
                  n->queue.end());
 }
 
-void drain_events(dora_node* n) {
+// Move every event the daemon has delivered into the node's queue; true when any arrived.
+bool drain_events(dora_node* n) {
   uint32_t kind;
   std::vector<uint8_t>& p = n->ev_buf;  // reused across events
   SubSpan sp(SP_RECV_DRAIN);
@@ -1333,7 +1335,7 @@ void drain_events(dora_node* n) {
     encode_event(n, kind, p);
     got = true;
   }
-  if (got) drop_oldest_inputs(n);
+  return got;
 }
 
 // The Metadata of a send as WBuf::bytes(WBuf::metadata(m)) would write it, straight into `w`
@@ -2386,10 +2388,16 @@ int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
   DORA_GUARD_BEGIN
   const uint64_t t0 = dora::mono_ns();
   for (;;) {
-    dora::drain_events(n);
+    const bool got = dora::drain_events(n);
     if (!n->queue.empty()) {
+      // The event handed over now is the node's, like the one the reference's event-stream
+      // thread holds (event_stream/thread.rs:139-157: taken from the daemon's queue, in its
+      // channel): the drop-oldest policy keeps queue_size inputs per input id among the rest.
+      // So a sender with queue_size + 1 samples in flight (node.cpp max_in_flight) never makes
+      // a default receiver drop, whenever that receiver pauses.
       *out = n->queue.front().release();
       n->queue.pop_front();
+      if (got) dora::drop_oldest_inputs(n);
       dora::finish_input(n, *out);
       return DORA_OK;
     }

@@ -108,9 +108,12 @@ def test_routing_drop_oldest_and_close():
             assert ev["type_info"].to_json()["data_type"] == "C"
         elif ev["type"] == "INPUT_CLOSED":
             closed.append(ev["id"])
-    # queue_size 3: the three newest inputs survive (node_communication/mod.rs:320-359)
-    assert [s for s, _ in got] == [2, 3, 4]
-    assert got[0][1] == bytes([2]) * 10
+    # queue_size 3 (node_communication/mod.rs:320-359): the first next() takes the oldest
+    # input — handed to the node, as the reference's event-stream thread takes events out of the
+    # daemon's queue (event_stream/thread.rs:139-157) — and the three newest of the rest survive
+    assert [s for s, _ in got] == [0, 2, 3, 4]
+    assert got[0][1] == bytes([0]) * 10
+    assert got[1][1] == bytes([2]) * 10
     assert closed == ["in"]
     dst.close()
     d.join()

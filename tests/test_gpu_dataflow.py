@@ -565,8 +565,10 @@ def _distinct_sources(n, size):
 
 def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
     """queue_size 2 (node_communication/mod.rs:320-359): a receiver that drains a burst of 60
-    inputs at once keeps exactly the newest 2, every dropped input's token goes back at once,
-    and the sender's close finds every token returned (no 10-s drop-token wait)."""
+    inputs at once is handed the oldest (the event its next() takes, like the one the reference's
+    event-stream thread holds) and keeps exactly the newest 2 of the rest; every dropped input's
+    token goes back at once, and the sender's close finds every token returned (no 10-s
+    drop-token wait)."""
     import threading
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
@@ -615,11 +617,12 @@ def test_slow_receiver_drop_oldest_returns_tokens(launcher, tmp_path):
     for b in bufs:
         b.free()
     assert not err, err
-    # exactly the newest queue_size inputs survived, bit-exact; the other 58 were dropped
-    assert [g[0] for g in got] == [n_msgs - 2, n_msgs - 1], got
+    # the handed-over input and exactly the newest queue_size of the rest survived, bit-exact;
+    # the other 57 were dropped
+    assert [g[0] for g in got] == [0, n_msgs - 2, n_msgs - 1], got
     from dora_amd.verify import to_i64
-    assert [to_i64(g[1]) for g in got] == sums[-2:]
-    assert got[0][2] == n_msgs - 2
+    assert [to_i64(g[1]) for g in got] == [sums[0]] + sums[-2:]
+    assert got[0][2] == n_msgs - 3
     assert node_stats["slots_created"] + node_stats["cache_hits"] == n_msgs
     assert close_s < 5.0, close_s
 
