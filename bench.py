@@ -735,10 +735,19 @@ def main():
     drops = {}
     drop_mark = [node.dataflow_counters("sink")["dropped_inputs"]]
 
+    # other processes with queues on this GPU at the end of each phase (dora_amd/tenants.py):
+    # an HBM-bound rate that drops mid-run on a shared box is their traffic, not ours
+    from dora_amd.tenants import gpu_tenants
+    tenants = {}
+
     def phase_drops(name):
         now = node.dataflow_counters("sink")["dropped_inputs"]
         drops[name] = drops.get(name, 0) + now - drop_mark[0]
         drop_mark[0] = now
+        t = gpu_tenants()
+        if t.get("visible"):
+            prev = tenants.get(name, (0, 0))
+            tenants[name] = (max(prev[0], t["others"]), max(prev[1], t["other_queues"]))
 
     copy_cal = box_copy_rate(S, stream)
     # the same at the mid sizes, where per-message dispatch rather than HBM binds
@@ -1103,6 +1112,8 @@ def main():
                            for s in base["series"] if s["mode"] == "latency"},
             "wall_s": base["wall_s"], "nproc": base["nproc"], "cores_used": base["cores"]}
     line["sink_dropped_by_phase"] = drops
+    # (other processes, their queues) on this GPU at each phase's end, when KFD sysfs is readable
+    line["gpu_tenants_by_phase"] = {k: list(v) for k, v in tenants.items()}
     line["affinity_after_init"] = affinity_after_init
     line["affinity_at_start"] = affinity
     if args.detail:
@@ -1162,6 +1173,9 @@ def compact_line(line, detail_path):
     out["latency_summary"] = {z: [lat[z]["p50_us"], lat[z]["p99_us"], lat[z]["p99_incl_pack_us"]]
                               for z in ("4096", "4194304", "40960000") if z in lat}
     out["latency_summary_keys"] = "size: [p50, p99, p99 incl. pack] us"
+    ten = line.get("gpu_tenants_by_phase")
+    if ten:  # the most other processes seen on this GPU at any phase's end
+        out["gpu_tenants_max"] = max(v[0] for v in ten.values())
     cross = line.get("cross_gpu")
     if cross:  # N > 1: each cross-GPU configuration in one short entry
         out["cross_gpu"] = {

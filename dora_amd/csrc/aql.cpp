@@ -577,6 +577,14 @@ bool lone_dev_args() {
   return v;
 }
 
+bool lone_coherent() {
+  static const bool v = [] {
+    const char* e = std::getenv("DORA_GPU_AQL_LONE_COHERENT");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // DORA_GPU_AQL_MID_COHERENT=0: CP-signalled mid-size packs keep the acquire fence and nt loads.
 bool mid_coherent() {
   static const bool v = [] {
@@ -766,9 +774,13 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // pipelined), and a pack whose every source load bypasses the CU's L1 has nothing
   // for it to invalidate (the in-dispatch control shows L1 the only cache a reread
   // finds stale; no cross-dispatch configuration ever read stale).
+  // A lone single-segment pack likewise (DORA_GPU_AQL_LONE_COHERENT=0: fenced): no packet acquire
+  // in its dispatch latency (0.1-0.2 us, aql_pipeline_bench mode 6 vs 5,
+  // profiles/r04_lone_dispatch_ab.jsonl).
   const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi ||
                    (cp && one && unroll == 4 && coherent_level() == 0 && mid_coherent() &&
-                    it0.bytes < cp_signal_window().second);
+                    it0.bytes < cp_signal_window().second) ||
+                   (one && unroll == 4 && coherent_level() == 0 && it0.lone && lone_coherent());
   const int k = batch                                      ? kBatchKernel
                 : coh                                        ? (one ? 4 : 5)
                 : (one && coherent_level() < 0 && unroll == 4) ? 6

@@ -19,11 +19,20 @@ print(json.dumps({"run": sys.argv[2], "headline_frac": d["roofline"]["frac"],
                           "send_phase_us")}}))
 PY
 }
+# SYNC_AB_VARIANTS: names from the list below (default: the r04 grid sweep)
+variants=${SYNC_AB_VARIANTS:-"g2048_bal g4096_bal g2048 g6144_bal"}
 for r in $(seq 1 "$rounds"); do
   run "r${r}_default"
-  run "r${r}_g2048_bal" DORA_GPU_CP_GRID=2048 DORA_GPU_BALANCED_CHUNKS=1
-  run "r${r}_g4096_bal" DORA_GPU_CP_GRID=4096 DORA_GPU_BALANCED_CHUNKS=1
-  run "r${r}_g2048" DORA_GPU_CP_GRID=2048
-  run "r${r}_g6144_bal" DORA_GPU_CP_GRID=6144 DORA_GPU_BALANCED_CHUNKS=1
+  for v in $variants; do
+    case $v in
+      g2048_bal) run "r${r}_$v" DORA_GPU_CP_GRID=2048 DORA_GPU_BALANCED_CHUNKS=1 ;;
+      g4096_bal) run "r${r}_$v" DORA_GPU_CP_GRID=4096 DORA_GPU_BALANCED_CHUNKS=1 ;;
+      g6144_bal) run "r${r}_$v" DORA_GPU_CP_GRID=6144 DORA_GPU_BALANCED_CHUNKS=1 ;;
+      g2048) run "r${r}_$v" DORA_GPU_CP_GRID=2048 ;;
+      g4096) run "r${r}_$v" DORA_GPU_CP_GRID=4096 ;;
+      fenced) run "r${r}_$v" DORA_GPU_AQL_LONE_COHERENT=0 ;;
+      hostargs) run "r${r}_$v" DORA_GPU_AQL_LONE_DEV_ARGS=0 ;;
+    esac
+  done
 done
 echo done

@@ -11,10 +11,13 @@ compares the sample with the new pattern.
 
 The negative control — L1-cached plain loads (test kernel `dora_aql_pack1p_u4`) without the
 fence — never delivered a stale byte on MI355X (r03, 0 of 40 trials per writer).  With no
-evidence either way the fence is back on by default (plain non-temporal loads behind it,
-`dora_aql_pack1_u4`); the coherent no-fence kernel is opt-in (`DORA_GPU_AQL_COHERENT=1`).
-This test keeps every shipped configuration bit-exact under that sequence and reports the
-negative control's outcome (a stale delivery there would be the evidence, and is printed).
+evidence either way the fence went back on (plain non-temporal loads behind it,
+`dora_aql_pack1_u4`).  r04 added a control that does fail (test_in_dispatch_stale_read_control:
+plain loads re-read stale words inside one dispatch, nt and sc1 loads never), and since then
+lone and CP-signalled mid-size packs use the coherent no-fence kernel by default; pipelined
+packs keep the fence.  This test keeps every shipped configuration bit-exact under that sequence
+and reports the cross-dispatch negative control's outcome (a stale delivery there would be
+evidence, and is printed).
 
 Each configuration runs in its own process (tests/fence_probe.py), since the knobs are read once.
 """
@@ -37,19 +40,22 @@ CONFIGS = {
     "plain_no_fence": ({"DORA_GPU_AQL_COHERENT": "plain", "DORA_GPU_AQL_ACQUIRE": "none"},
                        "dora_aql_pack1p_u4"),
     "plain_fence": ({"DORA_GPU_AQL_COHERENT": "plain"}, "dora_aql_pack1p_u4"),
-    # the default: non-temporal loads behind the agent-scope acquire fence
-    "default": ({}, "dora_aql_pack1_u4"),
-    # opt-in: agent-coherent loads, no fence
+    # the default of pipelined packs: non-temporal loads behind the agent-scope acquire fence
+    # (the probe's packs run alone, which by default take the coherent kernel: turned off here)
+    "default": ({"DORA_GPU_AQL_LONE_COHERENT": "0"}, "dora_aql_pack1_u4"),
+    # the default of lone packs (r04): agent-coherent loads, no fence
+    "lone": ({}, "dora_aql_pack1c_u4"),
+    # opt-in for every single-segment pack: agent-coherent loads, no fence
     "coherent": ({"DORA_GPU_AQL_COHERENT": "1"}, "dora_aql_pack1c_u4"),
 }
-SHIPPED = ("plain_fence", "default", "coherent")
+SHIPPED = ("plain_fence", "default", "lone", "coherent")
 SIZE = 4 << 10   # one chunk: one workgroup per pack
 WARM = 256       # fence_probe.WARM
 
 
 def _probe(cfg, engine):
     env = dict(os.environ)
-    for k in ("DORA_GPU_AQL_COHERENT", "DORA_GPU_AQL_ACQUIRE"):
+    for k in ("DORA_GPU_AQL_COHERENT", "DORA_GPU_AQL_ACQUIRE", "DORA_GPU_AQL_LONE_COHERENT"):
         env.pop(k, None)
     env.update(CONFIGS[cfg][0])
     r = subprocess.run([sys.executable, os.path.join(HERE, "fence_probe.py"), engine,
