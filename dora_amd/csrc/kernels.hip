@@ -57,8 +57,11 @@ uint32_t env_u32(const char* name) {
 }
 // workgroups of a signalling launch (0: kSignalGrid; DORA_GPU_SIGNAL_GRID, dora_gpu_pack_tune)
 std::atomic<uint32_t> g_signal_grid{env_u32("DORA_GPU_SIGNAL_GRID")};
-// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 8192)
-std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 8192u};
+// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 4096:
+// a lone 40.96 MB pack, 5,000 chunks, takes 14.05 us with 4096 workgroups against 14.84-14.92
+// with one per chunk and 15.5 with 2048, profiles/r04_sync_ab.jsonl; packs below 32 MiB have
+// fewer chunks than that)
+std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 4096u};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win

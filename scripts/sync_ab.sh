@@ -32,6 +32,7 @@ for r in $(seq 1 "$rounds"); do
       g4096) run "r${r}_$v" DORA_GPU_CP_GRID=4096 ;;
       fenced) run "r${r}_$v" DORA_GPU_AQL_LONE_COHERENT=0 ;;
       hostargs) run "r${r}_$v" DORA_GPU_AQL_LONE_DEV_ARGS=0 ;;
+      grid*) run "r${r}_$v" DORA_GPU_CP_GRID=${v#grid} ;;
     esac
   done
 done
