@@ -844,6 +844,11 @@ def main():
             # small sizes run ~1-2 us per message: >= 2000 of them, so a host hiccup does not
             # set the rate of a ~0.3 ms burst
             tp_n = args.tp_n if size > (4 << 20) else max(args.tp_n, 2000)
+            # sizes from 16 MiB: the packs' own device time as a region (stamps), so a slow run
+            # shows whether the GPU or the token path set its rate (the bimodal 40.96 MB ladder)
+            dev_region = size >= (16 << 20) and not args.no_kernel_timing
+            if dev_region:
+                node.region_begin()
             t_a = time.perf_counter()
             for k in range(tp_n):  # the last message asks for the ack (no trailing marker)
                 meta = {"seq": seq, "ack": True} if k == tp_n - 1 else {"seq": seq}
@@ -851,6 +856,23 @@ def main():
                 seq += 1
             wait_ack(seq - 1)
             dt = time.perf_counter() - t_a
+            dev = None
+            if dev_region:
+                node.sync()
+                reg = node.region_end()
+                iv = sorted(node.pack_intervals(tp_n + 8))
+                busy, end = 0.0, None
+                for a0, b0 in iv:  # union of the packs' intervals, ms
+                    if end is None or a0 > end:
+                        busy += b0 - a0
+                        end = b0
+                    elif b0 > end:
+                        busy += b0 - end
+                        end = b0
+                if reg["packs"]:
+                    dev = {"device_us_per_pack": round(reg["span_ms"] * 1e3 / reg["packs"], 3),
+                           "busy_us_per_pack": round(busy * 1e3 / reg["packs"], 3),
+                           "packs": reg["packs"]}
             # the sink's queue (queue_size 10, the reference default) may drop inputs when it
             # falls behind: only delivered messages count
             dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
@@ -875,7 +897,9 @@ def main():
                                     # Python ladder)
                                     "send_phase_us": {k: round(v, 3) for k, v in phases.items()},
                                     "slots_created": st1["slots_created"] - st0["slots_created"],
-                                    "cache_hits": st1["cache_hits"] - st0["cache_hits"]}
+                                    "cache_hits": st1["cache_hits"] - st0["cache_hits"],
+                                    # from 16 MiB: device span / packs and the packs' busy time
+                                    "device": dev}
             for b in bufs:
                 b.free()
 

@@ -24,6 +24,7 @@ print(json.dumps({"run": sys.argv[2], "value": d["value"], "frac": d["roofline"]
                   "py": {z: us(t, z) for z in ("4096", "1048576", "4194304", "16777216", "40960000")},
                   "native": {z: us(nat, z) for z in ("4096", "1048576", "4096000", "16777216", "40960000")},
                   "lat_p50": {z: d["latency_us"][z]["p50_us"] for z in ("4096", "4194304", "40960000")},
+                  "py_device": {z: (t.get(z) or {}).get("device") for z in ("16777216", "40960000")},
                   "drops": {k: v for k, v in d["sink_dropped_by_phase"].items() if v},
                   "load": d["cpu_share"].get("loadavg_1m")}))
 PY
