@@ -823,6 +823,16 @@ def main():
 
     # ---- throughput ladder (reference throughput mode: back-to-back messages per size) ----
     tp_ladder = {}
+    # Python collections inside a ladder step (diagnosis of the bimodal 40.96 MB step)
+    import gc
+    gc_log, gc_t0 = [], [0.0]
+
+    def gc_cb(phase, info):
+        if phase == "start":
+            gc_t0[0] = time.perf_counter()
+        elif len(gc_log) < 64:
+            gc_log.append((info.get("generation"), (time.perf_counter() - gc_t0[0]) * 1e6))
+    gc.callbacks.append(gc_cb)
     if not args.no_ladder and args.tp_n > 0 and args.workload == "c2":
         for size in [z for z in LADDER_SMALL if z] + LADDER:
             nb = native_sources(size)  # rotated past the L2s / Infinity Cache, as the native ladder
@@ -849,11 +859,18 @@ def main():
             dev_region = size >= (16 << 20) and not args.no_kernel_timing
             if dev_region:
                 node.region_begin()
+            gc_log.clear()
             t_a = time.perf_counter()
+            t_first = t_a
             for k in range(tp_n):  # the last message asks for the ack (no trailing marker)
                 meta = {"seq": seq, "ack": True} if k == tp_n - 1 else {"seq": seq}
                 node.send_output_device_bytes("throughput", bufs[k % nb].ptr, size, meta)
+                if k == 0:
+                    t_first = time.perf_counter()
+                    # the first send's own phases (one call; a slow first send shows where)
+                    first_phases = node.send_profile() if dev_region else None
                 seq += 1
+            t_sent = time.perf_counter()
             wait_ack(seq - 1)
             dt = time.perf_counter() - t_a
             dev = None
@@ -872,7 +889,19 @@ def main():
                 if reg["packs"]:
                     dev = {"device_us_per_pack": round(reg["span_ms"] * 1e3 / reg["packs"], 3),
                            "busy_us_per_pack": round(busy * 1e3 / reg["packs"], 3),
-                           "packs": reg["packs"]}
+                           "packs": reg["packs"],
+                           # host side of the same run: the first send call, the send loop,
+                           # and last send -> ack (the device span explains the rest)
+                           "host_us": {"first_send": round((t_first - t_a) * 1e6, 1),
+                                       "send_loop": round((t_sent - t_a) * 1e6, 1),
+                                       "close": round((t_a + dt - t_sent) * 1e6, 1),
+                                       "total": round(dt * 1e6, 1),
+                                       "device_span": round(reg["span_ms"] * 1e3, 1)},
+                           # Python garbage collections during the run: [generation, us]
+                           "gc": [[g, round(us, 1)] for g, us in gc_log],
+                           "first_send_phases_us": ({k: round(v, 2) for k, v in
+                                                     first_phases.items()}
+                                                    if first_phases else None)}
             # the sink's queue (queue_size 10, the reference default) may drop inputs when it
             # falls behind: only delivered messages count
             dropped = node.dataflow_counters("sink")["dropped_inputs"] - d0
@@ -902,6 +931,8 @@ def main():
                                     "device": dev}
             for b in bufs:
                 b.free()
+    if gc_cb in gc.callbacks:
+        gc.callbacks.remove(gc_cb)
 
     cold_buf.free()
 

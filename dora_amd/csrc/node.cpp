@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -818,12 +819,83 @@ void free_slot(dora_node* n, Slot* s) {
   delete s;
 }
 
+// Slots evicted from a sender's cache are freed by a process-wide thread, not on the send path:
+// hipFree of a 40.96 MB slot took 0.5-1 ms inside the first send after a size change (the
+// eviction happens when returned tokens are handled in alloc_sample), which made one message in
+// two hundred cost a millisecond — the slow mode of bench.py's 40.96 MB ladder step
+// (first_send 0.5-1.0 ms, alloc_us, in profiles/r04_py40_first_send.jsonl).  The sender still
+// waits for the slot's last fill and takes back its fill flag; the thread only destroys the
+// slot's events and frees its memory.  dora_node_free and exit drain it.
+struct SlotReaper {
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<std::pair<int, Slot*>> q;
+  size_t busy = 0;
+  bool started = false;
+
+  void push(int device, Slot* s) {
+    std::unique_lock<std::mutex> g(mu);
+    if (!started) {
+      started = true;
+      std::thread([this] { run(); }).detach();
+      std::atexit([] { reaper().drain(); });  // before HIP's own teardown (registered earlier)
+    }
+    q.emplace_back(device, s);
+    cv.notify_one();
+  }
+  void run() {
+    std::unique_lock<std::mutex> g(mu);
+    for (;;) {
+      cv.wait(g, [this] { return !q.empty(); });
+      auto [dev, s] = q.front();
+      q.pop_front();
+      ++busy;
+      g.unlock();
+      int prev = -1;
+      (void)hipGetDevice(&prev);
+      if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
+      if (s->done) (void)hipEventDestroy(s->done);
+      if (s->use_ev) (void)hipEventDestroy(s->use_ev);
+      (void)hipFree(s->ptr);
+      (void)hipGetLastError();
+      delete s;
+      g.lock();
+      --busy;
+      if (q.empty() && !busy) idle.notify_all();
+    }
+  }
+  void drain() {
+    std::unique_lock<std::mutex> g(mu);
+    idle.wait(g, [this] { return q.empty() && !busy; });
+  }
+  static SlotReaper& reaper() {
+    static SlotReaper* r = new SlotReaper();  // never destroyed: its thread is detached
+    return *r;
+  }
+};
+
+void free_slot_deferred(dora_node* n, Slot* s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(own_slots().mu);
+    own_slots().ptrs.erase(s->id);
+  }
+  if (!wait_slot_idle(n, s)) {  // as free_slot: a fill that never completed keeps its slot
+    std::fprintf(stderr, "dora-gpu: slot %llu: last fill did not complete; not freed\n",
+                 (unsigned long long)s->id);
+    return;
+  }
+  if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
+  s->flag = -1;
+  SlotReaper::reaper().push(n->core->device, s);
+}
+
 void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
   n->cache.push_back(s);
   while (n->cache.size() > kMaxCacheSize) {
     Slot* old = n->cache.front();
     n->cache.pop_front();
-    free_slot(n, old);
+    free_slot_deferred(n, old);
   }
 }
 
@@ -2164,6 +2236,7 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   n->bcast_out.clear();
   for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
   for (auto* s : n->cache) dora::free_slot(n, s);
+  dora::SlotReaper::reaper().drain();  // evicted slots: freed before the node's state goes
   for (auto& e : n->plan_cache) delete e.plan;
   n->plan_cache.clear();
   n->plan_index.clear();
