@@ -85,13 +85,27 @@ struct IpcMapping {
 };
 
 // Mappings a receiver keeps open for reuse (LRU beyond this).  Producers recycle at most
-// kMaxCacheSize (20) slots plus those in flight, so a steady edge stays within it; slots a
-// producer has freed (size changes) age out instead of pinning the producer's memory for good.
-constexpr size_t kMaxIpcMappings = 64;
+// kMaxCacheSlots slots plus those in flight, so a steady edge stays within it; slots a producer
+// has freed (size changes) age out instead of pinning the producer's memory for good.
+constexpr size_t kMaxIpcMappings = 128;
 
 namespace {
 
+// A sender's slot cache (mod.rs:365: 20 entries).  Device slots are HBM, and freeing one costs
+// the sender 0.5-1 ms of hipFree and the GPU a TLB invalidation while its packs run; a sender
+// whose message sizes change (the bench's ladders, variable point clouds) evicted slots at every
+// size change.  So the cache keeps the reference's 20 entries and more, up to kMaxCacheSlots, as
+// long as they hold at most slot_cache_bytes() (DORA_GPU_SLOT_CACHE_BYTES, default 4 GiB of the
+// GPU's 288 GB; 0: the reference's 20 entries); evicted slots are freed off the send path.
 constexpr size_t kMaxCacheSize = 20;          // mod.rs:365
+constexpr size_t kMaxCacheSlots = 64;
+uint64_t slot_cache_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DORA_GPU_SLOT_CACHE_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : uint64_t(4) << 30;
+  }();
+  return v;
+}
 constexpr uint64_t kDropWaitNs = 10000000000;  // 10 s per token on drop (mod.rs:397-426)
 
 struct Slot {
@@ -823,7 +837,9 @@ void free_slot(dora_node* n, Slot* s) {
 // hipFree of a 40.96 MB slot took 0.5-1 ms inside the first send after a size change (the
 // eviction happens when returned tokens are handled in alloc_sample), which made one message in
 // two hundred cost a millisecond — the slow mode of bench.py's 40.96 MB ladder step
-// (first_send 0.5-1.0 ms, alloc_us, in profiles/r04_py40_first_send.jsonl).  The sender still
+// (first_send 0.5-1.0 ms, alloc_us, in profiles/r04_py40_first_send.jsonl).  Freed off the send
+// path, the packs running meanwhile still slowed by ~0.3 us each (the unmapping), hence the
+// larger cache above.  The sender still
 // waits for the slot's last fill and takes back its fill flag; the thread only destroys the
 // slot's events and frees its memory.  dora_node_free and exit drain it.
 struct SlotReaper {
@@ -892,7 +908,14 @@ void free_slot_deferred(dora_node* n, Slot* s) {
 
 void add_to_cache(dora_node* n, Slot* s) {  // mod.rs:364-371
   n->cache.push_back(s);
-  while (n->cache.size() > kMaxCacheSize) {
+  auto over = [n] {
+    if (n->cache.size() <= kMaxCacheSize) return false;
+    if (n->cache.size() > kMaxCacheSlots) return true;
+    uint64_t bytes = 0;
+    for (const Slot* c : n->cache) bytes += c->cap;
+    return bytes > slot_cache_bytes();
+  };
+  while (over()) {
     Slot* old = n->cache.front();
     n->cache.pop_front();
     free_slot_deferred(n, old);
