@@ -749,6 +749,12 @@ def main():
             prev = tenants.get(name, (0, 0))
             tenants[name] = (max(prev[0], t["others"]), max(prev[1], t["other_queues"]))
 
+    # Python's cyclic collector is paused from here to the end of the measurements, as timeit
+    # does: a collection is the harness's pause, not the data plane's (a gen-0 collection of
+    # ~40 us between two sends of the C3 burst took it from 0.74 to 0.53 once)
+    import gc as _gc
+    _gc.collect()
+    _gc.disable()
     copy_cal = box_copy_rate(S, stream)
     # the same at the mid sizes, where per-message dispatch rather than HBM binds
     copy_mid = {str(z): box_copy_rate(z, stream) for z in (4 << 20, 16 << 20)
@@ -1166,6 +1172,8 @@ def main():
             "latency_us": {str(s["size"]): {"p50_us": s["p50_us"], "p99_us": s["p99_us"]}
                            for s in base["series"] if s["mode"] == "latency"},
             "wall_s": base["wall_s"], "nproc": base["nproc"], "cores_used": base["cores"]}
+    import gc as _gc
+    _gc.enable()
     line["sink_dropped_by_phase"] = drops
     # (other processes, their queues) on this GPU at each phase's end, when KFD sysfs is readable
     line["gpu_tenants_by_phase"] = {k: list(v) for k, v in tenants.items()}
