@@ -29,6 +29,7 @@
 #include <memory>
 #include <memory_resource>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <set>
 #include <sstream>
@@ -855,6 +856,16 @@ struct SlotReaper {
       started = true;
       std::thread([this] { run(); }).detach();
       std::atexit([] { reaper().drain(); });  // before HIP's own teardown (registered earlier)
+      // a forked child has no reaper thread: it starts its own, and forgets the parent's queue
+      pthread_atfork(nullptr, nullptr, [] {
+        SlotReaper& r = reaper();
+        new (&r.mu) std::mutex();
+        new (&r.cv) std::condition_variable();
+        new (&r.idle) std::condition_variable();
+        r.q.clear();
+        r.busy = 0;
+        r.started = false;
+      });
     }
     q.emplace_back(device, s);
     cv.notify_one();
