@@ -57,11 +57,12 @@ uint32_t env_u32(const char* name) {
 }
 // workgroups of a signalling launch (0: kSignalGrid; DORA_GPU_SIGNAL_GRID, dora_gpu_pack_tune)
 std::atomic<uint32_t> g_signal_grid{env_u32("DORA_GPU_SIGNAL_GRID")};
-// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 4096:
-// a lone 40.96 MB pack, 5,000 chunks, takes 14.05 us with 4096 workgroups against 14.84-14.92
-// with one per chunk and 15.5 with 2048, profiles/r04_sync_ab.jsonl; packs below 32 MiB have
-// fewer chunks than that)
-std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 4096u};
+// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 3584:
+// a synchronous 40.96 MB send (5,000 chunks) takes 21.7-22.0 us with 3584 workgroups against
+// 22.0-22.7 with 4096, 22.9 with one per chunk, 22.7-23.3 with 3072 and 24.6-25.3 with fewer,
+// larger chunks, in four interleaved rounds of 200 sends, profiles/r04_sync_ab.jsonl batches
+// sy4-sy6; packs below 28 MiB have fewer chunks than that)
+std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 3584u};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
