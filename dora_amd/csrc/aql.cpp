@@ -540,17 +540,19 @@ std::pair<uint64_t, uint64_t> cp_signal_window() {
   return v;
 }
 
-// DORA_GPU_AQL_CP_LONE=0: a single-segment pack above the CP window stays in-kernel-signalled
-// even when it runs alone (sync sends, idle queues).  DORA_GPU_AQL_CP_BIG=1: such packs are
-// CP-signalled even when others run beside them (an A/B knob for the pipelined headline).
-// DORA_GPU_AQL_CP_LONE=sync: only synchronous sends count as lone (not a pack that merely
-// finds the queues idle).
+// Which lone packs above the CP window are signalled by the command processor (with the CP
+// grid): synchronous sends only (default, DORA_GPU_AQL_CP_LONE=sync), also async sends that find
+// every queue idle (`idle`), or none (`0`).  An async send that finds the queues idle usually
+// opens a burst: given the whole GPU (3584 workgroups) it delays the packs queued right behind
+// it, and the 20-step headline lost 0.8 % (0.778 vs 0.786 mean over six interleaved rounds,
+// profiles/r04_headline20_ab.jsonl).  DORA_GPU_AQL_CP_BIG=1: such packs are CP-signalled even
+// when others run beside them (an A/B knob for the pipelined headline).
 int cp_lone_mode() {
   static const int v = [] {
     const char* e = std::getenv("DORA_GPU_AQL_CP_LONE");
     if (e && *e == '0') return 0;
-    if (e && std::string(e) == "sync") return 1;
-    return 2;
+    if (e && (std::string(e) == "idle" || *e == '2')) return 2;
+    return 1;
   }();
   return v;
 }
@@ -1066,8 +1068,11 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // Signalled by the command processor (inside a timed region only with a stamp area for the
   // pack's own stamps): a pack in the window, and a single-segment pack above it that runs alone
   // — sent synchronously, or finding every queue idle (aql.h).
-  p.lone = cp_lone_mode() > 0 && (sync || (cp_lone_mode() == 2 && queues_idle(a)));
-  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, p.lone || cp_big());
+  // lone: runs alone on the GPU (a synchronous send, or every queue idle): its arguments go to
+  // the device ring and it reads without the acquire fence (dispatch_locked)
+  p.lone = sync || queues_idle(a);
+  const bool cp_lone = cp_lone_mode() == 2 ? p.lone : cp_lone_mode() == 1 && sync;
+  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, cp_lone || cp_big());
   // a synchronous single-segment send returns on its pack's read signal (DORA_GPU_AQL_READ_SIGNAL=0:
   // on the fill), when the pack leaves at once (not from the backlog or in a batch)
   p.read_signal = sync && p.cp && n == 1 && segs[0].dst_off == 0 && !cp_stamps && read_signal &&
