@@ -39,9 +39,10 @@ bool aql_usable(const AqlQueue* q);
 //
 // `sync`: the caller waits for this pack before it does anything else (a synchronous send,
 // node.cpp wait_source_read).  A single-segment pack that is sent synchronously, or that finds
-// every queue idle, runs alone on the GPU: it is signalled by the command processor at any size
-// >= the CP window's lower bound, with a grid of up to DORA_GPU_CP_GRID workgroups (no done words to
-// poll, so no 1024-workgroup signalling cap).
+// every queue idle, runs alone on the GPU: its arguments go to the device ring and it reads
+// without the acquire fence; a synchronous one (DORA_GPU_AQL_CP_LONE) is also signalled by the
+// command processor at any size >= the CP window's lower bound, with a grid of up to
+// DORA_GPU_CP_GRID workgroups (no done words to poll, so no 1024-workgroup signalling cap).
 // Would a pack of these segments be signalled by the command processor when sent alone
 // (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI; `lone`: also a lone big pack)?
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
