@@ -144,6 +144,53 @@ def test_slots_recycle_through_drop_tokens(launcher, tmp_path):
     assert stats["cache_hits"] >= 60, stats
 
 
+def test_slot_cache_keeps_many_sizes(launcher, tmp_path):
+    """r04: a sender whose message sizes change keeps its slots (up to 64 within 4 GiB, node.cpp
+    slot_cache_bytes) instead of the reference's 20, so cycling through 30 sizes (30 slot
+    capacities) a second and a third time creates no slot (the 20-entry cache evicted and
+    re-created them on every pass: hipFree inside a send), and every delivered payload is still
+    bit-exact."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    from dora_amd.verify import to_i64
+    res = str(tmp_path / "sink.json")
+    sizes = [(2 * k + 1) << 20 for k in range(30)]  # 1..59 MiB: 30 slots of 2..60 MiB, 930 MiB
+    src = device.DeviceBuffer(sizes[-1])
+    s = device.Stream()
+    device.fill_splitmix(src.ptr, src.size, 0x51075, s)
+    sums = {z: to_i64(device.csum64(src.ptr, z, s)) for z in sizes}
+    s.close()
+    created = []
+    with Dataflow(_bench_desc(res), launcher=launcher) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        seq = 0
+        for rnd in range(3):
+            before = node.stats()["slots_created"]
+            for z in sizes:
+                node.send_output_device_bytes("data", src.ptr, z,
+                                              {"seq": seq, "csum": sums[z], "verify": True})
+                seq += 1
+                time.sleep(0.002)  # the token comes back: each send finds its best fit free
+            node.send_output("data", b"", {"seq": seq, "ack": True})
+            node.wait_input("ack", "seq", seq, 60.0)
+            seq += 1
+            created.append(node.stats()["slots_created"] - before)
+        node.close()
+        codes = df.wait(60)
+        log = df.log("sink")
+    src.free()
+    assert codes["sink"] == 0, log
+    out = json.load(open(res))
+    assert out["errors"] == 0
+    assert sum(x["verified"] for x in out["series"]) == 3 * len(sizes)
+    assert sum(x["mismatches"] for x in out["series"]) == 0
+    # round 1 creates the 30 slots; the 20-entry cache had to re-create at least 10 per later
+    # round, now none (a token late by more than the 2 ms pause could cost one)
+    assert created[0] >= 30, created
+    assert created[1] <= 1 and created[2] <= 1, created
+
+
 def test_python_receiver_c3_point_clouds(launcher):
     from dora_amd.dataflow import Dataflow
     from dora_amd.device import DeviceArray
