@@ -36,6 +36,9 @@ LADDER = [4096, 16384, 40960, 65536, 409600, 1 << 20, 4096000, 4 << 20, 16 << 20
 # the rest of the reference ladder (examples/benchmark/node/src/main.rs:11-21): sizes the
 # reference sends inline (< 4096 B, DataMessage::Vec); a device node sends them in slots too
 LADDER_SMALL = [0, 8, 64, 512, 2048]
+# host-resident sources of the latency ladder (output `latency_host`): below 4096 B they travel
+# inline as the reference's DataMessage::Vec (no slot, no GPU), 4096 B is an H2D device sample
+LADDER_HOST = [8, 512, 2048, 4096]
 
 
 def parse():
@@ -666,10 +669,11 @@ def main():
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
     desc = {"nodes": [
-        {"id": "node", "path": "dynamic", "outputs": ["latency", "throughput"],
+        {"id": "node", "path": "dynamic", "outputs": ["latency", "latency_host", "throughput"],
          "inputs": {"ack": "sink/ack"}, "_unstable_deploy": {"gpu": local_rank}},
         {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
          "inputs": {"latency": {"source": "node/latency", "queue_size": 10},
+                    "latency_host": {"source": "node/latency_host", "queue_size": 10},
                     "throughput": {"source": "node/throughput", "queue_size": 10}},
          "env": dict({"DORA_BENCH_RESULT": result_path}, **SINK_ENV),
          "_unstable_deploy": {"gpu": local_rank}},
@@ -817,6 +821,18 @@ def main():
             for _ in range(args.lat_n):
                 node.send_output_device_bytes("latency", ladder_bufs[size].ptr, size,
                                               {"seq": seq, "t_start": time.time_ns()})
+                seq += 1
+                time.sleep(args.lat_gap_us / 1e6)
+        # host-resident sources (bytes objects): the reference's own latency case, whose sources
+        # are host memory (examples/benchmark/node/src/main.rs:38-70)
+        host_src = {z: bytes(range(256)) * (z // 256) + bytes(z % 256) for z in LADDER_HOST}
+        for size in LADDER_HOST:
+            node.send_output("throughput", host_src[size], {"seq": seq})  # untimed, once
+            seq += 1
+            time.sleep(args.lat_gap_us / 1e6)
+            for _ in range(args.lat_n):
+                node.send_output("latency_host", host_src[size],
+                                 {"seq": seq, "t_start": time.time_ns()})
                 seq += 1
                 time.sleep(args.lat_gap_us / 1e6)
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
@@ -1077,10 +1093,11 @@ def main():
     traffic = pmc_traffic(S)
     lat = {}
     for s in sink.get("series", []):
-        if s["input"] == "latency":
-            lat[str(s["size"])] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
-                                   "p50_incl_pack_us": s["full_p50_us"],
-                                   "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
+        if s["input"] in ("latency", "latency_host"):
+            key = str(s["size"]) if s["input"] == "latency" else f"host_{s['size']}"
+            lat[key] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
+                        "p50_incl_pack_us": s["full_p50_us"],
+                        "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
     c2_series = [s for s in sink.get("series", []) if c3 is None or s["size"] != c3["msg_bytes"]]
     verified = sum(s["verified"] for s in c2_series)
     mismatches = sum(s["mismatches"] for s in c2_series)
@@ -1202,7 +1219,7 @@ def compact_line(line, detail_path):
                                 "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
                                 "dtype", "data") if k in line}
     cfg = line.get("config", {})
-    out["config"] = {"workload": cfg.get("workload", "")[:40], "msg_bytes": cfg.get("msg_bytes"),
+    out["config"] = {"workload": cfg.get("workload", ""), "msg_bytes": cfg.get("msg_bytes"),
                      "parallelism": cfg.get("parallelism")}
     r = line.get("roofline", {})
     out["roofline"] = dict(_pick(r, "bound", "achieved", "peak", "unit", "frac", "traffic",
@@ -1234,7 +1251,8 @@ def compact_line(line, detail_path):
                            "by_phase": {k: v for k, v in drops.items() if v}}
     lat = line.get("latency_us") or {}
     out["latency_summary"] = {z: [lat[z]["p50_us"], lat[z]["p99_us"], lat[z]["p99_incl_pack_us"]]
-                              for z in ("4096", "4194304", "40960000") if z in lat}
+                              for z in ("host_8", "host_2048", "8", "4096", "4194304",
+                                        "40960000") if z in lat}
     out["latency_summary_keys"] = "size: [p50, p99, p99 incl. pack] us"
     ten = line.get("gpu_tenants_by_phase")
     if ten:  # the most other processes seen on this GPU at any phase's end

@@ -476,7 +476,7 @@ class Daemon {
     ++routed_;
     TokenInfo* ti = nullptr;
     if (data.has_token()) {  // inserted even with no local receivers
-      ti = &tokens_[data.ipc.token];
+      ti = &tokens_[data.token()];
       ti->owner = i;
     }
     auto it = outputs_[i].find(output);
@@ -489,7 +489,7 @@ class Daemon {
         ev_buf_.raw(tail, tail_len);
         push_event_raw(rc.node, EV_INPUT, ev_buf_.data(), ev_buf_.size());
         if (ti) {
-          trace(TP_ROUTED, data.ipc.token);
+          trace(TP_ROUTED, data.token());
           ti->add(rc.node);
         }
       }
@@ -507,7 +507,7 @@ class Daemon {
       if (ti) ti->add(kForwarder);
       fwd_->push(std::move(job));
     }
-    if (ti) check_drop_token(data.ipc.token);
+    if (ti) check_drop_token(data.token());
   }
 
   // REQ_BCAST_GROUP (bcast.h): admit an RCCL group for output `output` of node `i` when every

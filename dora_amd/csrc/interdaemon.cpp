@@ -28,6 +28,7 @@ namespace dora {
 // node.cpp: send a sample with the producer's original timestamp (the remote message's).
 int proxy_send(dora_node* n, const char* output_id, const uint8_t* ti, size_t ti_len,
                const uint8_t* params, size_t params_len, dora_sample* sample, uint64_t ts);
+dora_sample* vec_sample(const uint8_t* p, size_t len);
 
 namespace {
 
@@ -306,6 +307,20 @@ void Forwarder::handle(ForwardJob& job) {
     if (job.data.kind == DATA_VEC) {
       e.has_data = true;
       e.data = std::move(job.data.vec);
+    } else if (job.data.kind == DATA_SHMEM) {
+      // a host-only node's shared-memory sample: copied out, then the token goes back
+      e.has_data = true;
+      const bool ok = read_shmem(job.data.shm.name, job.data.shm.len, &e.data);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        released_.push_back(job.data.shm.token);
+      }
+      if (!ok) {
+        std::fprintf(stderr, "dora-gpu daemon: could not read shared-memory sample `%s` of "
+                             "`%s/%s` for remote receivers; dropped\n",
+                     job.data.shm.name.c_str(), job.node_id.c_str(), job.output_id.c_str());
+        return;
+      }
     } else if (job.data.kind == DATA_DEVICE_IPC) {
       e.has_data = true;
       const bool ok = stage(job, &e.data, &e.type_info);
@@ -541,7 +556,9 @@ void Gateway::proxy_loop(Proxy* p) {
     }
     dora_sample* s = nullptr;
     int rc = DORA_OK;
-    if (e.has_data && !e.data.empty()) {
+    if (e.has_data && !e.data.empty() && e.data.size() < 4096) {
+      s = vec_sample(e.data.data(), e.data.size());  // below the zero-copy threshold: inline
+    } else if (e.has_data && !e.data.empty()) {
       rc = dora_node_allocate_data_sample(n, e.data.size(), &s);
       if (rc == DORA_OK) {
         void* dst = dora_sample_data(s);

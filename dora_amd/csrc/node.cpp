@@ -85,6 +85,20 @@ struct IpcMapping {
   }
 };
 
+// A host-only producer's shared-memory sample region as mapped here (DataMessage::SharedMemory),
+// shared like IpcMapping.  A device receiver registers it with HIP once, so its pull into HBM is a
+// DMA from pinned pages rather than a staged copy.
+struct ShmMapping {
+  void* base = nullptr;
+  size_t len = 0;
+  bool registered = false;
+  uint64_t last_use = 0;
+  ~ShmMapping() {
+    if (registered) (void)hipHostUnregister(base);
+    shmem_unmap(base, len);
+  }
+};
+
 // Mappings a receiver keeps open for reuse (LRU beyond this).  Producers recycle at most
 // kMaxCacheSlots slots plus those in flight, so a steady edge stays within it; slots a producer
 // has freed (size changes) age out instead of pinning the producer's memory for good.
@@ -128,7 +142,23 @@ struct Slot {
   // recorded after it, waited on before the slot is reused or freed
   hipEvent_t use_ev = nullptr;
   bool use_pending = false;
+  // host-only node: a POSIX shared-memory region (DataMessage::SharedMemory) instead of HBM
+  bool host = false;
+  std::string shm_name;
 };
+
+// The memory of a slot no fill can still write (its events, its HBM or shared-memory region).
+void release_slot_memory(Slot* s) {
+  if (s->host) {
+    shmem_unmap(s->ptr, s->cap);
+    shmem_unlink(s->shm_name);
+  } else {
+    if (s->done) (void)hipEventDestroy(s->done);
+    if (s->use_ev) (void)hipEventDestroy(s->use_ev);
+    (void)hipFree(s->ptr);
+  }
+  delete s;
+}
 
 // Async sends (default): the sender records the slot's interprocess event after the pack and
 // sends at once; the receiver waits on that event before handing the input out.  Sync sends
@@ -415,6 +445,43 @@ struct NodeCore {
       ipc_closes.fetch_add(1, std::memory_order_relaxed);
     }
   }
+  // shared-memory region name -> mapping (host-only producers' samples); bounded like ipc_cache
+  std::unordered_map<std::string, std::shared_ptr<ShmMapping>> shm_cache;
+
+  std::shared_ptr<ShmMapping> map_shmem(const std::string& name, uint64_t len, std::string* err) {
+    std::lock_guard<std::mutex> g(ipc_mu);
+    auto it = shm_cache.find(name);
+    std::shared_ptr<ShmMapping> m;
+    if (it != shm_cache.end()) {
+      m = it->second;
+    } else {
+      m = std::make_shared<ShmMapping>();
+      m->base = shmem_open(name, &m->len);
+      if (!m->base) {
+        *err = "shared-memory sample `" + name + "`: " + std::strerror(errno);
+        return nullptr;
+      }
+      if (device >= 0)
+        m->registered = hipHostRegister(m->base, m->len, hipHostRegisterDefault) == hipSuccess;
+      (void)hipGetLastError();
+      shm_cache.emplace(name, m);
+      while (shm_cache.size() > kMaxIpcMappings) {
+        auto victim = shm_cache.end();
+        for (auto v = shm_cache.begin(); v != shm_cache.end(); ++v)
+          if (v->second.use_count() == 1 &&
+              (victim == shm_cache.end() || v->second->last_use < victim->second->last_use))
+            victim = v;
+        if (victim == shm_cache.end()) break;
+        shm_cache.erase(victim);
+      }
+    }
+    if (len > m->len) {
+      *err = "shared-memory sample `" + name + "` is shorter than its message";
+      return nullptr;
+    }
+    m->last_use = ++ipc_clock;
+    return m;
+  }
   std::unordered_map<std::string, hipEvent_t> ipc_events;  // event handle bytes -> opened event
   // fill flags: the region is host-registered so the stream can write epochs into it
   uint8_t* region_dev = nullptr;
@@ -607,6 +674,9 @@ struct InputData {
   uint64_t local_cap = 0;
   int remote_device = -1;     // >= 0: `ptr` is a peer GPU's slot not yet pulled (ensure_local)
   hipEvent_t bcast_ev = nullptr;  // broadcast group input: completion of its receive into `local`
+  std::shared_ptr<ShmMapping> shm;  // a host-only producer's shared-memory sample, mapped here
+  bool host_mem = false;   // host receiver: `ptr` is the shared memory itself (read in place)
+  bool host_pull = false;  // device receiver: `ptr` is shared memory not yet pulled into HBM
   ~InputData() {
     if (!core) return;
     if (bcast_ev) {
@@ -828,10 +898,7 @@ void free_slot(dora_node* n, Slot* s) {
     return;
   }
   if (s->flag >= 0) n->core->free_flags.push_back(static_cast<uint32_t>(s->flag));
-  if (s->done) (void)hipEventDestroy(s->done);
-  if (s->use_ev) (void)hipEventDestroy(s->use_ev);
-  (void)hipFree(s->ptr);
-  delete s;
+  release_slot_memory(s);
 }
 
 // Slots evicted from a sender's cache are freed by a process-wide thread, not on the send path:
@@ -881,11 +948,8 @@ struct SlotReaper {
       int prev = -1;
       (void)hipGetDevice(&prev);
       if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
-      if (s->done) (void)hipEventDestroy(s->done);
-      if (s->use_ev) (void)hipEventDestroy(s->use_ev);
-      (void)hipFree(s->ptr);
+      release_slot_memory(s);
       (void)hipGetLastError();
-      delete s;
       g.lock();
       --busy;
       if (q.empty() && !busy) idle.notify_all();
@@ -969,12 +1033,12 @@ uint64_t slot_bytes(uint64_t len) {
   return (std::max<uint64_t>(len, 1) + kSlotGrain - 1) / kSlotGrain * kSlotGrain;
 }
 
-int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
-  // best fit among cached slots (mod.rs:321-346 `.rev()...min_by_key`); among slots of equal
-  // capacity the oldest returned one, whose last fill has had the longest to complete and whose
-  // flag line on_token has prefetched (the reference takes the newest; any fit is equivalent)
+// Best fit among cached slots (mod.rs:321-346 `.rev()...min_by_key`); among slots of equal
+// capacity the oldest returned one, whose last fill has had the longest to complete and whose
+// flag line on_token has prefetched (the reference takes the newest; any fit is equivalent).
+// `need`: the smallest capacity a new slot of `len` would have (an exact fit ends the search).
+int best_fit(dora_node* n, uint64_t len, uint64_t need) {
   int best = -1;
-  const uint64_t need = slot_bytes(len);  // the smallest capacity a slot can have
   for (int i = 0; i < static_cast<int>(n->cache.size()); ++i) {
     Slot* s = n->cache[static_cast<size_t>(i)];
     if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) {
@@ -982,6 +1046,11 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
       if (s->cap == need) break;  // an exact fit: no later slot fits better
     }
   }
+  return best;
+}
+
+int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
+  const int best = best_fit(n, len, slot_bytes(len));
   if (best >= 0) {
     Slot* s = n->cache[static_cast<size_t>(best)];
     n->cache.erase(n->cache.begin() + best);
@@ -1024,6 +1093,37 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   {
     std::lock_guard<std::mutex> g(own_slots().mu);
     own_slots().ptrs[s->id] = s->ptr;
+  }
+  ++n->slots_created;
+  n->core->region->hdr()->nodes[n->core->idx].slots_created.fetch_add(1, std::memory_order_relaxed);
+  *out = s;
+  return DORA_OK;
+}
+
+// A host-only node's sample >= 4096 B (mod.rs:321-346): best fit from the slot cache, else a
+// new POSIX shared-memory region of whole pages.  The node writes it with the CPU (as the
+// reference's copy_array_into_sample); device receivers pull it into HBM by DMA.
+int allocate_host_slot(dora_node* n, uint64_t len, Slot** out) {
+  constexpr uint64_t kPage = 4096;
+  const uint64_t need = (std::max<uint64_t>(len, 1) + kPage - 1) / kPage * kPage;
+  const int best = best_fit(n, len, need);
+  if (best >= 0) {
+    *out = n->cache[static_cast<size_t>(best)];
+    n->cache.erase(n->cache.begin() + best);
+    ++n->cache_hits;
+    return DORA_OK;
+  }
+  auto* s = new Slot();
+  s->host = true;
+  s->cap = need;
+  s->id = own_slots().next_id.fetch_add(1);
+  s->shm_name = "/dora-gpu-s-" + std::to_string(self_pid()) + "-" + std::to_string(s->id);
+  s->ptr = shmem_create(s->shm_name, s->cap);
+  if (!s->ptr) {
+    const int err = errno;
+    delete s;
+    return fail(DORA_ERR_INVALID, "shared-memory sample of %llu bytes: %s",
+                (unsigned long long)len, std::strerror(err));
   }
   ++n->slots_created;
   n->core->region->hdr()->nodes[n->core->idx].slots_created.fetch_add(1, std::memory_order_relaxed);
@@ -1114,6 +1214,21 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
         in->ptr = in->vec.data();
         in->len = in->vec.size();
         in->ext_len = in->len;
+      } else if (d.kind == DATA_SHMEM) {
+        // a host-only node's sample: read in place by a host receiver, pulled into HBM by DMA
+        // on first access by a device receiver (ensure_local)
+        in->has_token = true;
+        in->token = d.shm.token;
+        in->len = in->ext_len = d.shm.len;
+        std::string err;
+        in->shm = n->core->map_shmem(d.shm.name, d.shm.len, &err);
+        if (!in->shm) {
+          ev->type = DORA_EVENT_ERROR;
+          ev->error = err;
+        } else {
+          in->ptr = in->shm->base;
+          (n->core->device >= 0 ? in->host_pull : in->host_mem) = true;
+        }
       } else if (d.kind == DATA_DEVICE_IPC) {
         in->has_token = true;  // set first: a mapping failure still returns the token
         in->token = d.ipc.token;
@@ -1342,14 +1457,19 @@ int enqueue_peer_copy(NodeCore* c, void* dst, const void* src, int src_device, u
 // Pull a cross-GPU input into this node's receive pool (complete on return) and hand the
 // producer its slot back at once.
 int ensure_local(InputData* in) {
-  if (!in || in->remote_device < 0) return DORA_OK;
+  if (!in || (in->remote_device < 0 && !in->host_pull)) return DORA_OK;
   NodeCore* c = in->core.get();
   uint64_t cap = 0;
   void* local = c->recv_pool_get(in->ext_len, &cap);
   if (!local)
     return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->ext_len);
-  int rc;
-  if (peer_copy_mode() == PEER_SDMA) {
+  int rc = DORA_OK;
+  if (in->host_pull) {
+    // a host-only producer's shared memory (registered here): one DMA into HBM
+    hipError_t e = hipMemcpyAsync(local, in->ptr, in->ext_len, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "shared-memory pull: %s", hipGetErrorString(e));
+  } else if (peer_copy_mode() == PEER_SDMA) {
     rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->ext_len);
     if (rc == DORA_OK) {
       hipError_t e = hipStreamSynchronize(c->stream);
@@ -1368,10 +1488,15 @@ int ensure_local(InputData* in) {
   in->local = local;
   in->local_cap = cap;
   in->ptr = local;
-  in->remote_device = -1;
   c->report_drop_token(in->token);
   trace(TP_RELEASED, in->token);
   in->has_token = false;
+  if (in->host_pull) {
+    in->host_pull = false;
+    in->shm.reset();
+    return DORA_OK;
+  }
+  in->remote_device = -1;
   c->peer_copies.fetch_add(1, std::memory_order_relaxed);
   c->peer_bytes.fetch_add(in->ext_len, std::memory_order_relaxed);
   return DORA_OK;
@@ -1479,7 +1604,13 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
   DataMsg d;
   Slot* slot = nullptr;
   if (sample) {
-    if (sample->slot) {
+    if (sample->slot && sample->slot->host) {
+      slot = sample->slot;
+      d.kind = DATA_SHMEM;
+      d.shm.name = slot->shm_name;
+      d.shm.len = sample->len;
+      d.shm.token = generate_drop_token();
+    } else if (sample->slot) {
       slot = sample->slot;
       d.kind = DATA_DEVICE_IPC;
       std::memcpy(d.ipc.handle, &slot->handle, 64);
@@ -1536,7 +1667,10 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     return rc;
   }
   SubSpan sp_track(SP_SEND_TRACK);
-  if (slot) {
+  if (slot && d.kind == DATA_SHMEM) {
+    n->sent_out[d.shm.token] = slot;
+    if (token_out) *token_out = d.shm.token;
+  } else if (slot) {
     n->sent_out[d.ipc.token] = slot;
     if (d.ipc.fill == FILL_FLAG) {
       auto& t = n->transit;
@@ -1603,15 +1737,25 @@ void ensure_cp_stamps(dora_node* n) {
   }
 }
 
-int alloc_sample(dora_node* n, uint64_t len, dora_sample** out,
-                 uint64_t ext_len = 0) {  // mod.rs:303-319
-  if (n->core->device < 0) {
-    // host-only node (no GPU): only the reference's inline `DataMessage::Vec` path exists
-    if (len >= kZeroCopyThreshold)
-      return fail(DORA_ERR_INVALID,
-                  "host-only node cannot allocate a %llu-byte sample: samples >= %llu bytes live "
-                  "in HBM slots",
-                  (unsigned long long)len, (unsigned long long)kZeroCopyThreshold);
+// `host_inline`: the sample will be written by the host (a host-resident source), so below the
+// zero-copy threshold it takes the reference's inline `DataMessage::Vec` (mod.rs:303-319) on a
+// device node too: no slot, no H2D copy, no fill signal.
+int alloc_sample(dora_node* n, uint64_t len, dora_sample** out, uint64_t ext_len = 0,
+                 bool host_inline = false) {  // mod.rs:303-319
+  if (n->core->device < 0 && len >= kZeroCopyThreshold) {
+    // host-only node: a POSIX shared-memory slot (the reference's allocate_shared_memory)
+    auto* s = new dora_sample();
+    s->len = len;
+    handle_finished_drop_tokens(n);
+    int rc = allocate_host_slot(n, len, &s->slot);
+    if (rc != DORA_OK) {
+      delete s;
+      return rc;
+    }
+    *out = s;
+    return DORA_OK;
+  }
+  if (n->core->device < 0 || (host_inline && std::max(len, ext_len) < kZeroCopyThreshold)) {
     auto* s = new dora_sample();
     s->len = len;
     s->vec.assign(len, 0);  // AVec::__from_elem(128, 0, len)
@@ -1863,22 +2007,26 @@ int forward_in_place(dora_node* n, const char* output_id, const dora_event* ev,
 int forward_input(dora_node* n, const char* output_id, const dora_event* ev, const uint8_t* params,
                   size_t params_len) {
   InputData* in = ev->data.get();
-  if (in->has_token && !in->local && in->remote_device < 0 && in->len &&
+  if (in->host_pull) {  // a shared-memory input of a device receiver: into HBM first
+    int rc = ensure_local(in);
+    if (rc != DORA_OK) return rc;
+  }
+  if (in->has_token && !in->local && in->remote_device < 0 && in->len && !in->host_mem &&
       ev->ipc.device == n->core->device && ev->ipc.fill != FILL_BCAST && !edge_copy_forced() &&
       !forward_copy_forced() && !n->bcast_out.count(output_id))
     return forward_in_place(n, output_id, ev, params, params_len);
   const uint64_t len = in->len;
   const uint64_t ext = std::max(in->ext_len, len);  // the validity tail travels along
+  const bool device_src = (in->has_token || in->local) && !in->host_mem;
   dora_sample* s = nullptr;
-  int rc = alloc_sample(n, len, &s, ext);
+  int rc = alloc_sample(n, len, &s, ext, !device_src);
   if (rc != DORA_OK) return rc;
-  const bool device_src = in->has_token || in->local;
-  if (len && !s->slot) {
+  if (len && (!s->slot || s->slot->host)) {
     if (device_src) {
-      delete s;
+      dora_sample_discard(n, s);
       return fail(DORA_ERR_INVALID, "host-only node cannot forward device-resident data");
     }
-    std::memcpy(s->vec.data(), in->ptr, len);
+    std::memcpy(s->slot ? s->slot->ptr : s->vec.data(), in->ptr, len);
   } else if (len) {
     Segment seg{in->ptr, 0, ext};
     if (in->remote_device >= 0 && peer_copy_mode() == PEER_SDMA) {
@@ -2003,17 +2151,22 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
                   uint32_t flags = 0) {
   dora_sample* s = nullptr;
   const uint64_t t0 = mono_ns();
-  int rc = alloc_sample(n, plan->size, &s, plan->fill_size());
+  // a host-resident array below the zero-copy threshold goes inline, as in the reference
+  const bool host_src = plan->dev != ARROW_DEVICE_ROCM;
+  int rc = alloc_sample(n, plan->size, &s, plan->fill_size(), host_src);
   if (rc != DORA_OK) return rc;
   const uint64_t t1 = mono_ns();
   uint64_t t2 = t1, t3 = t1;
-  if (plan->size && !s->slot) {
-    // host-only node: small host payload copied into the inline Vec (arrow_utils.rs:48)
-    if (plan->dev == ARROW_DEVICE_ROCM) {
-      delete s;
+  if (plan->size && (!s->slot || s->slot->host)) {
+    // an inline Vec or a host-only node's shared-memory slot: the host copies the buffers
+    // (copy_array_into_sample, arrow_utils.rs:48)
+    if (!host_src) {
+      dora_sample_discard(n, s);
       return fail(DORA_ERR_INVALID, "host-only node cannot send device-resident data");
     }
-    for (const Segment& g : plan->segs) std::memcpy(s->vec.data() + g.dst_off, g.src, g.len);
+    uint8_t* dst = s->slot ? static_cast<uint8_t*>(s->slot->ptr) : s->vec.data();
+    for (const Segment& g : plan->segs) std::memcpy(dst + g.dst_off, g.src, g.len);
+    t2 = t3 = mono_ns();
   } else if (plan->size) {
     // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
     // every `timing_sample()`-th pack is stamped (DORA_GPU_TIMING_SAMPLE, default 8).
@@ -2090,6 +2243,16 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
 }
 
 }  // namespace
+
+// An inline Vec sample holding `len` host bytes: a remote node's small message, delivered as the
+// reference's receiving daemon delivers remote data (`data.map(DataMessage::Vec)`,
+// binaries/daemon/src/lib.rs:567), with no slot and no upload.
+dora_sample* vec_sample(const uint8_t* p, size_t len) {
+  auto* s = new dora_sample();
+  s->len = len;
+  s->vec.assign(p, p + len);
+  return s;
+}
 
 // A remote node's message re-sent by its proxy (interdaemon.cpp): the metadata keeps the
 // producer's timestamp.
@@ -2538,7 +2701,7 @@ int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
 }
 
 int dora_event_is_device(const dora_event* e) {
-  return e && e->data && (e->data->has_token || e->data->local);
+  return e && e->data && (e->data->has_token || e->data->local) && !e->data->host_mem;
 }
 
 int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
@@ -2582,7 +2745,8 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
   if (rc != DORA_OK) return rc;
   DORA_GUARD_END
   std::shared_ptr<void> keep = e->data;
-  if (!e->data->has_token && !e->data->local)  // inline Vec sample: a host array over its bytes
+  // an inline Vec sample, or shared memory read in place: a host array over its bytes
+  if (e->data->host_mem || (!e->data->has_token && !e->data->local))
     return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
                                e->meta.type_info.size(), keep, out_array, out_schema, 0, true);
   return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),

@@ -240,6 +240,55 @@ void Region::unlink() {
   }
 }
 
+void* shmem_create(const std::string& name, size_t len) {
+  const int fd = ::shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) return nullptr;
+  void* p = MAP_FAILED;
+  if (::ftruncate(fd, off_t(len)) == 0)
+    p = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  const int err = errno;
+  ::close(fd);
+  if (p == MAP_FAILED) {
+    ::shm_unlink(name.c_str());
+    errno = err;
+    return nullptr;
+  }
+  return p;
+}
+
+void* shmem_open(const std::string& name, size_t* len) {
+  const int fd = ::shm_open(name.c_str(), O_RDWR, 0);
+  if (fd < 0) return nullptr;
+  struct stat st {};
+  void* p = MAP_FAILED;
+  if (::fstat(fd, &st) == 0 && st.st_size > 0)
+    p = ::mmap(nullptr, size_t(st.st_size), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  const int err = errno;
+  ::close(fd);
+  if (p == MAP_FAILED) {
+    errno = err;
+    return nullptr;
+  }
+  *len = size_t(st.st_size);
+  return p;
+}
+
+void shmem_unmap(void* p, size_t len) {
+  if (p) ::munmap(p, len);
+}
+
+void shmem_unlink(const std::string& name) { ::shm_unlink(name.c_str()); }
+
+bool read_shmem(const std::string& name, uint64_t len, std::vector<uint8_t>* out) {
+  size_t cap = 0;
+  void* p = shmem_open(name, &cap);
+  if (!p) return false;
+  const bool ok = len <= cap;
+  if (ok) out->assign(static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + len);
+  shmem_unmap(p, cap);
+  return ok;
+}
+
 size_t region_header_bytes(size_t n) {
   return offsetof(RegionHdr, nodes) + n * sizeof(NodeEntry);
 }

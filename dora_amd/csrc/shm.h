@@ -214,6 +214,16 @@ class RingReader {
   uint64_t last_return_ = 0;  // when wait() last returned
 };
 
+// Sample regions of host-only nodes: DataMessage::SharedMemory, the reference's
+// `ShmemConf::new().size(len).create()` (apis/rust/node/src/node/mod.rs:321-346).  POSIX shm
+// mapped shared read-write; the creator unlinks it when the slot is freed.
+void* shmem_create(const std::string& name, size_t len);  // nullptr on failure (errno)
+void* shmem_open(const std::string& name, size_t* len);   // the whole region; nullptr on failure
+void shmem_unmap(void* p, size_t len);
+void shmem_unlink(const std::string& name);
+// The first `len` bytes of region `name` (the inter-daemon forwarder's copy).
+bool read_shmem(const std::string& name, uint64_t len, std::vector<uint8_t>* out);
+
 // futex helpers on shared (non-private) words
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us);
 void futex_wake(std::atomic<uint32_t>* w);

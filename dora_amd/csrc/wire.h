@@ -46,7 +46,15 @@ enum : uint32_t {
   DROP_BCAST_GROUP = 202,  // {output, nranks}: the daemon's answer to REQ_BCAST_GROUP (0: none)
 };
 
-enum : uint8_t { DATA_NONE = 0, DATA_VEC = 1, DATA_DEVICE_IPC = 2 };
+enum : uint8_t { DATA_NONE = 0, DATA_VEC = 1, DATA_DEVICE_IPC = 2, DATA_SHMEM = 3 };
+
+// DataMessage::SharedMemory {shared_memory_id, len, drop_token} (libraries/message/src/
+// common.rs:135-152): a host-only node's sample >= 4096 B in a POSIX shared-memory region.
+struct SharedMem {
+  std::string name;  // shm_open name ("/dora-gpu-s-<pid>-<slot id>")
+  uint64_t len = 0;
+  DropToken token{};
+};
 
 // DataMessage::DeviceIpc — the sample lives in an exported hipMalloc slot of `owner_pid`.
 struct DeviceIpc {
@@ -75,7 +83,9 @@ struct DataMsg {
   uint8_t kind = DATA_NONE;
   std::vector<uint8_t> vec;  // DATA_VEC
   DeviceIpc ipc{};           // DATA_DEVICE_IPC
-  bool has_token() const { return kind == DATA_DEVICE_IPC; }
+  SharedMem shm;             // DATA_SHMEM
+  bool has_token() const { return kind == DATA_DEVICE_IPC || kind == DATA_SHMEM; }
+  const DropToken& token() const { return kind == DATA_SHMEM ? shm.token : ipc.token; }
 };
 
 struct Metadata {
@@ -136,6 +146,11 @@ class WBuf {
       }
       if (d.ipc.fill == FILL_EVENT) raw(d.ipc.event, 64);
       if (d.ipc.fill == FILL_BCAST) u64(d.ipc.epoch);
+    }
+    if (d.kind == DATA_SHMEM) {
+      str(d.shm.name);
+      u64(d.shm.len);
+      token(d.shm.token);
     }
   }
   void metadata(const Metadata& m) {
@@ -230,7 +245,12 @@ class RBuf {
       if (d.ipc.fill == FILL_BCAST) d.ipc.epoch = u64();
       if (d.ipc.fill > FILL_BCAST) throw std::invalid_argument("unknown fill kind");
     }
-    if (d.kind > DATA_DEVICE_IPC) throw std::invalid_argument("unknown DataMessage kind");
+    if (d.kind == DATA_SHMEM) {
+      d.shm.name = str();
+      d.shm.len = u64();
+      d.shm.token = token();
+    }
+    if (d.kind > DATA_SHMEM) throw std::invalid_argument("unknown DataMessage kind");
     return d;
   }
   Metadata metadata() {

@@ -6,7 +6,7 @@
         if event["type"] == "INPUT":
             arr = event["value"]                    # DeviceArray: zero-copy view of the HBM sample
             host = arr.to_pyarrow()                 # host staging for pyarrow consumers (F12)
-    node.send_output("out", pa.array([...]), {"k": 1})   # host pyarrow -> DMA into a device slot
+    node.send_output("out", pa.array([...]), {"k": 1})   # host pyarrow: inline < 4096 B, else DMA
     node.send_output("out", device_array)                 # HBM array -> HIP pack kernel
     node.send_output("out", b"raw bytes")                 # ArrowTypeInfo::byte_array
 """
@@ -247,8 +247,14 @@ class Node:
                 # the array keeps the input alive; the event handle can go
                 out["value"] = DeviceArray(a, t)
                 out["value"]._device_id = self.device
-            else:   # inline DataMessage::Vec sample of a host-only node
-                out["value"] = ctypes.string_at(dp.value, dn.value) if dn.value else b""
+            else:
+                # an inline DataMessage::Vec sample (< 4096 B from a host source), or a host-only
+                # producer's shared memory read in place: a host pyarrow array over its bytes,
+                # as the reference's PyEvent::value; it keeps the input alive
+                a, s = ArrowArray(), ArrowSchema()
+                call("dora_event_array", ev.ptr, byref(a), byref(s))
+                import pyarrow as pa
+                out["value"] = pa.Array._import_from_c(ctypes.addressof(a), ctypes.addressof(s))
         out["_event"] = ev
         return out
 

@@ -12,7 +12,6 @@ node's device data plane (python.rs:340-385: bytes as `byte_array`, arrays packe
 """
 from __future__ import annotations
 
-import ctypes
 import enum
 import importlib.util
 import os
@@ -48,18 +47,11 @@ def _status(ret) -> int:
 
 def host_value(ev: dict):
     """The input of a node event as a host pyarrow array (what a reference operator receives)."""
-    import pyarrow as pa
-    from . import _lib
-    from .arrow_c import ArrowArray, ArrowSchema
     from .device import DeviceArray
     v = ev.get("value")
     if isinstance(v, DeviceArray):
         return v.to_pyarrow()
-    if isinstance(v, (bytes, bytearray)):  # inline Vec sample of a host-only node
-        a, s = ArrowArray(), ArrowSchema()
-        _lib.call("dora_event_array", ev["_event"].ptr, ctypes.byref(a), ctypes.byref(s))
-        return pa.Array._import_from_c(ctypes.addressof(a), ctypes.addressof(s))
-    return v
+    return v  # an inline Vec or shared-memory sample: a host pyarrow array already (node.py)
 
 
 class _Operator:

@@ -166,6 +166,10 @@ def test_compact_line_fits_the_driver_tail():
     full = json.load(open(os.path.join(os.path.dirname(__file__), "..", "profiles",
                                        "r03_final_bench_1.json")))
     full["sink_dropped_by_phase"] = {"warmup": 0, "latency_ladder": 2, "timed_region": 0}
+    full["config"]["workload"] = ("C2: examples/benchmark node->sink edge, device-resident UInt8 "
+                                  "samples, 1 node + 1 sink per GPU")
+    for z in ("host_8", "host_512", "host_2048", "host_4096"):
+        full["latency_us"][z] = dict(full["latency_us"]["8"])
     full["sync_send_headline"].update({"hbm_frac_2S": 0.19, "pack_own_us": 17.9,
                                        "pack_own_frac": 0.57, "gap_us_median": 6.3})
     c = bench.compact_line(full, os.path.join(bench.ROOT, "gpurun_out", "bench_detail.json"))
@@ -176,7 +180,9 @@ def test_compact_line_fits_the_driver_tail():
               "roofline", "cpu_baseline"):
         assert k in c, k
     assert list(c)[-1] == "cpu_baseline"
-    assert set(c["latency_summary"]) == {"4096", "4194304", "40960000"}
+    assert set(c["latency_summary"]) == {"host_8", "host_2048", "8", "4096", "4194304",
+                                         "40960000"}
+    assert c["config"]["workload"] == full["config"]["workload"]  # whole, not cut
     assert c["roofline"]["frac"] == full["roofline"]["frac"]
     assert c["sink_dropped"]["by_phase"] == {"latency_ladder": 2}
     assert c["c3"]["frac"] == full["c3"]["roofline"]["frac"]

@@ -1,6 +1,7 @@
 """Control plane on the CPU (no GPU): daemon routing, AllNodesReady, drop-oldest input queues,
 InputClosed / end of stream, metadata parameters, output checks — with host-only nodes, which
-carry only the reference's inline `DataMessage::Vec` samples (< 4096 B)."""
+carry the reference's inline `DataMessage::Vec` samples (< 4096 B) and, from 4096 B, its
+`DataMessage::SharedMemory` samples (POSIX shm regions, recycled through drop tokens)."""
 import ctypes
 import os
 import threading
@@ -44,6 +45,12 @@ def _start_nodes(shm, ids):
     [t.join(20) for t in ts]
     assert set(out) == set(ids)
     return out
+
+
+def as_bytes(v) -> bytes:
+    """The bytes of a received UInt8 value (a host pyarrow array, as the reference's value)."""
+    import numpy as np
+    return np.asarray(v).tobytes()
 
 
 DESC = {"nodes": [
@@ -94,8 +101,6 @@ def test_routing_drop_oldest_and_close():
     time.sleep(0.2)
     with pytest.raises(_lib.DoraGpuError, match="unknown dora node output"):
         src.send_output("nope", b"x")
-    with pytest.raises(_lib.DoraGpuError, match="host-only"):
-        src.send_output("out", b"\0" * 5000)
     src.close()          # closes outputs -> InputClosed + end of stream for dst
     got = []
     closed = []
@@ -112,8 +117,8 @@ def test_routing_drop_oldest_and_close():
     # input — handed to the node, as the reference's event-stream thread takes events out of the
     # daemon's queue (event_stream/thread.rs:139-157) — and the three newest of the rest survive
     assert [s for s, _ in got] == [0, 2, 3, 4]
-    assert got[0][1] == bytes([0]) * 10
-    assert got[1][1] == bytes([2]) * 10
+    assert as_bytes(got[0][1]) == bytes([0]) * 10
+    assert as_bytes(got[1][1]) == bytes([2]) * 10
     assert closed == ["in"]
     dst.close()
     d.join()
@@ -136,9 +141,85 @@ def test_zero_length_sample_and_ordering():
             if ev["metadata"]["k"] % 2:   # empty sample -> ArrayData::new_empty(UInt8)
                 assert len(ev["value"]) == 0 and str(ev["value"].type) == "uint8"
             elif ev["metadata"]["k"] % 50:
-                assert ev["value"] == bytes([ev["metadata"]["k"] % 256]) * (ev["metadata"]["k"] % 50)
+                assert as_bytes(ev["value"]) == bytes([ev["metadata"]["k"] % 256]) * (ev["metadata"]["k"] % 50)
     assert seen == list(range(n))
     nodes["b"].close()
+    d.join()
+
+
+def test_host_only_shared_memory_samples_recycle():
+    """A host-only node sends samples >= 4096 B as DataMessage::SharedMemory (the reference's
+    allocate_shared_memory, apis/rust/node/src/node/mod.rs:321-346): the receiver reads the
+    region in place as a pyarrow array, its drop token returns the region to the sender's
+    best-fit cache, and a steady stream of one size creates no new regions.  Sizes below 4096 B
+    stay inline Vec samples (mod.rs:40)."""
+    import glob
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["o"]},
+        {"id": "b", "inputs": {"i": {"source": "a/o", "queue_size": 1000}}}]})
+    nodes = _start_nodes(d.shm, ["a", "b"])
+    a, b = nodes["a"], nodes["b"]
+    sizes = [4095, 4096, 4097, 1 << 20, 5_000_001]
+    seen = {}
+    for rep in range(3):
+        for z in sizes:
+            payload = bytes((k * 131 + z + rep) % 251 for k in range(256)) * (z // 256 + 1)
+            a.send_output("o", payload[:z], {"z": z, "rep": rep})
+            ev = b.next(timeout=10)
+            assert ev["type"] == "INPUT" and ev["metadata"] == {"z": z, "rep": rep}
+            assert not ev["on_device"] and ev["data_len"] == z
+            assert as_bytes(ev["value"]) == payload[:z], (z, rep)
+            assert ev["type_info"].to_json()["data_type"] == "C"
+            seen.setdefault(z, []).append(ev["data_ptr"])
+            del ev  # the value goes: the token returns, the region is reusable
+    st = a.stats()
+    # one region per size >= 4096 (created in the first round, reused in the next two)
+    assert st["slots_created"] == 4, st
+    assert st["cache_hits"] >= 8, st
+    mine = glob.glob(f"/dev/shm/dora-gpu-s-{os.getpid()}-*")
+    assert len(mine) == 4, mine
+    a.close()
+    while b.next(timeout=5) is not None:
+        pass
+    b.close()
+    d.join()
+    assert d.rc == 0
+    # the sender unlinks its regions when it goes
+    assert not glob.glob(f"/dev/shm/dora-gpu-s-{os.getpid()}-*")
+
+
+def test_host_only_receiver_holding_shared_memory_inputs():
+    """A receiver that keeps several shared-memory inputs alive holds their regions (the sender
+    allocates new ones meanwhile); releasing them returns every token, and a forward of such an
+    input by a host-only relay is a CPU copy into the relay's own region."""
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["o"]},
+        {"id": "r", "inputs": {"i": {"source": "a/o", "queue_size": 100}}, "outputs": ["f"]},
+        {"id": "c", "inputs": {"i": {"source": "r/f", "queue_size": 100}}}]})
+    nodes = _start_nodes(d.shm, ["a", "r", "c"])
+    a, r, c = nodes["a"], nodes["r"], nodes["c"]
+    held = []
+    for k in range(5):
+        a.send_output("o", bytes([k + 1]) * 70000, {"k": k})
+        ev = r.next(timeout=10)
+        r.forward("f", ev)
+        held.append(ev)
+        got = c.next(timeout=10)
+        assert got["metadata"] == {"k": k} and as_bytes(got["value"]) == bytes([k + 1]) * 70000
+        del got
+    assert a.stats()["in_flight"] == 5 and a.stats()["slots_created"] == 5
+    del ev
+    held.clear()
+    deadline = time.monotonic() + 5
+    while a.stats()["in_flight"] and time.monotonic() < deadline:
+        a.send_output("o", b"", {"k": -1})  # handles returned tokens
+        r.next(timeout=5)
+    assert a.stats()["in_flight"] == 0
+    for n in (a, r):
+        n.close()
+    while c.next(timeout=5) is not None:
+        pass
+    c.close()
     d.join()
 
 
@@ -158,7 +239,7 @@ def test_busy_stats_count_blocked_time():
     threading.Timer(0.3, lambda: src.send_output("out", b"late", {"seq": 1})).start()
     ev = dst.next(timeout=5)
     waited = time.monotonic() - t0
-    assert ev["type"] == "INPUT" and bytes(ev["value"]) == b"late"
+    assert ev["type"] == "INPUT" and as_bytes(ev["value"]) == b"late"
     i1, f1 = idle_ns()
     # the daemon thread also idles in this process, so at least the receiver's wait is there
     assert i1 - i0 >= 0.8 * 0.3e9 and waited >= 0.29

@@ -1,11 +1,12 @@
 """Dataflows spanning machines: one daemon per machine, InterDaemonEvent::Output /
 InputsClosed over TCP (libraries/message/src/daemon_to_daemon.rs:9-21, the remote branch of
 send_out in binaries/daemon/src/lib.rs:955-1000), modelled on examples/multiple-daemons
-(a source on one machine, its receivers on another).  CPU only: host-only nodes, inline
-samples; the device-sample staging path is covered by tests/test_gpu_dataflow.py."""
+(a source on one machine, its receivers on another).  CPU only: host-only nodes, inline and
+shared-memory samples; the device-sample staging path is covered by tests/test_gpu_dataflow.py."""
 import threading
 import time
 
+import numpy as np
 import pytest
 
 from dora_amd.dataflow import Dataflow, daemon_spec, parse_descriptor
@@ -83,7 +84,10 @@ def test_two_daemons_deliver_in_order_and_close(tmp_path):
         lt.join(30)
         sent = []
         for i in range(100):
-            payload = bytes((i * 7 + j) & 0xFF for j in range(16 + 37 * i % 3000))
+            # every tenth message >= 4096 B: a shared-memory sample on A (read by the
+            # forwarder) and on B (written by the host-only proxy)
+            n_b = 16 + 37 * i % 3000 if i % 10 else 4096 + 997 * i
+            payload = bytes((i * 7 + j) & 0xFF for j in range(n_b))
             t0 = time.time_ns()
             src.send_output("data", payload, {"seq": i, "tag": f"m{i}"})
             sent.append((payload, t0))
@@ -103,7 +107,7 @@ def test_two_daemons_deliver_in_order_and_close(tmp_path):
         data = [g for g in got[k] if g[0] == "data"]
         assert [g[1]["seq"] for g in data] == list(range(100))
         for (pid, meta, value, ts_ns), (payload, t0) in zip(data, sent):
-            assert value == payload and meta["tag"] == f"m{meta['seq']}"
+            assert np.asarray(value).tobytes() == payload and meta["tag"] == f"m{meta['seq']}"
             assert ts_ns >= t0 - 1000  # the producer's timestamp travels with the message
         side = [g for g in got[k] if g[0] == "side"]
         assert len(side) == 1 and side[0][1] == {"last": True}
