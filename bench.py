@@ -144,18 +144,13 @@ def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
             b.free()
 
 
-def aql_kernel_name(workload: str, body: int) -> str:
-    """The AQL pack kernel a send of this workload dispatches (kernels.hip build_aql_args*: 4
-    loads in flight per lane unless DORA_GPU_PACK_VARIANT says u8; one segment at offset 0 ->
-    pack1, with agent-coherent source loads (pack1c) when DORA_GPU_AQL_COHERENT=1)."""
-    v = os.environ.get("DORA_GPU_PACK_VARIANT", "")
-    u = 8 if v.startswith("u8") else 4
-    coh = os.environ.get("DORA_GPU_AQL_COHERENT", "0")
-    if workload != "c2":
-        c = "c" if u == 4 and coh == "all" else ""
-        return f"dora_aql_pack{c}_u{u} (AQL)"
-    c = "c" if u == 4 and coh in ("1", "all") else ""
-    return f"dora_aql_pack1{c}_u{u} (AQL)"
+def aql_kernel_name(workload: str, region_kernels=None) -> str:
+    """The AQL pack kernel of a timed region: the one dispatched most there
+    (dora_gpu_aql_dispatch_counts), else the one a pipelined send of this workload dispatches
+    (aql.cpp dispatch_locked: one segment at offset 0 -> pack1, nested arrays -> pack)."""
+    if region_kernels:
+        return max(region_kernels, key=region_kernels.get) + " (AQL)"
+    return ("dora_aql_pack1_u4" if workload == "c2" else "dora_aql_pack_u4") + " (AQL)"
 
 
 def pmc_traffic(msg_bytes: int):
@@ -615,7 +610,8 @@ def run_c3_block(node, stream, wait_ack, seq, steps=20, nsrc=24, steady_steps=20
         "slots_created_in_region": after["slots_created"] - before["slots_created"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "kernel": aql_kernel_name("c3", S),
+                     "kernel": aql_kernel_name("c3", {k: kern1[k] - kern0.get(k, 0) for k in kern1
+                                                      if kern1[k] - kern0.get(k, 0)}),
                      "device_us_per_launch": round(span_ms * 1e3 / max(packs, 1), 3),
                      "region_packs": packs, "algorithmic_bytes_per_launch": 2 * S,
                      "traffic": (pmc_traffic(S) or (None, None))[1],
@@ -1136,7 +1132,8 @@ def main():
                                      if copy_cal and copy_cal.get("TBps_2S") else None),
                      "traffic": traffic[1] if traffic else None,
                      "traffic_source": traffic[0] if traffic else None,
-                     "kernel": (aql_kernel_name(args.workload, S) if stats["fill_paths"]["aql"]
+                     "kernel": (aql_kernel_name(args.workload, region_kernels)
+                                if stats["fill_paths"]["aql"]
                                 else "pack_kernel (HIP fill streams)"),
                      # AQL packets of the timed region per kernel (dora_gpu_aql_dispatch_counts)
                      "region_kernels": region_kernels,

@@ -1,4 +1,5 @@
-"""ctypes binding of libdora_gpu.so (include/dora_gpu.h).
+"""ctypes binding of libdora_gpu.so (include/dora_gpu.h) and of the test hooks in
+libdora_gpu_testing.so (include/dora_gpu_testing.h).
 
 The library is built in-tree (dora_amd/lib/, `python -m dora_amd.build`).  There is no CPU
 fallback: if the library is missing, importing the data plane raises.
@@ -16,6 +17,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # DORA_GPU_LIB: another build of the library for this process (A/B of two builds on one box;
 # spawned tools keep the in-tree one through their rpath)
 LIB_PATH = os.environ.get("DORA_GPU_LIB") or os.path.join(LIB_DIR, "libdora_gpu.so")
+TESTING_PATH = os.path.join(LIB_DIR, "libdora_gpu_testing.so")
 
 ARROW_DEVICE_CPU = 1
 ARROW_DEVICE_ROCM = 10
@@ -56,8 +58,6 @@ _SIGS = {
     "dora_gpu_aql_batch_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_uint64),
                                          POINTER(c_uint64)]),
     "dora_gpu_aql_cp_signalled": (c_int, [c_int, POINTER(c_uint64)]),
-    "dora_gpu_test_fill_reached": (c_int, [c_void_p, c_uint64]),
-    "dora_gpu_test_cp_arm": (c_int, [c_void_p, c_uint64]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),
@@ -90,8 +90,6 @@ _SIGS = {
     "dora_gpu_plan_type_info": (c_int, [c_void_p, POINTER(c_uint8), c_size_t,
                                         POINTER(c_size_t)]),
     "dora_gpu_pack": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
-    "dora_gpu_pack_signal_tune": (c_int, [ctypes.c_uint32, c_int]),
-    "dora_gpu_pack_tune": (c_int, [c_int, c_int, ctypes.c_uint32]),
     "dora_gpu_array_upload": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema),
                                       POINTER(ArrowArray)]),
     "dora_gpu_array_download": (c_int, [POINTER(ArrowArray), POINTER(ArrowSchema),
@@ -103,30 +101,6 @@ _SIGS = {
     "dora_gpu_schema_release": (None, [POINTER(ArrowSchema)]),
     "dora_gpu_csum64": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
     "dora_gpu_csum64_sync": (c_int, [c_void_p, c_size_t, c_void_p, POINTER(c_uint64)]),
-    "dora_gpu_l2_touch": (c_int, [c_void_p, c_size_t, c_void_p]),
-    "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
-    "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
-    "dora_gpu_test_bar_free": (None, [c_void_p]),
-    "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
-    "dora_gpu_test_bcast_group": (c_int, [c_int, c_void_p, c_uint64, POINTER(c_int),
-                                          POINTER(c_int)]),
-    "dora_gpu_test_l1_stale": (c_int, [c_int, c_int, POINTER(c_uint32), POINTER(c_uint32),
-                                       POINTER(c_uint32)]),
-    "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
-                                           POINTER(ctypes.c_double)]),
-    "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
-                                         c_void_p, c_size_t, c_uint64, c_uint64, c_void_p,
-                                         c_void_p, c_size_t, c_int, c_void_p, c_size_t,
-                                         POINTER(c_size_t)]),
-    "dora_gpu_test_ide_inputs_closed": (c_int, [c_char_p, POINTER(c_char_p), POINTER(c_char_p),
-                                                c_size_t, c_uint64, c_void_p, c_void_p,
-                                                c_size_t, POINTER(c_size_t)]),
-    "dora_gpu_test_ide_decode": (c_int, [c_void_p, c_size_t, c_char_p, c_size_t,
-                                         POINTER(c_size_t)]),
-    "dora_gpu_test_batch_args": (c_int, [c_size_t, POINTER(c_size_t), POINTER(c_uint64),
-                                         POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
-                                         POINTER(c_uint64), c_void_p, c_size_t,
-                                         POINTER(ctypes.c_uint32)]),
     "dora_gpu_fill_splitmix": (c_int, [c_void_p, c_size_t, c_uint64, c_void_p]),
     # node API
     "dora_node_init": (c_int, [c_char_p, c_char_p, c_int, POINTER(c_void_p)]),
@@ -207,7 +181,41 @@ _SIGS = {
     "dora_daemon_free": (None, [c_void_p]),
 }
 
+# libdora_gpu_testing.so (include/dora_gpu_testing.h): test and microbenchmark hooks, a library
+# of their own so that the product ABI carries none of them
+_TEST_SIGS = {
+    "dora_gpu_test_fill_reached": (c_int, [c_void_p, c_uint64]),
+    "dora_gpu_test_cp_arm": (c_int, [c_void_p, c_uint64]),
+    "dora_gpu_test_pack_signal_tune": (c_int, [ctypes.c_uint32, c_int]),
+    "dora_gpu_test_pack_tune": (c_int, [c_int, c_int, ctypes.c_uint32]),
+    "dora_gpu_test_l2_touch": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
+    "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
+    "dora_gpu_test_bar_free": (None, [c_void_p]),
+    "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
+    "dora_gpu_test_bcast_group": (c_int, [c_int, c_void_p, c_uint64, POINTER(c_int),
+                                          POINTER(c_int)]),
+    "dora_gpu_test_l1_stale": (c_int, [c_int, c_int, POINTER(c_uint32), POINTER(c_uint32),
+                                       POINTER(c_uint32)]),
+    "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
+                                           POINTER(ctypes.c_double)]),
+    "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
+                                         c_void_p, c_size_t, c_uint64, c_uint64, c_void_p,
+                                         c_void_p, c_size_t, c_int, c_void_p, c_size_t,
+                                         POINTER(c_size_t)]),
+    "dora_gpu_test_ide_inputs_closed": (c_int, [c_char_p, POINTER(c_char_p), POINTER(c_char_p),
+                                                c_size_t, c_uint64, c_void_p, c_void_p,
+                                                c_size_t, POINTER(c_size_t)]),
+    "dora_gpu_test_ide_decode": (c_int, [c_void_p, c_size_t, c_char_p, c_size_t,
+                                         POINTER(c_size_t)]),
+    "dora_gpu_test_batch_args": (c_int, [c_size_t, POINTER(c_size_t), POINTER(c_uint64),
+                                         POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                         POINTER(c_uint64), c_void_p, c_size_t,
+                                         POINTER(ctypes.c_uint32)]),
+}
+
 _lib = None
+_testing = None
 
 
 def load(path: str = LIB_PATH):
@@ -228,8 +236,30 @@ def load(path: str = LIB_PATH):
     return lib
 
 
+def load_testing():
+    """Load libdora_gpu_testing.so (after the product library it links against) and declare
+    the test hooks; raise if it is absent."""
+    global _testing
+    if _testing is not None:
+        return _testing
+    load()
+    if not os.path.exists(TESTING_PATH):
+        raise ImportError(f"{TESTING_PATH} is missing: build it with `python -m dora_amd.build`")
+    lib = ctypes.CDLL(TESTING_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _TEST_SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _testing = lib
+    return lib
+
+
 def declared_symbols():
     return list(_SIGS)
+
+
+def declared_test_symbols():
+    return list(_TEST_SIGS)
 
 
 def check(rc: int) -> int:
@@ -241,5 +271,5 @@ def check(rc: int) -> int:
 
 
 def call(name: str, *args):
-    lib = load()
+    lib = load_testing() if name.startswith("dora_gpu_test_") else load()
     return check(getattr(lib, name)(*args))

@@ -110,6 +110,25 @@ def build(verbose: bool = False) -> str:
     return out
 
 
+TESTING_SOURCES = ["testing/testing.cpp"]
+TESTING_NAME = "libdora_gpu_testing.so"
+
+
+def build_testing(verbose: bool = False) -> str:
+    """libdora_gpu_testing.so: the test and microbenchmark hooks (include/dora_gpu_testing.h),
+    linked against libdora_gpu.so (rpath $ORIGIN) — the shipped library exports none of them."""
+    lib = build(verbose)
+    objs = _compile_all(TESTING_SOURCES, verbose)
+    out = os.path.join(LIB, TESTING_NAME)
+    if _newer(out, objs + [lib]):
+        cmd = [HIPCC, "-shared", "-fPIC", "-o", out, *objs, f"-L{LIB}", "-ldora_gpu",
+               "-Wl,-rpath,$ORIGIN", "-Wl,-soname," + TESTING_NAME]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return out
+
+
 TOOLS = {  # binary name -> sources (linked against libdora_gpu.so, rpath $ORIGIN)
     "dora-gpu-daemon": ["tools/daemon_main.cpp"],
     "dora-gpu-bench-sink": ["tools/bench_sink.cpp"],
@@ -168,3 +187,4 @@ if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
     print(build_pyext(verbose="-v" in sys.argv))
     print(build_tools(verbose="-v" in sys.argv))
+    print(build_testing(verbose="-v" in sys.argv))

@@ -41,10 +41,10 @@ namespace dora {
 
 // kernels.hip: the AQL kernels' argument block for `n` segments (<= aql_max_segments()).
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid, int* unroll, uint64_t dst_cap);
+                   uint8_t* out, size_t cap, uint32_t* grid, uint64_t dst_cap);
 size_t aql_args_size();
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
-                    uint32_t* grid, int* unroll, uint64_t grid_cap = 0);
+                    uint32_t* grid);
 size_t aql_batch_args_size();
 uint32_t aql_chunk_bytes(const Segment* segs, size_t n);
 int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t cap,
@@ -80,9 +80,8 @@ struct Pending {
   uint64_t dst_cap = 0, bytes = 0;
   uint32_t chunk = 0;
   bool profile = false;
-  bool cp = false;  // may be signalled by the command processor (cp_signal_window) when alone
+  bool cp = false;  // signalled by the command processor (aql_cp_candidate)
   bool lone = false;  // runs alone on the GPU (a synchronous send, or every queue idle)
-  bool read_signal = false;  // CP-signalled, and workgroup 0 stores the flag's read_epoch
   uint64_t* cp_stamps = nullptr;  // CP-signalled: the timed region's stamp area (device), or none
 };
 
@@ -91,15 +90,37 @@ struct Pending {
 constexpr int kMaxQueues = 8;
 
 // The kernels of the embedded code object, in AqlQueue::kobj order.
-constexpr int kKernels = 9;
-constexpr int kBatchKernel = 7;
-constexpr int kReduceKernel = 8;
+constexpr int kKernels = 5;
+constexpr int kMultiKernel = 0;   // multi-segment packs (nested arrays)
+constexpr int kOneKernel = 1;     // single-segment packs behind the acquire fence
+constexpr int kOneCohKernel = 2;  // single-segment packs with agent-coherent loads, no fence
+constexpr int kBatchKernel = 3;
+constexpr int kReduceKernel = 4;
 constexpr uint32_t kReduceArgsBytes = 32;  // base, areas, out, n, area_words
-constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4",   "dora_aql_pack_u8",
-                                                "dora_aql_pack1_u4",  "dora_aql_pack1_u8",
-                                                "dora_aql_pack1c_u4", "dora_aql_packc_u4",
-                                                "dora_aql_pack1p_u4", "dora_aql_packb_u4",
+constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4", "dora_aql_pack1_u4",
+                                                "dora_aql_pack1c_u4", "dora_aql_packb_u4",
                                                 "dora_aql_stamp_reduce"};
+
+// Dispatch policy (every figure below was measured against the alternative
+// on MI355X, the alternatives are not built any more):
+// * four HSA queues per process: 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s against
+//   two (profiles/r01_aql_queues_ab.jsonl);
+constexpr int kQueues = 4;
+// * packs of [1 MiB, 32 MiB) are signalled by the command processor (the packet's completion
+//   signal, every wave waiting for its own stores), so consecutive packets of a queue overlap:
+//   4 MB over 4 queues 1.95 -> 1.59-1.64 us each (profiles/r03_aql_pipeline_probe.jsonl), C3's
+//   multi-segment clouds too (r04, profiles/r04_c3_ab.jsonl).  Larger packs only when they run
+//   alone (a synchronous send): 40.96 MB 17.8-18.3 -> 14.05 us own time;
+constexpr uint64_t kCpLo = uint64_t(1) << 20, kCpHi = uint64_t(32) << 20;
+// * HBM-bound packs from 8 MiB run in order per queue (barrier bit) over four queues, three from
+//   32 MiB: C3 0.68-0.70 -> 0.72-0.75 (profiles/r04_full_ab.jsonl), 40.96 MB 14.1-14.5 ->
+//   12.9-13.0 us per pack (profiles/r02_aql_big_ab.jsonl);
+constexpr uint64_t kBarrierBytes = uint64_t(8) << 20;
+// * a queue holds at most two in-kernel-signalled packets (one running, one ready) and three
+//   CP-signalled ones (they overlap: 4 MB 1.88 -> 1.66 us at depth 3, r03_cp_signal_ab.jsonl);
+//   sends finding every queue that deep leave together as a batch pack of <= 32 MiB.
+constexpr size_t kDepth = 2, kCpDepth = 3;
+constexpr uint64_t kBatchBytes = uint64_t(32) << 20;
 
 struct AqlQueue {
   std::mutex mu;
@@ -107,8 +128,8 @@ struct AqlQueue {
   // Packs rotate over these hardware queues: one queue overlaps consecutive packs only partly
   // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl),
   // and the command processor's per-queue dispatch rate bounds a pipeline of <= 8 messages in
-  // flight (traces: ~12 us from dispatch to fill flag at 2 queues).  4 queues by default
-  // (DORA_GPU_AQL_QUEUES): 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s, the 40.96 MB
+  // flight (traces: ~12 us from dispatch to fill flag at 2 queues).  4 queues (kQueues):
+  // 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s, the 40.96 MB
   // headline (HIP fill streams) unchanged (profiles/r01_aql_queues_ab.jsonl).
   hsa_queue_t* qs[kMaxQueues] = {};
   uint64_t rd[kMaxQueues] = {};  // last read index seen per queue (the CP writes it to host memory)
@@ -230,51 +251,11 @@ hsa_status_t on_cpu_pool(hsa_amd_memory_pool_t pool, void* p) {
   return HSA_STATUS_SUCCESS;
 }
 
-// DORA_GPU_AQL_COHERENT (aql_pack).  Default (0, r03): every pack reads its sources with
-// non-temporal loads behind the packet's agent-scope acquire fence.  "1": single-segment packs
-// read with agent-coherent loads (dora_aql_pack1c_u4) and carry no acquire fence (the r02
-// default; 4 MB -8 %, 1 MB -15 % per message, profiles/r02_coherent_ab.jsonl).  r03 could not
-// make a source rewritten between sends read stale without the fence — host BAR stores, SDMA
-// and blit copies, with the source's lines loaded into every L2 and into the L1s of the CUs of
-// 256 earlier packs, even with L1-cached loads (tests/test_gpu_fence.py) — so there is no
-// evidence the fence is needed, and none that it is not: it stays on by default, and "1" is for
-// senders that know their sources are fresh.  "all" does the same for multi-segment packs, which
-// then copy their arguments from the device ring into LDS with coherent loads first: one
-// dependent memory round trip at every workgroup's start made C3 slower, 4.50 -> 4.89-5.23 us
-// per cloud (profiles/r02_coherent_c3_ab.jsonl), so it is a knob.
-int coherent_level() {
-  static const int v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_COHERENT");
-    if (e && *e == '1') return 1;
-    if (e && std::string(e) == "all") return 2;
-    if (e && std::string(e) == "plain") return -1;
-    return 0;
-  }();
-  return v;
-}
-
-// DORA_GPU_AQL_PRELOAD=0: single-segment packs use the device argument ring too.
-bool preload_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_PRELOAD");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
 void on_queue_error(hsa_status_t st, hsa_queue_t*, void* data) {
   const char* m = nullptr;
   hsa_status_string(st, &m);
   std::fprintf(stderr, "dora-gpu: AQL pack queue error: %s\n", m ? m : "?");
   static_cast<AqlQueue*>(data)->failed.store(true);
-}
-
-bool aql_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL");
-    return !(e && *e == '0');
-  }();
-  return v;
 }
 
 // Set up the queue of HIP device `device`; nullptr (and a note on stderr when DORA_GPU_TRACE
@@ -339,11 +320,10 @@ AqlQueue* create(int device) {
         hsa_executable_symbol_get_info(
             sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &a->priv[k]) !=
             HSA_STATUS_SUCCESS ||
-        ka != (k < 2                  ? aql_args_size()
-               : k == kBatchKernel    ? aql_batch_args_size()
-               : k == kReduceKernel   ? size_t(kReduceArgsBytes)
-               : k == 5               ? sizeof(void*)
-                                      : size_t(kArgs1Bytes)) ||
+        ka != (k == kMultiKernel    ? aql_args_size()
+               : k == kBatchKernel  ? aql_batch_args_size()
+               : k == kReduceKernel ? size_t(kReduceArgsBytes)
+                                    : size_t(kArgs1Bytes)) ||
         ka > kSlotBytes) {
       delete a;
       return note("kernel symbol / argument size");  // no hidden arguments expected
@@ -365,21 +345,11 @@ AqlQueue* create(int device) {
     std::memcpy(a->ring + size_t(r) * kSlotBytes, zero.data(), kSlotBytes);
   __builtin_ia32_sfence();
   (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
-  const char* qe = std::getenv("DORA_GPU_AQL_QUEUES");
-  const int want = std::max(1, std::min(kMaxQueues, qe ? std::atoi(qe) : 4));
-  for (int i = 0; i < want; ++i) {
+  for (int i = 0; i < kQueues; ++i) {
     if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
       break;
     a->nq = i + 1;
-    // DORA_GPU_AQL_PRIORITY=high|low: the queues' scheduling priority against other queues
-    // of the GPU (other processes, HIP streams); default normal
-    if (const char* pr = std::getenv("DORA_GPU_AQL_PRIORITY")) {
-      const std::string v(pr);
-      if (v == "high" || v == "low")
-        (void)hsa_amd_queue_set_priority(
-            a->qs[i], v == "high" ? HSA_AMD_QUEUE_PRIORITY_HIGH : HSA_AMD_QUEUE_PRIORITY_LOW);
-    }
   }
   if (a->nq == 0) {
     hsa_amd_memory_pool_free(ring);
@@ -390,7 +360,7 @@ AqlQueue* create(int device) {
   // per dispatch by the command processor, so no wave reads them over PCIe)
   hsa_amd_agent_iterate_memory_pools(f.cpu, on_cpu_pool, &f);
   void* hr = nullptr;
-  if (preload_enabled() && f.kernarg_ok &&
+  if (f.kernarg_ok &&
       hsa_amd_memory_pool_allocate(f.kernarg, size_t(kRingSlots) * kHostSlotBytes, 0, &hr) ==
           HSA_STATUS_SUCCESS) {
     if (hsa_amd_agents_allow_access(1, &f.gpu, nullptr, hr) == HSA_STATUS_SUCCESS) {
@@ -420,7 +390,7 @@ AqlQueue* aql_queue(int device) {
   static std::mutex& mu = g_queues_mu;
   static AqlQueue** queues = g_queues;
   static bool tried[64] = {};
-  if (!aql_enabled() || device < 0 || device >= 64) return nullptr;
+  if (device < 0 || device >= 64) return nullptr;
   std::lock_guard<std::mutex> g(mu);
   if (!tried[device]) {
     tried[device] = true;
@@ -461,6 +431,8 @@ void aql_fence_all() {
     if (!a) continue;
     drain_backlog(a, t0, std::chrono::seconds(5));
     std::lock_guard<std::mutex> g(a->mu);
+    // fills launched through HIP after a failed dispatch (fallback_locked) are in no Use
+    if (a->fallback) (void)hipStreamSynchronize(a->fallback);
     for (Use& u : a->uses)
       while (u.flag && !fill_reached(u.flag, u.epoch) &&
              std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5))
@@ -474,6 +446,8 @@ void aql_forget_flags(int device, const void* base, size_t size) {
   const auto t0 = std::chrono::steady_clock::now();
   drain_backlog(a, t0, std::chrono::seconds(2));
   std::lock_guard<std::mutex> g(a->mu);
+  // fallback fills (fallback_locked) write flags in no Use: the region must outlive them
+  if (a->fallback) (void)hipStreamSynchronize(a->fallback);
   const auto* lo = static_cast<const uint8_t*>(base);
   // sends still backlogged after the bound: never dispatched, and their flags are about to go
   // away — drop them rather than let a later dispatch write into the unmapped region
@@ -503,117 +477,12 @@ void aql_forget_flags(int device, const void* base, size_t size) {
 
 namespace {
 
-// Single-segment packs of [min, max) bytes are signalled by the command processor when they go out
-// alone (DORA_GPU_AQL_CP_SIGNAL=min:max in bytes, "0": never).  The in-kernel signal's tail —
-// every workgroup waiting for its stores' acknowledgement, workgroup 0's last poll of the done
-// words — keeps a queue from starting its next packet, so a queue runs one pack at a time; with
-// the CP's completion signal instead, consecutive packets of a queue overlap.
-// DESIGN §9 (profiles/r03_aql_pipeline_probe.jsonl, mode 5): 4 MB packs over 4 queues
-// 1.95 -> 1.59-1.64 us each, 1 MB 1.38-1.42 -> 1.51 (so not below 2 MiB), 16 / 40.96 MB flat.
-// Multi-segment packs (C3's point clouds) in the window too (r04 default; DORA_GPU_AQL_CP_MULTI=0:
-// in-kernel signals).  r03 kept them opt-in: the 20-send burst lost (0.68-0.70 -> 0.35-0.63)
-// to host stalls at its first sends.  The r04 trace found the stall: the region before the
-// burst read its CP packs' stamp areas through the BAR (~57 ms of uncached reads), long enough
-// for the daemon and the receiver to fall asleep, and the burst's first messages waited 16 us
-// for the daemon's routing, the sender at its in-flight cap behind them.  With the stamps
-// reduced on the GPU (aql_stamp_reduce), 4 interleaved runs of the C3 block: burst 0.70-0.72 vs
-// 0.66-0.71 in-kernel, steady 0.73-0.76 vs 0.71-0.75 (profiles/r04_c3_ab.jsonl).
-bool cp_multi() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_CP_MULTI");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-std::pair<uint64_t, uint64_t> cp_signal_window() {
-  static const std::pair<uint64_t, uint64_t> v = [] {
-    std::pair<uint64_t, uint64_t> w{uint64_t(1) << 20, uint64_t(32) << 20};
-    if (const char* e = std::getenv("DORA_GPU_AQL_CP_SIGNAL")) {
-      if (*e == '0' && e[1] == 0) return std::pair<uint64_t, uint64_t>{0, 0};
-      char* end = nullptr;
-      const uint64_t lo = std::strtoull(e, &end, 10);
-      if (end && *end == ':') w = {lo, std::strtoull(end + 1, nullptr, 10)};
-    }
-    return w;
-  }();
-  return v;
-}
-
-// Which lone packs above the CP window are signalled by the command processor (with the CP
-// grid): synchronous sends only (default, DORA_GPU_AQL_CP_LONE=sync), also async sends that find
-// every queue idle (`idle`), or none (`0`).  An async send that finds the queues idle usually
-// opens a burst: given the whole GPU (3584 workgroups) it delays the packs queued right behind
-// it, and the 20-step headline lost 0.8 % (0.778 vs 0.786 mean over six interleaved rounds,
-// profiles/r04_headline20_ab.jsonl).  DORA_GPU_AQL_CP_BIG=1: such packs are CP-signalled even
-// when others run beside them (an A/B knob for the pipelined headline).
-int cp_lone_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_CP_LONE");
-    if (e && *e == '0') return 0;
-    if (e && (std::string(e) == "idle" || *e == '2')) return 2;
-    return 1;
-  }();
-  return v;
-}
-bool lone_kernel_signal() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_LONE_SIGNAL");
-    return e && std::string(e) == "kernel";
-  }();
-  return v;
-}
-bool cp_big() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_CP_BIG");
-    return e && *e == '1';
-  }();
-  return v;
-}
-
-bool lone_dev_args() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_LONE_DEV_ARGS");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-bool lone_coherent() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_LONE_COHERENT");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-// DORA_GPU_AQL_MID_COHERENT=0: CP-signalled mid-size packs keep the acquire fence and nt loads.
-bool mid_coherent() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_MID_COHERENT");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-uint64_t barrier_bytes() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BARRIER_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : uint64_t(8) << 20;
-  }();
-  return v;
-}
-
 // Queues the barrier-bit packs of `bytes` spread over: three from 32 MiB (three concurrent 40 MB
 // copies saturate HBM: 12.9-13.0 us per pack on three queues vs 13.2 on four,
 // profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
-// the 20-cloud burst, profiles/r04_full_ab.jsonl).  DORA_GPU_AQL_BIG_QUEUES=N: N for every size.
+// the 20-cloud burst, profiles/r04_full_ab.jsonl).
 int big_queues(int nq, uint64_t bytes) {
-  static const int v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BIG_QUEUES");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return std::min(nq, v ? v : bytes >= (uint64_t(32) << 20) ? 3 : 4);
+  return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : 4);
 }
 
 // The number of the oldest dispatch still in an outstanding list (a->next when none is).
@@ -651,49 +520,31 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   SubSpan sp_args(SP_AQL_ARGS);
   uint8_t args[kSlotBytes];
   uint32_t grid = 0;
-  int unroll = 4;
   // one segment at sample offset 0: the preloaded kernels, arguments from host memory
   const bool batch = n > 1;
   const bool one = !batch && a->hring && it0.n == 1 && segs[0].dst_off == 0;
-  // A lone mid-size single-segment pack signalled by the command processor (cp_signal_window):
-  // no in-kernel flag, every wave waits for its own stores, the packet's completion signal is
-  // the flag's CpSignal line (shm.h FillFlag)
-  bool cp = !batch && it0.cp && it0.flag_host && (one || cp_multi());
-  // DORA_GPU_AQL_LONE_SIGNAL=kernel: a lone single-segment pack keeps the in-kernel signal (its
-  // round trip is ~1.5 us shorter than the command processor's: 4 KB packs 7.0-7.2 vs 8.5-8.7 us,
-  // profiles/r04_lone_latency.jsonl) with up to kMaxSignalWgs workgroups instead of 1024
-  const bool lone_kernel = !batch && one && it0.lone && lone_kernel_signal() &&
-                           segs[0].len >= cp_signal_window().first;
-  if (lone_kernel) cp = false;
+  // A mid-size pack, or a lone big single-segment one, signalled by the command processor
+  // (aql_cp_candidate): no in-kernel flag, every wave waits for its own stores, the packet's
+  // completion signal is the flag's CpSignal line (shm.h FillFlag)
+  const bool cp = !batch && it0.cp && it0.flag_host;
   int rc;
   if (batch) {
     BatchItem bi[kBatchMsgs];
     for (size_t m = 0; m < n; ++m)
       bi[m] = {items[m].segs, items[m].n, items[m].dst, items[m].sig, items[m].dst_cap};
     rc = build_aql_batch_args(bi, n, args, sizeof(args), &grid);
-  } else if (cp && one && it0.read_signal) {
-    // a synchronous send: workgroup 0 tells the sender when the source has been read (the flag
-    // tagged with bit 0, pack_device.h signal_read); the command processor reports the fill
-    const FillSignal rs{reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(sig.flag) | 1),
-                        sig.epoch, sig.done};
-    rc = build_aql_args1(segs[0], dst, rs, args, &grid, &unroll, kMaxSignalWgs);
   } else if (cp) {
     // no flag, done words non-null: per-wave store waits; `epoch` carries the stamp area
     const FillSignal per_wave{nullptr, reinterpret_cast<uintptr_t>(it0.cp_stamps), sig.done};
-    rc = one ? build_aql_args1(segs[0], dst, per_wave, args, &grid, &unroll)
-             : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, &unroll,
-                              it0.dst_cap);
+    rc = one ? build_aql_args1(segs[0], dst, per_wave, args, &grid)
+             : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, it0.dst_cap);
   } else if (one) {
-    rc = build_aql_args1(segs[0], dst, sig, args, &grid, &unroll, lone_kernel ? kMaxSignalWgs : 0);
+    rc = build_aql_args1(segs[0], dst, sig, args, &grid);
   } else {
-    rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, &unroll, it0.dst_cap);
+    rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, it0.dst_cap);
   }
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};
-  static const bool no_prof = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_PROFILE");
-    return e && *e == '0';
-  }();
   if (cp) {
     // set the flag up for this fill (its previous fill has completed: the slot was reused), then
     // name the epoch; the command processor's decrement completes it (fill_reached)
@@ -702,7 +553,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
            sig.epoch);
     // the device address of the CpSignal line: the flag's device address + its offset
     done.handle = reinterpret_cast<uint64_t>(sig.flag) + offsetof(FillFlag, cp);
-  } else if (profile && a->profiling && !no_prof) {
+  } else if (profile && a->profiling) {
     if (a->free_sigs.empty() && a->used_sigs.size() < kProfileSignals) {
       hsa_signal_t s;
       if (hsa_signal_create(1, 0, nullptr, &s) == HSA_STATUS_SUCCESS) a->free_sigs.push_back(s);
@@ -714,16 +565,13 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
       a->used_sigs.push_back(done);
     }
   }
-  // Coherent multi-segment packs (DORA_GPU_AQL_COHERENT=all, coherent_level): the kernel reads
-  // its arguments from the device-ring slot through a pointer preloaded from the host ring.
-  const bool coh_multi = coherent_level() >= 2 && !one && !batch && unroll == 4 && a->hring;
   uint8_t* slot;
   // A lone single-segment pack (nothing to overlap its dispatch with) takes its arguments from
   // the device ring like a multi-segment one: the command processor's preload then reads HBM, not
   // host memory over PCIe — 0.6-0.7 us less from doorbell to completion at any size
-  // (aql_pipeline_bench modes 5 vs 7, profiles/r04_lone_dispatch_ab.jsonl; DORA_GPU_AQL_LONE_DEV_ARGS=0:
-  // host memory).  Pipelined packs keep the host ring: no HDP flush per send.
-  const bool dev_args1 = one && it0.lone && lone_dev_args();
+  // (aql_pipeline_bench modes 5 vs 7, profiles/r04_lone_dispatch_ab.jsonl).  Pipelined packs keep
+  // the host ring: no HDP flush per send.
+  const bool dev_args1 = one && it0.lone;
   if (one && !dev_args1) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
     slot = a->hring + r * kHostSlotBytes;
@@ -735,11 +583,6 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     // are posted writes ordered before the doorbell
     __builtin_ia32_sfence();
     *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // UC store: ordered before the packet
-    if (coh_multi) {
-      uint8_t* const dev_slot = slot;
-      slot = a->hring + r * kHostSlotBytes;
-      std::memcpy(slot, &dev_slot, sizeof(dev_slot));
-    }
   }
   // HBM-bound packs (>= barrier_bytes) run in order per queue (barrier bit) over at most three
   // queues (aql_pack).  Smaller packs overlap freely on all queues.
@@ -764,29 +607,18 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   }
   hsa_queue_store_write_index_relaxed(q, idx + 1);
   auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  // DORA_GPU_AQL_COHERENT=1 (coherent_level): single-segment packs read their source with
-  // agent-coherent loads (dora_aql_pack1c_u4: sc1 nt, bypassing the CU's L1 like the default's nt
-  // loads) and their packets carry no acquire fence (below); their arguments are preloaded into
-  // SGPRs by the command processor, so no kernarg line can be stale either.  Interleaved A/B on
-  // one box, sources rotated past the caches (profiles/r02_coherent_ab.jsonl): 1 MB 1.45-1.49 ->
-  // 1.23-1.26 us per message, 4 MB median 2.02 -> 1.81, 16 MB -1 %, 40.96 MB unchanged.
-  // A CP-signalled single-segment pack inside the CP window (1-32 MiB) reads its source
-  // agent-coherently and carries no acquire fence (mid_coherent): the packet's acquire is a
-  // per-packet cost of the command processor (4 MB: 1.50-1.58 -> 1.37-1.46 us per message
-  // pipelined), and a pack whose every source load bypasses the CU's L1 has nothing
-  // for it to invalidate (the in-dispatch control shows L1 the only cache a reread
-  // finds stale; no cross-dispatch configuration ever read stale).
-  // A lone single-segment pack likewise (DORA_GPU_AQL_LONE_COHERENT=0: fenced): no packet acquire
-  // in its dispatch latency (0.1-0.2 us, aql_pipeline_bench mode 6 vs 5,
-  // profiles/r04_lone_dispatch_ab.jsonl).
-  const bool coh = (coherent_level() >= 1 && one && unroll == 4) || coh_multi ||
-                   (cp && one && unroll == 4 && coherent_level() == 0 && mid_coherent() &&
-                    it0.bytes < cp_signal_window().second) ||
-                   (one && unroll == 4 && coherent_level() == 0 && it0.lone && lone_coherent());
-  const int k = batch                                      ? kBatchKernel
-                : coh                                        ? (one ? 4 : 5)
-                : (one && coherent_level() < 0 && unroll == 4) ? 6
-                                                               : (one ? 2 : 0) + (unroll == 8 ? 1 : 0);
+  // A CP-signalled single-segment pack inside the CP window (1-32 MiB), and a lone one, read
+  // their source with agent-coherent loads (dora_aql_pack1c_u4: sc1 nt, bypassing the CU's L1 like
+  // the fenced kernel's nt loads) and their packets carry no acquire fence: the packet's acquire is
+  // a per-packet cost of the command processor (4 MB: 1.50-1.58 -> 1.37-1.46 us per message
+  // pipelined; a lone pack's dispatch 0.1-0.2 us, r04_lone_dispatch_ab.jsonl), and a
+  // pack whose every source load bypasses the CU's L1 has nothing for it to invalidate (DESIGN §8:
+  // inside one dispatch only plain loads re-read stale words; across dispatches no configuration
+  // ever read stale, test_gpu_fence.py rewrites the source between > 512 such packs).  Their
+  // arguments come preloaded into SGPRs, or from the device ring behind the HDP flush (lone).
+  // Pipelined packs outside the window and multi-segment packs keep the fence.
+  const bool coh = one && ((cp && it0.bytes < kCpHi) || it0.lone);
+  const int k = batch ? kBatchKernel : one ? (coh ? kOneCohKernel : kOneKernel) : kMultiKernel;
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
@@ -801,31 +633,18 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   p->reserved2 = 0;
   p->completion_signal = done;
   // agent-scope acquire: the pack reads device memory of this GPU; it publishes its sample
-  // itself (write-through stores + fill flag), so no release (below).  Below the barrier size no barrier bit, so packs
-  // of one queue overlap (ramps and signal tails hide behind each other); HBM-bound packs at or
-  // above it run one at a time per queue, like HIP stream order (more concurrent 40 MB copies
-  // only contend for HBM).
-  const bool barrier = big;
-  // No release fence at the end of a pack: its sample, done words and fill flag are all stored
-  // write-through (sc1 / system scope) and complete before the flag is set, so the kernel-end
-  // L2 write-back has nothing of the pack's to publish — and costs C3 ~8 % of its device time
-  // (5.18-5.41 -> 4.81-4.83 us per cloud, profiles/r02_release_ab.jsonl; 4 / 16 MB unchanged).
-  // DORA_GPU_AQL_RELEASE=agent restores it (A/B knob).
-  static const uint32_t release = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_RELEASE");
-    return uint32_t(e && std::string(e) == "agent" ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE);
-  }();
-  // DORA_GPU_AQL_ACQUIRE=none: measurement knob only (a pack could then read source lines a
-  // stale L2 still holds)
-  static const uint32_t acquire = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_ACQUIRE");
-    return uint32_t(e && std::string(e) == "none" ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT);
-  }();
+  // itself (write-through stores + fill flag), so no release.  Below the barrier size no barrier
+  // bit, so packs of one queue overlap (ramps and signal tails hide behind each other); HBM-bound
+  // packs at or above it run one at a time per queue, like HIP stream order (more concurrent
+  // 40 MB copies only contend for HBM).  No release fence at the end of a pack: its sample, done
+  // words and fill flag are all stored write-through (sc1 / system scope) and complete before the
+  // flag is set, so the kernel-end L2 write-back has nothing of the pack's to publish — and costs
+  // C3 ~8 % of its device time (5.18-5.41 -> 4.81-4.83 us per cloud, profiles/r02_release_ab.jsonl).
   const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                          (barrier ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
-                          ((coh ? uint32_t(HSA_FENCE_SCOPE_NONE) : acquire)
+                          (big ? (1 << HSA_PACKET_HEADER_BARRIER) : 0) |
+                          ((coh ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT)
                            << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                          (release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                          (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
                    __ATOMIC_RELEASE);
@@ -843,38 +662,6 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     a->batched_msgs += n;
   }
   return DORA_OK;
-}
-
-bool batching_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BATCH");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-// Packets a queue may hold before sends wait in the backlog: one running, one ready behind it
-// (DORA_GPU_AQL_DEPTH).
-size_t queue_depth() {
-  static const size_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_DEPTH");
-    const long d = e ? std::atol(e) : 2;
-    return size_t(std::max(1L, std::min(64L, d)));
-  }();
-  return v;
-}
-
-// Packets a queue may hold when the send would be signalled by the command processor
-// (DORA_GPU_AQL_CP_DEPTH, default 3): such packets of one queue overlap, so a third one keeps
-// the queue busy (native ladder, profiles/r03_cp_signal_ab.jsonl: 4 MB 1.88 -> 1.66 us per
-// message at depth 3, 8 MB 2.74 -> 2.70-2.77, 16 MB 5.30 -> 5.39-5.48).
-size_t cp_queue_depth() {
-  static const size_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_CP_DEPTH");
-    const long d = e ? std::atol(e) : 3;
-    return size_t(std::max(1L, std::min(64L, d)));
-  }();
-  return v;
 }
 
 // Drop the completed packets at the front of queue `i`'s outstanding list.
@@ -901,33 +688,13 @@ bool queues_idle(AqlQueue* a) {
 int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
   if (a->hold) return -1;
   if (nq <= 0 || nq > a->nq) nq = a->nq;
-  const size_t d = depth ? depth : queue_depth();
+  const size_t d = depth ? depth : kDepth;
   for (int j = 0; j < nq; ++j) {
     const int i = int((a->next + uint64_t(j)) % uint64_t(nq));
     if (a->outq[i].size() >= d) prune(a, i);
     if (a->outq[i].size() < d) return i;
   }
   return -1;
-}
-
-// Bytes a batch may carry (DORA_GPU_AQL_BATCH_BYTES, default 32 MiB), and the size from
-// which a batch runs like a big pack — barrier bit, at most three queues — instead of
-// overlapping on all four (DORA_GPU_AQL_BATCH_BIG_BYTES, default: never).
-uint64_t batch_bytes() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BATCH_BYTES");
-    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
-    return x ? x : uint64_t(32) << 20;
-  }();
-  return v;
-}
-uint64_t batch_big_bytes() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_BATCH_BIG_BYTES");
-    const uint64_t x = e ? std::strtoull(e, nullptr, 10) : 0;
-    return x ? x : ~uint64_t(0);
-  }();
-  return v;
 }
 
 // Sends that were accepted (aql_pack returned DORA_OK) but can no longer leave through the AQL
@@ -974,22 +741,20 @@ void pump_locked(AqlQueue* a) {
     for (const Pending& p : a->backlog) {
       if (n == kBatchMsgs) break;
       if (n && (segs + p.n > kBatchSegs || p.chunk != a->backlog.front().chunk ||
-                bytes + p.bytes > batch_bytes()))
+                bytes + p.bytes > kBatchBytes))
         break;
       segs += p.n;
       bytes += p.bytes;
       ++n;
     }
-    const bool big = n > 1 && bytes >= batch_big_bytes();
-    const int qi = pick_queue(a, big ? big_queues(a->nq, bytes) : 0,
-                              n == 1 && a->backlog.front().cp ? cp_queue_depth() : 0);
+    const int qi = pick_queue(a, 0, n == 1 && a->backlog.front().cp ? kCpDepth : 0);
     if (qi < 0) return;
     Pending batch[kBatchMsgs];
     for (size_t k = 0; k < n; ++k) {
       batch[k] = a->backlog.front();
       a->backlog.pop_front();
     }
-    if (dispatch_locked(a, size_t(qi), batch, n, big) != DORA_OK) {
+    if (dispatch_locked(a, size_t(qi), batch, n, false) != DORA_OK) {
       // the queues are unusable from here on: these sends and the rest of the backlog leave
       // through HIP instead
       a->failed.store(true);
@@ -1033,24 +798,9 @@ void dispatcher_main(AqlQueue* a) {
 
 }  // namespace
 
-// DORA_GPU_AQL_READ_SIGNAL=1 (opt-in): synchronous single-segment sends return on their pack's
-// read signal (pack_device.h signal_read) instead of the command processor's fill signal.  Not
-// the default: the host saw the signal 1.9 us sooner (gap 6.8-7.2 vs 8.6-9.1 us), but the
-// in-kernel completion (done words, workgroup 0's poll, a 4096-workgroup cap) made each 40.96 MB
-// pack 2.8 us longer (17.5-17.7 vs 14.7-14.8 us): 24.8-25.7 vs 23.9-24.4 us per synchronous send
-// over three interleaved rounds (profiles/r04_headline_ab.jsonl, read_off = the default).
-bool aql_read_signal_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_READ_SIGNAL");
-    return e && *e == '1';
-  }();
-  return v;
-}
-
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
-             uint64_t* cp_stamps, bool sync, bool* read_signal) {
-  if (read_signal) *read_signal = false;
+             uint64_t* cp_stamps, bool sync) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -1065,49 +815,35 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.cp_stamps = cp_stamps;
   for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
   std::lock_guard<std::mutex> g(a->mu);
-  // Signalled by the command processor (inside a timed region only with a stamp area for the
-  // pack's own stamps): a pack in the window, and a single-segment pack above it that runs alone
-  // — sent synchronously, or finding every queue idle (aql.h).
   // lone: runs alone on the GPU (a synchronous send, or every queue idle): its arguments go to
-  // the device ring and it reads without the acquire fence (dispatch_locked)
+  // the device ring and it reads without the acquire fence (dispatch_locked).  Signalled by the
+  // command processor (inside a timed region only with a stamp area for the pack's own stamps):
+  // a pack in the CP window, and a synchronous single-segment pack above it (aql.h).  An async
+  // send that finds the queues idle usually opens a burst: given the whole GPU (3584 workgroups)
+  // it delays the packs queued right behind it, so it keeps the in-kernel signal (the 20-step
+  // headline 0.778 vs 0.786 mean over six interleaved rounds, profiles/r04_headline20_ab.jsonl).
   p.lone = sync || queues_idle(a);
-  const bool cp_lone = cp_lone_mode() == 2 ? p.lone : cp_lone_mode() == 1 && sync;
-  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, cp_lone || cp_big());
-  // a synchronous single-segment send returns on its pack's read signal (DORA_GPU_AQL_READ_SIGNAL=0:
-  // on the fill), when the pack leaves at once (not from the backlog or in a batch)
-  p.read_signal = sync && p.cp && n == 1 && segs[0].dst_off == 0 && !cp_stamps && read_signal &&
-                  aql_read_signal_enabled() && a->hring;
-  // HBM-bound packs (>= DORA_GPU_AQL_BARRIER_BYTES, default 8 MiB) run in order per queue
-  // (barrier bit) over at most three (four below 32 MiB) queues, big_queues: more concurrent
-  // 40 MB copies only contend (14.1-14.5 us per pack without the barrier, 12.9-13.0 with it;
-  // profiles/r02_aql_big_ab.jsonl).  r04 lowered the size from 32 to 8 MiB (the
-  // in-flight cap's boundary): C3's 13 MB clouds 0.68-0.70 -> 0.72-0.75 of HBM over the 20-cloud
-  // burst, 16 MB native sends 5.36-5.55 -> 5.20-5.25 us, over three interleaved full runs each
-  // (profiles/r04_full_ab.jsonl).
-  const bool big = barrier_bytes() && p.bytes >= barrier_bytes();
-  if (big || !batching_enabled()) {
-    const size_t qi = big ? size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)))
-                          : size_t(a->next % uint64_t(a->nq));
-    const int rc = dispatch_locked(a, qi, &p, 1, big);
+  p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, sync);
+  // HBM-bound packs (>= kBarrierBytes) run in order per queue (barrier bit) over at most three
+  // (four below 32 MiB) queues, big_queues: more concurrent 40 MB copies only contend (14.1-14.5
+  // us per pack without the barrier, 12.9-13.0 with it; profiles/r02_aql_big_ab.jsonl).
+  const bool big = p.bytes >= kBarrierBytes;
+  if (big) {
+    const size_t qi = size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)));
+    const int rc = dispatch_locked(a, qi, &p, 1, true);
     prune(a, int(qi));
-    if (rc == DORA_OK && read_signal) *read_signal = p.read_signal;
     return rc;
   }
-  // Below that, a queue holds at most queue_depth() packets (one running, one ready): the
-  // command processor runs a queue's packets one after another with a ~1-2 us gap, four queues
-  // at most share the compute pipes (DESIGN §6 "4 MB"), so a send that finds them all busy
-  // waits in the backlog and leaves with the sends queued behind it as one batch pack — fewer,
-  // larger dispatches instead of more queues.
+  // Below that, a queue holds at most kDepth packets (one running, one ready): the command
+  // processor runs a queue's packets one after another with a ~1-2 us gap, four queues at most
+  // share the compute pipes, so a send that finds them all busy waits in the backlog
+  // and leaves with the sends queued behind it as one batch pack — fewer, larger dispatches
+  // instead of more queues.
   p.chunk = aql_chunk_bytes(segs, n);
   if (a->backlog.empty()) {
-    const int qi = pick_queue(a, 0, p.cp ? cp_queue_depth() : 0);
-    if (qi >= 0) {
-      const int rc = dispatch_locked(a, size_t(qi), &p, 1, false);
-      if (rc == DORA_OK && read_signal) *read_signal = p.read_signal;
-      return rc;
-    }
+    const int qi = pick_queue(a, 0, p.cp ? kCpDepth : 0);
+    if (qi >= 0) return dispatch_locked(a, size_t(qi), &p, 1, false);
   }
-  p.read_signal = false;  // a backlogged send may leave in a batch pack
   a->backlog.push_back(p);
   ++a->backlogged;
   pump_locked(a);
@@ -1124,12 +860,9 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone) {
   if (n == 0) return false;
   const bool single = n == 1 && segs[0].dst_off == 0;
-  if (!single && !cp_multi()) return false;
   uint64_t bytes = 0;
   for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
-  const auto cw = cp_signal_window();
-  if (cw.second == 0) return false;  // DORA_GPU_AQL_CP_SIGNAL=0
-  return bytes >= cw.first && (bytes < cw.second || (lone && single));
+  return bytes >= kCpLo && (bytes < kCpHi || (lone && single));
 }
 
 int bar_alloc(int device, size_t bytes, void** out) {
@@ -1300,8 +1033,7 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
                     mode == 0 || wave_wait ? done + size_t(sl) * kMaxSignalWgs : nullptr};
       uint8_t args[kArgs1Bytes];
       uint32_t grid = 0;
-      int unroll = 4;
-      if (build_aql_args1(sg, dst + b * stride, fs, args, &grid, &unroll) != DORA_OK)
+      if (build_aql_args1(sg, dst + b * stride, fs, args, &grid) != DORA_OK)
         return DORA_ERR_INVALID;
       const uint64_t r = a->next++ % kRingSlots;
       uint8_t* slot = (dev_args ? a->ring + r * kSlotBytes : a->hring + r * kHostSlotBytes);
@@ -1316,7 +1048,7 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
       while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) __builtin_ia32_pause();
       hsa_queue_store_write_index_relaxed(q, idx + 1);
       auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-      const int k = coherent ? 4 : 2;  // dora_aql_pack1c_u4 / dora_aql_pack1_u4
+      const int k = coherent ? kOneCohKernel : kOneKernel;
       p->workgroup_size_x = 256;
       p->workgroup_size_y = 1;
       p->workgroup_size_z = 1;
@@ -1430,7 +1162,10 @@ int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
   ++a->dispatched[k];
   if (hsa_signal_wait_scacquire(a->reduce_sig, HSA_SIGNAL_CONDITION_LT, 1,
                                 uint64_t(5) * 1000000000ull, HSA_WAIT_STATE_ACTIVE) != 0) {
-    a->failed.store(true);  // a reduction that never completes: stop using these queues
+    // A diagnostic: the data-path queues stay in use.  The packet is still queued and may yet
+    // run: its signal is abandoned (a later reduction makes its own), and the caller must not
+    // free or reuse `areas` / `out` (node.cpp leaks them and reads the areas through the BAR).
+    a->reduce_sig.handle = 0;
     return fail(DORA_ERR_TIMEOUT, "stamp reduction did not complete in 5 s");
   }
   return DORA_OK;

@@ -21,7 +21,7 @@ namespace dora {
 struct AqlQueue;
 
 // The process's AQL queue for HIP device `device`, created on first use; nullptr when HSA or
-// the code object cannot be set up (callers then launch through HIP).  DORA_GPU_AQL=0 disables.
+// the code object cannot be set up (callers then launch through HIP).
 AqlQueue* aql_queue(int device);
 // A queue aql_queue returned is still usable (not marked failed): callers may keep the pointer
 // (queues are never freed) instead of looking it up under the global lock on every send.
@@ -40,19 +40,15 @@ bool aql_usable(const AqlQueue* q);
 // `sync`: the caller waits for this pack before it does anything else (a synchronous send,
 // node.cpp wait_source_read).  A single-segment pack that is sent synchronously, or that finds
 // every queue idle, runs alone on the GPU: its arguments go to the device ring and it reads
-// without the acquire fence; a synchronous one (DORA_GPU_AQL_CP_LONE) is also signalled by the
-// command processor at any size >= the CP window's lower bound, with a grid of up to
-// DORA_GPU_CP_GRID workgroups (no done words to poll, so no 1024-workgroup signalling cap).
-// Would a pack of these segments be signalled by the command processor when sent alone
-// (DORA_GPU_AQL_CP_SIGNAL window, DORA_GPU_AQL_CP_MULTI; `lone`: also a lone big pack)?
-bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
-//
-// `read_signal` (sync sends): set when the pack stores the epoch into the flag's read_epoch once
-// it has read its whole source (before its fill completes): the sender may return on that.
+// without the acquire fence; a synchronous one is also signalled by the command processor at any
+// size >= 1 MiB, with a grid of up to 3584 workgroups (no done words to poll, so no
+// 1024-workgroup signalling cap).
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
-             uint64_t* cp_stamps = nullptr, bool sync = false, bool* read_signal = nullptr);
-bool aql_read_signal_enabled();
+             uint64_t* cp_stamps = nullptr, bool sync = false);
+// Would a pack of these segments be signalled by the command processor: [1 MiB, 32 MiB), or
+// (`lone`: a synchronous send) a single-segment pack of any size from 1 MiB.
+bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
 
 // Forget every argument slot whose fill flag lies in [base, base + size) (a node's control
 // region about to be unmapped), after waiting (bounded) for those fills to signal.

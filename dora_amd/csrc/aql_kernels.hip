@@ -19,10 +19,6 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_packb_u4(
   dora::pack::pack_body<4, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
 }
 
-extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack_u8(AqlPackArgs a) {
-  dora::pack::pack_body<8, 2>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
-}
-
 // Single-segment packs (a UInt8 payload at sample offset 0: send_output_raw / _bytes, the C2
 // benchmark) with every argument in SGPRs: the 56 bytes below are preloaded by the command
 // processor once per dispatch (gfx950 kernarg preload, built with
@@ -57,44 +53,13 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u4(
   pack1<4>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
 
-extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1_u8(
-    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
-    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
-  pack1<8>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
-}
-
 // As dora_aql_pack1_u4, reading the source with agent-coherent loads (pack_device.h kCoherent):
-// dispatched without the packet's acquire fence (aql.cpp, DORA_GPU_AQL_COHERENT).
+// dispatched without the packet's acquire fence (aql.cpp dispatch_locked: lone packs and packs
+// the command processor signals inside its window).
 extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
     uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
     uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
   pack1<4, dora::pack::kCoherent>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
-}
-
-// Multi-segment packs without the packet's acquire fence: the one (preloaded) argument is the
-// device-ring slot holding the AqlPackArgs, which the workgroup copies into LDS with
-// agent-coherent loads — a kernarg s_load could be served a stale L2 or scalar-cache line of a
-// slot last used kRingSlots packs ago once no fence invalidates them — and the sources are read
-// coherently as in dora_aql_pack1c_u4 (aql.cpp, DORA_GPU_AQL_COHERENT).
-extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_packc_u4(const AqlPackArgs* ap) {
-  __shared__ AqlPackArgs a;
-  constexpr uint32_t kWords = sizeof(AqlPackArgs) / 4;
-  static_assert(sizeof(AqlPackArgs) % 4 == 0 && kWords <= kThreads, "arguments fit one pass");
-  if (threadIdx.x < kWords) {
-    const auto r = dora::pack::src_rsrc(reinterpret_cast<const uint8_t*>(ap));
-    reinterpret_cast<uint32_t*>(&a)[threadIdx.x] =
-        __builtin_amdgcn_raw_buffer_load_b32(r, threadIdx.x * 4, 0, dora::pack::kCoherentPolicy);
-  }
-  __syncthreads();
-  dora::pack::pack_body<4, dora::pack::kCoherent>(a, __builtin_amdgcn_workgroup_id_x(), a.grid);
-}
-
-// Test kernel: as dora_aql_pack1_u4 with PLAIN (L1-cached) source loads.  Selected only by
-// DORA_GPU_AQL_COHERENT=plain, for the acquire fence's negative control (tests/test_gpu_fence.py).
-extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1p_u4(
-    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* flag, uint32_t* done,
-    uint64_t epoch, uint32_t chunk_bytes, uint32_t grid) {
-  pack1<4, dora::pack::kPlainSrc>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
 
 // Region-end reduction of CP-signalled packs' stamp areas (aql.cpp aql_stamp_reduce, node.cpp

@@ -627,130 +627,3 @@ InterDaemonEvent decode_ide(const uint8_t* p, size_t n) {
 }  // namespace dora
 
 // ---- test hooks (dora_gpu.h) ----
-namespace dora {
-namespace {
-
-int copy_out(const std::vector<uint8_t>& v, uint8_t* out, size_t cap, size_t* out_len) {
-  if (out_len) *out_len = v.size();
-  if (!out || cap < v.size())
-    return dora::fail(DORA_ERR_INVALID, "buffer of %zu bytes, %zu needed", cap, v.size());
-  std::memcpy(out, v.data(), v.size());
-  return DORA_OK;
-}
-
-std::string hex(const uint8_t* p, size_t n) {
-  static const char* d = "0123456789abcdef";
-  std::string s;
-  s.reserve(2 * n);
-  for (size_t i = 0; i < n; ++i) {
-    s.push_back(d[p[i] >> 4]);
-    s.push_back(d[p[i] & 15]);
-  }
-  return s;
-}
-
-std::string jstr(const std::string& v) {
-  std::string s = "\"";
-  for (unsigned char c : v) {
-    if (c == '"' || c == '\\') {
-      s.push_back('\\');
-      s.push_back(static_cast<char>(c));
-    } else if (c < 0x20) {
-      char b[8];
-      std::snprintf(b, sizeof(b), "\\u%04x", c);
-      s += b;
-    } else {
-      s.push_back(static_cast<char>(c));
-    }
-  }
-  return s + "\"";
-}
-
-}  // namespace
-}  // namespace dora
-
-extern "C" int dora_gpu_test_ide_output(const char* dataflow_id, const char* node_id,
-                                        const char* output_id, const uint8_t* type_info,
-                                        size_t type_info_len, const uint8_t* params,
-                                        size_t params_len, uint64_t meta_ns, uint64_t event_ns,
-                                        const uint8_t* hlc_id, const uint8_t* data, size_t data_len,
-                                        int has_data, uint8_t* out, size_t cap, size_t* out_len) {
-  if (!dataflow_id || !node_id || !output_id || !type_info || !hlc_id || (params_len && !params) ||
-      (data_len && !data))
-    return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::InterDaemonEvent e;
-  e.kind = dora::IDE_OUTPUT;
-  e.dataflow_id = dataflow_id;
-  e.node_id = node_id;
-  e.output_id = output_id;
-  e.type_info.assign(type_info, type_info + type_info_len);
-  if (params_len) e.parameters.assign(params, params + params_len);
-  e.timestamp_ns = meta_ns;
-  e.event_ns = event_ns;
-  std::memcpy(e.hlc_id.data(), hlc_id, 16);
-  e.has_data = has_data != 0;
-  if (data_len) e.data.assign(data, data + data_len);
-  std::vector<uint8_t> f;
-  try {
-    dora::encode_ide(e, f);
-  } catch (const std::exception& ex) {
-    return dora::fail(DORA_ERR_INVALID, "%s", ex.what());
-  }
-  return dora::copy_out(f, out, cap, out_len);
-}
-
-extern "C" int dora_gpu_test_ide_inputs_closed(const char* dataflow_id,
-                                               const char* const* receivers,
-                                               const char* const* inputs, size_t n,
-                                               uint64_t event_ns, const uint8_t* hlc_id,
-                                               uint8_t* out, size_t cap, size_t* out_len) {
-  if (!dataflow_id || !hlc_id || (n && (!receivers || !inputs)))
-    return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::InterDaemonEvent e;
-  e.kind = dora::IDE_INPUTS_CLOSED;
-  e.dataflow_id = dataflow_id;
-  for (size_t i = 0; i < n; ++i) e.inputs.emplace_back(receivers[i], inputs[i]);
-  e.event_ns = event_ns;
-  std::memcpy(e.hlc_id.data(), hlc_id, 16);
-  std::vector<uint8_t> f;
-  try {
-    dora::encode_ide(e, f);
-  } catch (const std::exception& ex) {
-    return dora::fail(DORA_ERR_INVALID, "%s", ex.what());
-  }
-  return dora::copy_out(f, out, cap, out_len);
-}
-
-extern "C" int dora_gpu_test_ide_decode(const uint8_t* frame, size_t len, char* json, size_t cap,
-                                        size_t* json_len) {
-  if (!frame && len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::InterDaemonEvent e;
-  try {
-    e = dora::decode_ide(frame, len);
-  } catch (const std::exception& ex) {
-    return dora::fail(DORA_ERR_INVALID, "%s", ex.what());
-  }
-  using dora::hex;
-  using dora::jstr;
-  std::string j = "{\"kind\": " + std::to_string(e.kind) + ", \"dataflow_uuid\": \"" +
-                  hex(e.dataflow_uuid.data(), 16) + "\", \"event_ns\": " +
-                  std::to_string(e.event_ns);
-  if (e.kind == dora::IDE_OUTPUT) {
-    j += ", \"node_id\": " + jstr(e.node_id) + ", \"output_id\": " + jstr(e.output_id) +
-         ", \"metadata_version\": " + std::to_string(e.meta_version) +
-         ", \"meta_ns\": " + std::to_string(e.timestamp_ns) + ", \"type_info\": \"" +
-         hex(e.type_info.data(), e.type_info.size()) + "\", \"parameters\": \"" +
-         hex(e.parameters.data(), e.parameters.size()) + "\", \"has_data\": " +
-         (e.has_data ? "true" : "false") + ", \"data\": \"" + hex(e.data.data(), e.data.size()) +
-         "\"";
-  } else {
-    j += ", \"inputs\": [";
-    for (size_t i = 0; i < e.inputs.size(); ++i)
-      j += (i ? ", [" : "[") + jstr(e.inputs[i].first) + ", " + jstr(e.inputs[i].second) + "]";
-    j += "]";
-  }
-  j += "}";
-  std::vector<uint8_t> v(j.begin(), j.end());
-  v.push_back(0);
-  return dora::copy_out(v, reinterpret_cast<uint8_t*>(json), cap, json_len);
-}

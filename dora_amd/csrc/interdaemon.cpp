@@ -450,14 +450,24 @@ void Gateway::read_loop(int fd) {
                    static_cast<unsigned long long>(len));
       break;
     }
+    // The buffer grows as the bytes arrive, in steps of at most 64 MiB: a length prefix alone
+    // (an unauthenticated peer's 8 bytes) commits no memory beyond the first step.
+    constexpr uint64_t kStep = uint64_t(64) << 20;
+    buf.clear();
+    bool ok = true;
     try {
-      buf.resize(len);
+      while (ok && buf.size() < len) {
+        const size_t at = buf.size();
+        const size_t n = size_t(std::min<uint64_t>(kStep, len - at));
+        buf.resize(at + n);
+        ok = recv_all(fd, buf.data() + at, n);
+      }
     } catch (const std::bad_alloc&) {
       std::fprintf(stderr, "dora-gpu daemon: no memory for a %llu-byte inter-daemon frame\n",
                    static_cast<unsigned long long>(len));
       break;
     }
-    if (!recv_all(fd, buf.data(), len)) break;
+    if (!ok) break;
     InterDaemonEvent e;
     try {
       e = decode_ide(buf.data(), buf.size());

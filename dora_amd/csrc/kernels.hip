@@ -32,55 +32,32 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
 }
 
 // Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
-// DORA_GPU_PACK_VARIANT = u4 | u8 | u4nt | u8nt (tuning knob; default below).
 struct Variant {
   int unroll;
   bool nt;
   bool wt = false;  // write-through (sc1 nt) stores without a fill signal (microbenchmark)
 };
 
-std::atomic<int> g_unroll{0};       // 0 = default (4) / env
-std::atomic<int> g_nt{-1};          // -1 = default (off) / env
-std::atomic<uint32_t> g_chunk{0};   // 0 = auto / env
-// DORA_GPU_LINE_CHUNKS=0: body chunks start at the first aligned unit (pack_device.h kLine)
-bool line_chunks() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_LINE_CHUNKS");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
-uint32_t env_u32(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
-}
-// workgroups of a signalling launch (0: kSignalGrid; DORA_GPU_SIGNAL_GRID, dora_gpu_pack_tune)
-std::atomic<uint32_t> g_signal_grid{env_u32("DORA_GPU_SIGNAL_GRID")};
-// workgroups at most of a pack the command processor signals (DORA_GPU_CP_GRID, default 3584:
-// a synchronous 40.96 MB send (5,000 chunks) takes 21.7-22.0 us with 3584 workgroups against
-// 22.0-22.7 with 4096, 22.9 with one per chunk, 22.7-23.3 with 3072 and 24.6-25.3 with fewer,
-// larger chunks, in four interleaved rounds of 200 sends, profiles/r04_sync_ab.jsonl batches
-// sy4-sy6; packs below 28 MiB have fewer chunks than that)
-std::atomic<uint32_t> g_cp_grid{env_u32("DORA_GPU_CP_GRID") ? env_u32("DORA_GPU_CP_GRID") : 3584u};
+// Microbenchmark tuning of HIP-launched packs (pack_tune, the test library's
+// dora_gpu_test_pack_tune): 0 / -1 = the defaults below.
+std::atomic<int> g_unroll{0};
+std::atomic<int> g_nt{-1};
+std::atomic<uint32_t> g_chunk{0};
+// workgroups of a signalling launch (0: kSignalGrid)
+std::atomic<uint32_t> g_signal_grid{0};
+// workgroups at most of a pack the command processor signals (3584: a synchronous 40.96 MB send
+// (5,000 chunks) takes 21.7-22.0 us with 3584 workgroups against 22.0-22.7 with 4096, 22.9 with
+// one per chunk, 22.7-23.3 with 3072 and 24.6-25.3 with fewer, larger chunks, in four interleaved
+// rounds of 200 sends, profiles/r04_sync_ab.jsonl batches sy4-sy6; packs below 28 MiB have fewer
+// chunks than that)
+std::atomic<uint32_t> g_cp_grid{3584u};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
 // 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
-// cache) and are neutral below; 8 loads in flight per lane for large bodies.
+// cache) and are neutral below.
 Variant pack_variant() {
-  static const Variant env = [] {
-    Variant d{0, true};
-    if (const char* e = std::getenv("DORA_GPU_PACK_VARIANT")) {
-      const std::string s(e);
-      if (s.rfind("u8", 0) == 0) d.unroll = 8;
-      if (s.rfind("u4", 0) == 0) d.unroll = 4;
-      if (s.rfind("u2", 0) == 0) d.unroll = 2;
-      d.nt = s.find("nt") != std::string::npos;
-    }
-    return d;
-  }();
-  Variant v = env;
+  Variant v{0, true};
   if (const int u = g_unroll.load(std::memory_order_relaxed)) v.unroll = u;
   if (const int nt = g_nt.load(std::memory_order_relaxed); nt >= 0) {
     v.nt = nt != 0;
@@ -165,13 +142,6 @@ int default_unroll(uint64_t) { return 4; }
 
 uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
   if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
-  // read once: getenv scans the environment (~0.1 us per send on the AQL path)
-  static const uint32_t env_chunk = [] {
-    const char* e = std::getenv("DORA_GPU_PACK_CHUNK");
-    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-    return v >= kLine && v % kLine == 0 && v <= (1u << 30) ? static_cast<uint32_t>(v) : 0u;
-  }();
-  if (env_chunk) return env_chunk;
   // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
   // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
   // 8-32 MB preferred 32 KiB x 8 loads in isolation (the 8-load variant's chunk, kept for the
@@ -362,12 +332,11 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     for (size_t k = 0; k < m; ++k) {
       const Segment& s = segs[i + k];
       a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
-      chunks += segment_chunks(reinterpret_cast<uintptr_t>(dst), s.dst_off, s.len, a.chunk_bytes,
-                               line_chunks());
+      chunks += segment_chunks(reinterpret_cast<uintptr_t>(dst), s.dst_off, s.len, a.chunk_bytes);
       if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
       a.chunk_end[k] = static_cast<uint32_t>(chunks);
     }
-    a.nseg = static_cast<uint32_t>(m) | (line_chunks() ? 0u : kUnitChunks);
+    a.nseg = static_cast<uint32_t>(m);
     // one launch holding the whole plan: its boundary units may be written whole
     if (!any_x && m == n) a.edge_mask = edge_mask(segs, n, dst, dst_cap);
     const bool first = launch == 0, last = launch + 1 == n_launch;
@@ -494,9 +463,7 @@ size_t aql_batch_args_size() { return sizeof(dora::pack::AqlBatchArgs); }
 uint32_t aql_chunk_bytes(const Segment* segs, size_t n) {
   uint64_t body = 0;
   for (size_t k = 0; k < n; ++k) body += segs[k].len;
-  Variant var = pack_variant();
-  if (var.unroll == 0) var.unroll = default_unroll(body);
-  return choose_chunk_bytes(body, var.unroll);
+  return choose_chunk_bytes(body, 4);  // the AQL kernels keep 4 loads in flight per lane
 }
 
 // Arguments of dora_aql_packb_u4: the segments of `n` messages with absolute destinations,
@@ -537,12 +504,12 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
   uint64_t chunks = 0;
   for (size_t k = 0; k < ns; ++k) {
     a.seg[k] = {all[k].src, all[k].dst, all[k].len};
-    chunks += segment_chunks(0, all[k].dst, all[k].len, chunk, line_chunks());
+    chunks += segment_chunks(0, all[k].dst, all[k].len, chunk);
     if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
     a.chunk_end[k] = static_cast<uint32_t>(chunks);
     a.edge_mask |= uint64_t(all[k].edge) << (2 * k);
   }
-  a.nseg = static_cast<uint32_t>(ns) | (line_chunks() ? 0u : kUnitChunks);
+  a.nseg = static_cast<uint32_t>(ns);
   a.n_chunks = static_cast<uint32_t>(chunks);
   const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
   const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
@@ -558,7 +525,7 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
 }
 
 // Workgroups of an AQL pack signalled as `sig` says.  In-kernel signals (a flag): the signalling
-// grid (kSignalGrid, or DORA_GPU_SIGNAL_GRID up to the kMaxSignalWgs done words).  Signalled by
+// grid (kSignalGrid, or a tuned grid up to the kMaxSignalWgs done words).  Signalled by
 // the command processor (no flag): nothing to poll, so up to aql_cp_grid() workgroups — a lone
 // 40.96 MB pack capped at 1024 keeps 8 MiB in flight, half of what HBM needs.
 uint32_t aql_cp_grid() { return std::max<uint32_t>(1, g_cp_grid.load(std::memory_order_relaxed)); }
@@ -569,31 +536,10 @@ uint64_t signal_grid_cap(const FillSignal& sig) {
   return g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
 }
 
-// DORA_GPU_BALANCED_CHUNKS=1: when a pack has more chunks than workgroups (a C3 cloud: 1,587
-// chunks of 8 KiB over 1,024 workgroups, so 563 workgroups copy two chunks and the rest one),
-// the chunk grows in whole lines until every workgroup copies at most one (13 MB: ~12.5 KiB
-// each, 4 loads in flight per lane over ~1 pass).  `count(c)` = the pack's chunks at size c.
-bool balanced_chunks() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_BALANCED_CHUNKS");
-    return e && *e == '1';
-  }();
-  return v;
-}
-
-template <class F>
-uint32_t balance_chunk(uint32_t chunk, uint64_t body, uint64_t grid_cap, F count) {
-  if (!balanced_chunks() || count(chunk) <= grid_cap) return chunk;
-  uint64_t c = ((body + grid_cap - 1) / grid_cap + kLine - 1) / kLine * kLine;
-  for (int i = 0; i < 64 && count(c) > grid_cap; ++i) c += kLine * uint64_t(i + 1);
-  return c <= (uint64_t(1) << 30) && count(c) <= grid_cap ? uint32_t(c) : chunk;
-}
-
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid_out, int* unroll_out,
-                   uint64_t dst_cap) {
+                   uint8_t* out, size_t cap, uint32_t* grid_out, uint64_t dst_cap) {
   if (n == 0 || n > size_t(kMaxAqlSegs)) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   if (cap < sizeof(AqlPackArgs)) return fail(DORA_ERR_INVALID, "AQL pack: argument buffer");
   AqlPackArgs a;
@@ -604,25 +550,17 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
     if (segs[k].op != SEG_COPY) return fail(DORA_ERR_INVALID, "AQL pack: transform segment");
     body += segs[k].len;
   }
-  Variant var = pack_variant();
-  if (var.unroll == 0) var.unroll = default_unroll(body);
-  a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
+  a.chunk_bytes = choose_chunk_bytes(body, 4);
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
-  a.chunk_bytes = balance_chunk(a.chunk_bytes, body, signal_grid_cap(sig), [&](uint64_t c) {
-    uint64_t t = 0;
-    for (size_t k = 0; k < n; ++k)
-      t += segment_chunks(base, segs[k].dst_off, segs[k].len, c, line_chunks());
-    return t;
-  });
   uint64_t chunks = 0;
   for (size_t k = 0; k < n; ++k) {
     const Segment& s = segs[k];
     a.seg[k] = {static_cast<const uint8_t*>(s.src), s.dst_off, s.len};
-    chunks += segment_chunks(base, s.dst_off, s.len, a.chunk_bytes, line_chunks());
+    chunks += segment_chunks(base, s.dst_off, s.len, a.chunk_bytes);
     if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
     a.chunk_end[k] = static_cast<uint32_t>(chunks);
   }
-  a.nseg = static_cast<uint32_t>(n) | (line_chunks() ? 0u : kUnitChunks);
+  a.nseg = static_cast<uint32_t>(n);
   a.edge_mask = edge_mask(segs, n, dst, dst_cap);
   a.n_chunks = static_cast<uint32_t>(chunks);
   a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
@@ -631,7 +569,6 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.epoch = sig.epoch;
   std::memcpy(out, &a, sizeof(a));
   *grid_out = a.grid;
-  *unroll_out = var.unroll == 8 ? 8 : 4;
   return DORA_OK;
 }
 
@@ -639,19 +576,13 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
 // dst, src, len, flag, done, epoch, chunk_bytes, grid — 56 bytes, the same chunk shape and grid
 // build_aql_args chooses for one segment at sample offset 0.
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
-                    uint32_t* grid_out, int* unroll_out, uint64_t grid_cap) {
+                    uint32_t* grid_out) {
   if (sg.op != SEG_COPY || sg.dst_off != 0)
     return fail(DORA_ERR_INVALID, "AQL single-segment pack: segment at offset %llu",
                 (unsigned long long)sg.dst_off);
-  Variant var = pack_variant();
-  if (var.unroll == 0) var.unroll = default_unroll(sg.len);
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
-  // a caller's cap (a lone in-kernel-signalled pack: up to the kMaxSignalWgs done words)
-  const uint64_t cap = grid_cap ? std::min<uint64_t>(grid_cap, sig.flag ? kMaxSignalWgs : grid_cap)
-                                : signal_grid_cap(sig);
-  const uint32_t chunk_bytes =
-      balance_chunk(choose_chunk_bytes(sg.len, var.unroll), sg.len, cap,
-                    [&](uint64_t c) { return segment_chunks(base, 0, sg.len, c); });
+  const uint64_t cap = signal_grid_cap(sig);
+  const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, 4);
   const uint64_t chunks = segment_chunks(base, 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap));
@@ -662,7 +593,6 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
   std::memcpy(out + 48, &chunk_bytes, 4);
   std::memcpy(out + 52, &grid, 4);
   *grid_out = grid;
-  *unroll_out = var.unroll == 8 ? 8 : 4;
   return DORA_OK;
 }
 
@@ -766,6 +696,28 @@ int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, u
   return DORA_OK;
 }
 
+// Microbenchmark tuning of HIP-launched packs (the test library's dora_gpu_test_pack_tune /
+// dora_gpu_test_pack_signal_tune): 16-B loads in flight per lane (0 = default 4; 2, 4, 8),
+// non-temporal policy (-1 default, 0, 1; 2 = the signalling kernels' write-through stores
+// without a signal), bytes per workgroup (0 = auto, else a multiple of 128); workgroups of a
+// signalling launch (0: kSignalGrid), and whether dora_gpu_pack signals a scratch flag.
+int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
+  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8)
+    return fail(DORA_ERR_INVALID, "unroll must be 0, 2, 4 or 8");
+  if (chunk_bytes % pack::kLine)
+    return fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 128 (a cache line)");
+  g_unroll.store(unroll);
+  g_nt.store(nontemporal < 0 ? -1 : nontemporal == 2 ? 2 : (nontemporal ? 1 : 0));
+  g_chunk.store(chunk_bytes);
+  return DORA_OK;
+}
+
+int pack_signal_tune(uint32_t grid, bool bench_signal) {
+  g_signal_grid.store(grid);
+  g_bench_signal.store(bench_signal);
+  return DORA_OK;
+}
+
 int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
   if (!len) return DORA_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
@@ -808,25 +760,6 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                            nullptr, nullptr, nullptr, dst_len);
 }
 
-int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal) {
-  dora::g_signal_grid.store(grid);
-  dora::g_bench_signal.store(bench_signal != 0);
-  return DORA_OK;
-}
-
-int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
-  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8)
-    return dora::fail(DORA_ERR_INVALID, "unroll must be 0, 2, 4 or 8");
-  if (chunk_bytes % dora::pack::kLine)
-    return dora::fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 128 (a cache line)");
-  dora::g_unroll.store(unroll);
-  // 2: the signalling kernels' write-through stores in a launch that signals nothing (to
-  // separate the store policy's cost from the fill signal's in scripts/pack_microbench.py)
-  dora::g_nt.store(nontemporal < 0 ? -1 : nontemporal == 2 ? 2 : (nontemporal ? 1 : 0));
-  dora::g_chunk.store(chunk_bytes);
-  return DORA_OK;
-}
-
 int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream_t stream) {
   if (!out_dev || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   return dora::launch_csum(data, len, out_dev, static_cast<hipStream_t>(stream));
@@ -845,40 +778,6 @@ int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uin
   }
   (void)hipFree(d);
   return rc;
-}
-
-int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
-                             const uint64_t* dsts, const uint64_t* dst_caps,
-                             const uint64_t* flags, const uint64_t* epochs, uint8_t* out,
-                             size_t cap, uint32_t* grid) {
-  if (!n_msgs || !seg_counts || !segs || !dsts || !dst_caps || !flags || !epochs || !out || !grid)
-    return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  if (n_msgs > 8) return dora::fail(DORA_ERR_INVALID, "batch of %zu messages", n_msgs);
-  std::vector<std::vector<dora::Segment>> s(n_msgs);
-  dora::BatchItem items[8];
-  size_t k = 0;
-  for (size_t m = 0; m < n_msgs; ++m) {
-    for (size_t j = 0; j < seg_counts[m]; ++j, ++k)
-      s[m].push_back({reinterpret_cast<const void*>(segs[3 * k]), segs[3 * k + 1], segs[3 * k + 2]});
-    items[m] = {s[m].data(), s[m].size(), reinterpret_cast<uint8_t*>(dsts[m]),
-                dora::FillSignal{reinterpret_cast<uint64_t*>(flags[m]), epochs[m], nullptr},
-                dst_caps[m]};
-  }
-  return dora::build_aql_batch_args(items, n_msgs, out, cap, grid);
-}
-
-int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream) {
-  if (!data && len) return dora::fail(DORA_ERR_INVALID, "data is NULL");
-  return dora::launch_l2_touch(data, len, static_cast<hipStream_t>(stream));
-}
-
-int dora_gpu_test_l1_stale(int device, int mode, uint32_t* bad_first, uint32_t* stale,
-                           uint32_t* blocks) {
-  if (!bad_first || !stale || !blocks || mode < 0 || mode > 2)
-    return dora::fail(DORA_ERR_INVALID, "bad l1 stale probe arguments");
-  DORA_GUARD_BEGIN
-  return dora::l1_stale_probe(device, mode, bad_first, stale, blocks);
-  DORA_GUARD_END
 }
 
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream) {

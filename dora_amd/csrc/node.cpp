@@ -160,9 +160,6 @@ void release_slot_memory(Slot* s) {
   delete s;
 }
 
-// Async sends (default): the sender records the slot's interprocess event after the pack and
-// sends at once; the receiver waits on that event before handing the input out.  Sync sends
-// synchronise the node stream before the descriptor leaves (DORA_GPU_SEND_MODE=sync).
 // getpid() is a system call on current glibc; the descriptor path asks for it per message.
 // Cached per process, refreshed in a forked child.
 int self_pid() {
@@ -175,14 +172,6 @@ int self_pid() {
     pid.store(p, std::memory_order_relaxed);
   }
   return p;
-}
-
-bool async_sends() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_SEND_MODE");
-    return !(e && std::string(e) == "sync");
-  }();
-  return v;
 }
 
 // Samples a node may have in flight (sent, token not yet back) before an allocation waits.
@@ -214,70 +203,14 @@ size_t max_in_flight(uint64_t len) {
   return len < kSmallInFlightBytes ? 11 : 8;
 }
 
-// Opt-in (DORA_GPU_SPLIT_IN_FLIGHT=1): the cap above bounds only the samples whose fill has
-// COMPLETED and whose token is not back, while samples still being packed count against this
-// larger total (24 below 8 MiB, 12 below 32 MiB, 8 above; DORA_GPU_MAX_TOTAL_IN_FLIGHT), so a
-// burst keeps the GPU's queues and batch packs fed.  Not the default: fills still in transit
-// complete while a receiver pauses, so a queue_size-10 receiver that pauses during a burst then
-// finds more than 10 ready inputs and drops (r03: 473 of 2000 4 MB inputs in
-// test_default_queue_keeps_up_with_async_burst) — the total in flight is what bounds it.
-size_t max_total_in_flight(uint64_t len) {
-  static const long env = [] {
-    const char* e = std::getenv("DORA_GPU_MAX_TOTAL_IN_FLIGHT");
-    return e ? std::atol(e) : 0L;
-  }();
-  static const bool split = [] {
-    const char* e = std::getenv("DORA_GPU_SPLIT_IN_FLIGHT");
-    return e && *e == '1';
-  }();
-  const size_t cap = max_in_flight(len);
-  if (!split) return cap;
-  if (env > 0) return std::max(cap, static_cast<size_t>(env));
-  const size_t d = len < kSmallInFlightBytes ? 24 : len < (uint64_t(32) << 20) ? 12 : 8;
-  return std::max(cap, d);
-}
+// Streams the HIP-launched fills of a node rotate over (host sources, compacting transforms,
+// relays; device-source packs go to the AQL queues, aql.h).  A pack ends in a drain tail (its
+// last workgroups, the fill signal) and starts with a ramp; on one stream consecutive fills
+// serialise those, on three hardware queues the next fill streams through them (r01 probe,
+// profiles/r01_stream_probe.jsonl: 40.96 MB 17.1 -> 13.2 us per message, 16 MB 9.8 -> 6.0).
+constexpr size_t kFillStreams = 3;
 
-// Streams the sends of a node spread their fills over (DORA_GPU_FILL_STREAMS, default 3).  A
-// pack ends in a drain tail (its last workgroups, the fill signal) and starts with a ramp; on
-// one stream consecutive fills serialise those, on three hardware queues the next fill streams
-// through them (r01 probe, profiles/r01_stream_probe.jsonl: 40.96 MB 17.1 -> 13.2 us per
-// message, 16 MB 9.8 -> 6.0).  1 = every fill on the node stream.
-size_t fill_stream_count() {
-  static const size_t v = [] {
-    const char* e = std::getenv("DORA_GPU_FILL_STREAMS");
-    long x = e ? std::atol(e) : 3;
-    return static_cast<size_t>(x < 1 ? 1 : x > 8 ? 8 : x);
-  }();
-  return v;
-}
-
-// Validity bitmaps of device arrays travel in the sample's tail (DORA_GPU_VALIDITY=inline:
-// in the metadata, as the reference's ArrowTypeInfo carries them).  Sending a device array then
-// reads nothing back to the host: the plan is a host walk and one pack launch copies buffers
-// and bitmaps; receivers import the bitmaps zero-copy (C3: 125 KB per cloud no longer crosses
-// PCIe twice and the control plane once per message).
-bool validity_in_sample() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_VALIDITY");
-    return !(e && std::string(e) == "inline");
-  }();
-  return v;
-}
-
-// Packs of device sources are dispatched on the process's own AQL queues (aql.h) instead of
-// hipLaunchKernel: ~0.5 us of host time instead of 3-5, and no 12-20 us first launch after an
-// idle period (profiles/r02_aql_big_ab.jsonl).  Packs >= 32 MiB run in order per queue there
-// (aql.cpp), which keeps the 40.96 MB packs at the fill streams' device time.
-// DORA_GPU_AQL_MAX_BYTES caps the size (larger packs go to the HIP fill streams);
-// DORA_GPU_AQL=0 disables the path.
-uint64_t aql_max_bytes() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_AQL_MAX_BYTES");
-    return e ? std::strtoull(e, nullptr, 10) : ~uint64_t(0);
-  }();
-  return v;
-}
-
+// DORA_GPU_PIN=0: leave the node's CPU affinity alone (shm.cpp pin_to_numa)
 bool numa_pinning() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_PIN");
@@ -300,14 +233,9 @@ int gpu_numa_node(int device) {
   return numa;
 }
 
-uint64_t timing_sample() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_TIMING_SAMPLE");
-    long x = e ? std::atol(e) : 8;
-    return static_cast<uint64_t>(x > 0 ? x : 8);
-  }();
-  return v;
-}
+// With profiling on, every n-th pack launch is stamped with timing events (default period;
+// dora_node_set_timing_period)
+constexpr uint64_t kTimingPeriod = 8;
 
 enum PeerCopyMode { PEER_KERNEL, PEER_SDMA };
 
@@ -321,7 +249,8 @@ PeerCopyMode peer_copy_mode() {
   return v;
 }
 
-// Force the cross-GPU copy path on same-GPU edges (tests on a one-GPU box).
+// DORA_GPU_EDGE_COPY=1 (testing): the cross-GPU receive path on same-GPU edges, the one-GPU
+// rehearsal of C4/C5 (tests, bench.py DORA_BENCH_GPUS).
 bool edge_copy_forced() {
   static const bool v = [] {
     const char* e = std::getenv("DORA_GPU_EDGE_COPY");
@@ -340,13 +269,9 @@ bool fanout_rccl() {
   return v;
 }
 
-uint64_t slot_wait_ns() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_SLOT_WAIT_US");
-    return uint64_t(e ? std::atoll(e) : 5000) * 1000;
-  }();
-  return v;
-}
+// How long an allocation waits for a returned token at the in-flight cap before it allocates
+// anyway, as the reference would (a receiver may legitimately hold many inputs)
+constexpr uint64_t kSlotWaitNs = 5000000;
 
 // Slots of every node in this process by process-wide id: a sample whose owner is this process
 // (another node here, or the node itself) is read in place — IPC handles cannot be opened in
@@ -385,7 +310,7 @@ struct NodeCore {
   int idx = -1;
   int device = 0;
   hipStream_t stream = nullptr;
-  // Fill streams (fill_stream_count() > 1): sends rotate over them.  Work already queued on the
+  // Fill streams (kFillStreams): HIP-launched fills rotate over them.  Work already queued on the
   // node stream is ordered before a fill (node_ev), and fills are ordered before node-stream
   // work queued after dora_node_stream() hands the stream out (fence_fills).
   std::vector<hipStream_t> fill_streams;
@@ -578,9 +503,8 @@ struct NodeCore {
   void ensure_fill_streams() {
     if (!fill_streams.empty() || fill_streams_tried) return;
     fill_streams_tried = true;
-    if (fill_stream_count() > 1 && async_sends() &&
-        hipEventCreateWithFlags(&node_ev, hipEventDisableTiming) == hipSuccess) {
-      for (size_t i = 0; i < fill_stream_count(); ++i) {
+    if (hipEventCreateWithFlags(&node_ev, hipEventDisableTiming) == hipSuccess) {
+      for (size_t i = 0; i < kFillStreams; ++i) {
         hipStream_t s = nullptr;
         hipEvent_t e = nullptr;
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
@@ -708,7 +632,6 @@ struct dora_sample {
   uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
   uint64_t epoch = 0;
   bool stamped = false;  // the pack kernel stamps its start / signal time into the flag line
-  bool read_signal = false;  // the pack stores read_epoch once it has read its source (aql.h)
 };
 
 namespace dora {
@@ -745,9 +668,6 @@ struct dora_node {
   // samples sent, by drop token (map nodes from a pool: no malloc per send)
   std::pmr::unsynchronized_pool_resource sent_pool;
   std::pmr::unordered_map<dora::DropToken, dora::Slot*, dora::DropTokenHash> sent_out{&sent_pool};
-  // fills of sent samples not yet seen complete, in send order (flag, epoch): the in-transit
-  // part of sent_out (max_total_in_flight)
-  std::deque<std::pair<const std::atomic<uint64_t>*, uint64_t>> transit;
   dora::WBuf send_buf;                 // request encoding scratch of send_sample, reused
   std::vector<uint8_t> ti_buf;         // type-info scratch of pack_and_send, reused
   dora_plan bytes_plan;                // send_output_bytes: the one-buffer plan, re-pointed
@@ -760,7 +680,7 @@ struct dora_node {
   std::vector<dora::TimingPair> timing;  // ring of kTimingPairs
   size_t timing_next = 0;
   uint64_t timing_seq = 0;
-  uint64_t timing_period = 0;            // stamp every n-th pack (0: DORA_GPU_TIMING_SAMPLE)
+  uint64_t timing_period = 0;            // stamp every n-th pack (0: kTimingPeriod)
   hipEvent_t timing_ref = nullptr;       // recorded when profiling is (re)enabled
   std::vector<double> intervals;         // (start, stop) ms after timing_ref per stamped pack
   // Timed region (dora_node_region_begin/end): the first pack after begin stamps its start;
@@ -835,9 +755,8 @@ void harvest_region_stamp(dora_node* n, Slot* s) {
   if (s->region_cp_area >= 0 && ff.epoch.load(std::memory_order_acquire) != s->region_epoch &&
       ff.cp_epoch.load(std::memory_order_acquire) == s->region_epoch) {
     n->region_cp_used.push_back(uint32_t(s->region_cp_area));  // resolved at region_end
-  } else if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch ||
-             ff.read_epoch.load(std::memory_order_acquire) == s->region_epoch) {
-    // an in-kernel-signalled fill, or a read-signalled one (its workgroup 0 stamps the line)
+  } else if (ff.epoch.load(std::memory_order_acquire) == s->region_epoch) {
+    // an in-kernel-signalled fill (its workgroup 0 stamps the line)
     const uint64_t a = ff.t_start, b = ff.t_end;
     if (b >= a && a) {
       if (!n->region_stamped || a < n->region_tmin) n->region_tmin = a;
@@ -1073,7 +992,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   s->id = own_slots().next_id.fetch_add(1);
   hipError_t e = hipMalloc(&s->ptr, slot_bytes(len));
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
-  if (e == hipSuccess && async_sends()) {
+  if (e == hipSuccess) {
     if (n->core->region_dev && !n->core->free_flags.empty()) {
       s->flag = static_cast<int>(n->core->free_flags.back());
       n->core->free_flags.pop_back();
@@ -1377,9 +1296,8 @@ void finish_input(dora_node* n, dora_event* ev) {
       // in-kernel-signalled fill of exactly this epoch writes them (a CP-signalled fill writes
       // none, and the line may already carry a later fill's stamps if the slot was refilled)
       const FillFlag& ff = h->nodes[d.flag_node].fill[d.flag_index];
-      if ((ff.epoch.load(std::memory_order_acquire) == d.epoch &&
-           ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) ||
-          ff.read_epoch.load(std::memory_order_acquire) == d.epoch) {
+      if (ff.epoch.load(std::memory_order_acquire) == d.epoch &&
+          ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) {
         const double ns_per_tick = 1e9 / kRealtimeHz;
         trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
         trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
@@ -1509,16 +1427,9 @@ int ensure_local(InputData* in) {
 // made the receiver drop inputs whenever it waited on the GPU: 20-25 % of a 1-4 MB burst from
 // the Python node (scripts/py_tp.py), inputs the reference would have delivered.
 // How long an input may sit in the queue uncounted because its producer's fill has not
-// signalled (DORA_GPU_TRANSIT_LIMIT_MS, default 2000): past that the drop-oldest policy counts
-// it again, so a fill that never completes (a lost queue, a GPU fault) cannot grow the queue
-// beyond its queue_size.
-uint64_t transit_limit_ns() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_TRANSIT_LIMIT_MS");
-    return uint64_t(e ? std::strtoull(e, nullptr, 10) : 2000) * 1000000ull;
-  }();
-  return v;
-}
+// signalled: past 2 s the drop-oldest policy counts it again, so a fill that never completes (a
+// lost queue, a GPU fault) cannot grow the queue beyond its queue_size.
+constexpr uint64_t kTransitLimitNs = 2000000000ull;
 
 bool fill_in_transit(dora_node* n, const dora_event* e) {
   if (!e->pending || e->ipc.fill != FILL_FLAG) return false;
@@ -1526,7 +1437,7 @@ bool fill_in_transit(dora_node* n, const dora_event* e) {
   if (e->ipc.flag_node >= h->n_nodes || e->ipc.flag_index >= kFillFlags) return false;
   if (fill_reached(&h->nodes[e->ipc.flag_node].fill[e->ipc.flag_index].epoch, e->ipc.epoch))
     return false;
-  return mono_ns() - e->arrived_ns < transit_limit_ns();
+  return mono_ns() - e->arrived_ns < kTransitLimitNs;
 }
 
 // drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
@@ -1672,27 +1583,10 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
     if (token_out) *token_out = d.shm.token;
   } else if (slot) {
     n->sent_out[d.ipc.token] = slot;
-    if (d.ipc.fill == FILL_FLAG) {
-      auto& t = n->transit;
-      t.emplace_back(n->core->flag_host(static_cast<int>(d.ipc.flag_index)), d.ipc.epoch);
-      // bounded even for a sender that never reaches its cap
-      while (t.size() > 256 && fill_reached(t.front().first, t.front().second))
-        t.pop_front();
-      if (t.size() > 1024) t.pop_front();
-    }
     if (token_out) *token_out = d.ipc.token;
     trace(TP_SENT, d.ipc.token);
   }
   return DORA_OK;
-}
-
-// Sent samples whose fill has not been seen complete (the front of `transit` completes first:
-// fills of one sender finish roughly in order; one flag load per completed fill).
-size_t in_transit(dora_node* n) {
-  auto& t = n->transit;
-  while (!t.empty() && fill_reached(t.front().first, t.front().second))
-    t.pop_front();
-  return t.size();
 }
 
 constexpr uint64_t kZeroCopyThreshold = 4096;  // mod.rs:40
@@ -1704,14 +1598,10 @@ constexpr uint32_t kRegionCpAreas = 256;
 constexpr size_t kCpAreaWords = 1 + kCpStampWgs;
 
 // Stamp areas for timed regions' CP-signalled packs (dora_node_region_begin), made and zeroed with
-// the node's AQL queues at its first send, never inside or just before a region
-// (DORA_GPU_REGION_CP_STAMPS=0: none; such packs then signal in-kernel inside regions).
+// the node's AQL queues at its first send, never inside or just before a region (without them,
+// e.g. no large BAR, such packs signal in-kernel inside regions).
 void ensure_cp_stamps(dora_node* n) {
-  static const bool on = [] {
-    const char* v = std::getenv("DORA_GPU_REGION_CP_STAMPS");
-    return !(v && *v == '0');
-  }();
-  if (!on || n->region_cp_stamps || n->core->device < 0) return;
+  if (n->region_cp_stamps || n->core->device < 0) return;
   const size_t bytes = size_t(kRegionCpAreas) * kCpAreaWords * 8;
   void* d = nullptr;
   if (bar_alloc(n->core->device, bytes, &d) != DORA_OK) {
@@ -1777,21 +1667,13 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out, uint64_t ext_len
     SubSpan sp_tok(SP_ALLOC_TOKENS);
     handle_finished_drop_tokens(n);
     sp_tok.stop();
-    // Async sends run ahead of the GPU; bound the samples in flight so the sender waits for a
+    // Sends run ahead of the GPU; bound the samples in flight so the sender waits for a
     // returned slot instead of hipMalloc-ing new ones (a device slot costs far more to create
-    // than a shm region).
-    // After `slot_wait_ns` without a returned token the slot is allocated anyway, as the
-    // reference would (a receiver may legitimately hold many inputs).
+    // than a shm region).  After kSlotWaitNs without a returned token the slot is allocated
+    // anyway, as the reference would (a receiver may legitimately hold many inputs).
     SubSpan sp_wait(SP_ALLOC_WAIT);
     const uint64_t t0 = mono_ns();
-    // completed-and-unreturned samples against the cap, everything against the total
-    auto blocked = [&] {
-      const size_t total = n->sent_out.size();
-      if (total >= max_total_in_flight(len)) return true;
-      if (total < max_in_flight(len)) return false;
-      return total - std::min(total, in_transit(n)) >= max_in_flight(len);
-    };
-    while (async_sends() && blocked() && mono_ns() - t0 < slot_wait_ns()) {
+    while (n->sent_out.size() >= max_in_flight(len) && mono_ns() - t0 < kSlotWaitNs) {
       n->core->drops.wait(1000);
       handle_finished_drop_tokens(n);
       if (n->core->region->hdr()->nodes[n->core->idx].state.load() == 2) break;
@@ -1875,16 +1757,6 @@ hipError_t order_fill(dora_node* n, dora_sample* s, hipStream_t st) {
   return hipStreamSynchronize(st);
 }
 
-// The pack kernel signals the fill flag itself (DORA_GPU_KERNEL_SIGNAL=0: a separate stream
-// write-value packet after the kernel, which ROCm runs as a ~4 us blit kernel).
-bool kernel_signal() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_KERNEL_SIGNAL");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
-
 // Launch the fill of sample `s` (segments into its slot) on stream `st` and order its
 // completion signal.
 int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
@@ -1898,14 +1770,14 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   }
   FillSignal sig{};
   const FillSignal* sp = nullptr;
-  if (s->slot->flag >= 0 && n->core->fill_done && kernel_signal()) {
+  if (s->slot->flag >= 0 && n->core->fill_done) {
     sig.flag = n->core->flag_dev(s->slot->flag);
     sig.epoch = ++n->core->epoch;
     sig.done = n->core->fill_done + size_t(s->slot->flag) * kMaxSignalWgs;
     sp = &sig;
   }
   if (sp && !st && !t_start && !t_stop && dev == ARROW_DEVICE_ROCM &&
-      nseg <= aql_max_segments() && std::max(s->len, s->ext_len) < aql_max_bytes() &&
+      nseg <= aql_max_segments() &&
       std::all_of(segs, segs + nseg, [](const Segment& g) { return g.op == SEG_COPY; }) &&
       [&] {
         SubSpan sq(SP_STREAM_QUERY);
@@ -1921,17 +1793,15 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       // a timed region's pack may be signalled by the command processor if it has a stamp area
       int area = -1;
       uint64_t* stamps = nullptr;
-      // (a synchronous send's read-signalled pack stamps the flag line instead)
+      // (only a pack aql_pack will CP-signal takes one: a region has kRegionCpAreas of them)
       if (n->region_armed && n->region_cp_stamps && n->region_cp_next < kRegionCpAreas &&
-          aql_cp_candidate(segs, nseg, /*lone=*/true) && !(sync && aql_read_signal_enabled())) {
+          aql_cp_candidate(segs, nseg, sync)) {
         area = int(n->region_cp_next++);
         stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
       }
       s->slot->region_cp_area = area;
-      bool read_sig = false;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync, &read_sig) == DORA_OK) {
-        s->read_signal = read_sig;
+                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -1967,14 +1837,6 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
 // Re-send a received input on an output with its type info (a relay stage): one copy into a
 // fresh slot of this node — for a cross-GPU input straight from the peer's slot over xGMI, so
 // a pipeline hop moves the payload once.
-// DORA_GPU_FORWARD_COPY=1: relays always copy (no in-place re-send).
-bool forward_copy_forced() {
-  static const bool v = [] {
-    const char* e = std::getenv("DORA_GPU_FORWARD_COPY");
-    return e && *e && *e != '0';
-  }();
-  return v;
-}
 
 // A same-GPU device input re-sent in place: the descriptor points at the producer's slot (its
 // fill is complete: the input was handed out), under a token of this node; the input — and with
@@ -2013,7 +1875,7 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
   }
   if (in->has_token && !in->local && in->remote_device < 0 && in->len && !in->host_mem &&
       ev->ipc.device == n->core->device && ev->ipc.fill != FILL_BCAST && !edge_copy_forced() &&
-      !forward_copy_forced() && !n->bcast_out.count(output_id))
+      !n->bcast_out.count(output_id))
     return forward_in_place(n, output_id, ev, params, params_len);
   const uint64_t len = in->len;
   const uint64_t ext = std::max(in->ext_len, len);  // the validity tail travels along
@@ -2113,7 +1975,6 @@ void form_bcast_groups(dora_node* n) {
 struct SourceWait {
   uint8_t kind = FILL_DONE;  // FILL_FLAG: flag >= epoch; FILL_EVENT: event; FILL_BCAST: stream
   const std::atomic<uint64_t>* flag = nullptr;
-  const std::atomic<uint64_t>* read = nullptr;  // the flag's read_epoch, if the pack stores it
   uint64_t epoch = 0;
   hipEvent_t event = nullptr;
 };
@@ -2127,9 +1988,7 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
   if (w.kind == FILL_FLAG && w.flag) {
     const uint64_t t0 = mono_ns();
     uint32_t spins = 0;
-    // the pack's read signal (its workgroup 0 saw every workgroup's loads return), or the fill
-    while (!(w.read && w.read->load(std::memory_order_acquire) >= w.epoch) &&
-           !fill_reached(w.flag, w.epoch)) {
+    while (!fill_reached(w.flag, w.epoch)) {
       if (++spins < 4096) {
         __builtin_ia32_pause();
         continue;
@@ -2169,15 +2028,15 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     t2 = t3 = mono_ns();
   } else if (plan->size) {
     // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
-    // every `timing_sample()`-th pack is stamped (DORA_GPU_TIMING_SAMPLE, default 8).
-    const uint64_t period = n->timing_period ? n->timing_period : timing_sample();
+    // every n-th pack is stamped (dora_node_set_timing_period, default kTimingPeriod).
+    const uint64_t period = n->timing_period ? n->timing_period : kTimingPeriod;
     const bool timed = n->profile && plan->dev != ARROW_DEVICE_CPU &&
                        (n->timing_seq++ % period) == 0;
     TimingPair* tp = timed ? next_timing_pair(n, plan->size) : nullptr;
     hipEvent_t t_start = tp ? tp->start : nullptr, t_stop = tp ? tp->stop : nullptr;
     // Timed region: packs that signal their own fill stamp their device time into the flag
     // line; only packs that cannot (kernel signal off, transforms) need timing events
-    const bool stampable = kernel_signal() && n->core->fill_done && !plan->compact;
+    const bool stampable = n->core->fill_done && !plan->compact;
     if (n->region_armed && plan->dev != ARROW_DEVICE_CPU) {
       if (!stampable && !n->region_started && !tp) {  // its start is the fallback's origin
         t_start = n->region_start;
@@ -2220,8 +2079,6 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     wait.kind = n->bcast_out.count(output_id) ? uint8_t(FILL_BCAST) : s->fill;
     wait.epoch = s->epoch;
     if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
-    if (s->fill == FILL_FLAG && s->read_signal)
-      wait.read = &reinterpret_cast<const FillFlag*>(wait.flag)->read_epoch;
     if (s->fill == FILL_EVENT) wait.event = s->slot->done;
   }
   rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
@@ -2309,15 +2166,8 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     DORA_HIP(hipStreamCreateWithFlags(&core->stream, hipStreamNonBlocking));
     // Fill streams are created on first use: device-source packs go to the AQL queues, so only
     // host sources, compacting transforms and node-stream-ordered fills need them, and a node
-    // that never sends such a pack holds one HIP hardware queue, not four.  With
-    // DORA_GPU_AQL=0 or a size cap (DORA_GPU_AQL_MAX_BYTES) a node with outputs creates them
-    // up front: HIP maps streams onto its 4 hardware queues in creation order, and fill streams
-    // created late share one (40.96 MB: 13.2 -> 15.0-15.2 us device time per pack, r01).
-    const char* aql_env = std::getenv("DORA_GPU_AQL");
-    const bool aql_off = aql_env && *aql_env == '0';
-    if (e.outputs[0] != 0 && (aql_off || dora::aql_max_bytes() != ~uint64_t(0)))
-      core->ensure_fill_streams();
-    if (dora::async_sends()) {
+    // that never sends such a pack holds one HIP hardware queue, not four.
+    {
       // host-register the control region so this node's stream can write fill epochs into it
       void* dev = nullptr;
       if (hipHostRegister(core->region->base(), core->region->size(), hipHostRegisterMapped) ==
@@ -2350,9 +2200,6 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
   }
   n->min_queue_size = SIZE_MAX;
   for (auto& kv : n->queue_size) n->min_queue_size = std::min<size_t>(n->min_queue_size, kv.second);
-  const char* prof = std::getenv("DORA_GPU_PROFILE_PACK");
-  if (prof && *prof && *prof != '0' && device >= 0)
-    n->profile = dora::ensure_timing(n) == DORA_OK;
   // Subscribe and wait for AllNodesReady (event_stream/mod.rs:37-118, daemon PendingNodes)
   int rc = core->request(dora::REQ_SUBSCRIBE, {});
   if (rc != DORA_OK) {
@@ -2553,7 +2400,7 @@ int dora_node_send_output_ex(dora_node* n, const char* output_id, const struct A
   int rc = (n->compact && device_type == ARROW_DEVICE_ROCM)
                ? dora::build_plan_compact(array, schema, device_type, &plan)
                : dora::build_plan(array, schema, device_type, &plan,
-                                  device && dora::validity_in_sample());
+                                  device);
   if (rc != DORA_OK) return rc;
   if (keyed && !plan->read_device) {
     // keep it: a later send of the same buffers reuses plan and type info.  64 entries cover a
@@ -2888,9 +2735,15 @@ int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_
       if (na && n->region_reduce_idx) {
         std::copy(n->region_cp_used.begin(), n->region_cp_used.begin() + na, n->region_reduce_idx);
         std::fill(n->region_reduce_out, n->region_reduce_out + 2 * na, uint64_t(0));
-        reduced = dora::aql_stamp_reduce(n->core->device, n->region_cp_stamps,
-                                         uint32_t(dora::kCpAreaWords), n->region_reduce_idx, na,
-                                         n->region_reduce_out) == DORA_OK;
+        const int rrc = dora::aql_stamp_reduce(n->core->device, n->region_cp_stamps,
+                                               uint32_t(dora::kCpAreaWords), n->region_reduce_idx,
+                                               na, n->region_reduce_out);
+        reduced = rrc == DORA_OK;
+        if (rrc == DORA_ERR_TIMEOUT) {
+          // the reduction may still run and write them: leak both (later regions read the BAR)
+          n->region_reduce_idx = nullptr;
+          n->region_reduce_out = nullptr;
+        }
         if (!reduced) dora::clear_error();
       }
       std::vector<uint64_t> w(1 + dora::kCpStampWgs);

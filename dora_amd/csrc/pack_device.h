@@ -38,17 +38,13 @@ constexpr uint32_t kSignalGrid = 1024;
 // (profiles/r02_c3_edges_ab.jsonl, the same cloud with every buffer at 0 mod 64).
 constexpr uint64_t kLine = 128;
 
-// Bit 31 of PackArgsT::nseg: chunks start at the first aligned unit instead (the r01 layout;
-// DORA_GPU_LINE_CHUNKS=0, an A/B knob).
-constexpr uint32_t kUnitChunks = 1u << 31;
-
 // Chunks of one segment [d0, d0 + len) of a destination at `base` (host and device agree).
 __host__ __device__ inline uint64_t segment_chunks(uint64_t base, uint64_t d0, uint64_t len,
-                                                   uint64_t chunk_bytes, bool line = true) {
+                                                   uint64_t chunk_bytes) {
   const uint64_t A0 = (base + d0 + 15) & ~uint64_t(15);
   const uint64_t A1 = (base + d0 + len) & ~uint64_t(15);
   if (A1 <= A0) return 1;
-  const uint64_t O = line ? A0 & ~(kLine - 1) : A0;
+  const uint64_t O = A0 & ~(kLine - 1);
   return (A1 - O + chunk_bytes - 1) / chunk_bytes;
 }
 
@@ -116,10 +112,6 @@ typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // which never return a line another XCD's writer has since replaced, so the dispatch needs no
 // acquire fence (its L2 invalidation) to see a source rewritten since an earlier pack read it.
 constexpr int kCoherent = 4;
-// 5: as 2, but the source is read with PLAIN loads (L1-cached).  Test kernel only: the acquire
-// fence's negative control (tests/test_gpu_fence.py) — every shipped kernel reads sources with
-// nt or sc1 loads, which bypass the CU's L1 (MI355X_MICROARCH.md § visibility).
-constexpr int kPlainSrc = 5;
 // raw buffer loads: cache policy bits sc1 (16) | nt (2); resource word 3 as for gfx9 raw buffers
 constexpr int kCoherentPolicy = 16 | 2;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const uint8_t* p) {
@@ -137,7 +129,7 @@ __device__ __forceinline__ uint8_t ld1(const uint8_t* p) {
 
 template <int NT, bool DW = false>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-  constexpr bool nt = NT != 0 && NT != kPlainSrc;
+  constexpr bool nt = NT != 0;
   if constexpr (DW) {  // p only 4-byte aligned
     if constexpr (nt) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(p));
     return *reinterpret_cast<const u32x4_a4*>(p);
@@ -147,7 +139,7 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
 }
 template <int NT>
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT == 2 || NT == kCoherent || NT == kPlainSrc) {
+  if constexpr (NT == 2 || NT == kCoherent) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
   } else if constexpr (NT == 3) {
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
@@ -240,7 +232,7 @@ __device__ __forceinline__ void copy_shifted(uint8_t* dp, const uint8_t* sbase, 
 // the byte the destination already has (padding stays as it was, arrow_utils.rs:48).
 template <int NT, class A>
 __device__ __forceinline__ uint8_t unit_byte(const A& a, uint64_t o) {
-  for (uint32_t k = 0; k < (a.nseg & ~kUnitChunks); ++k) {
+  for (uint32_t k = 0; k < a.nseg; ++k) {
     const PackSeg g = a.seg[k];
     if (o - g.dst_off < g.len) return ld1<NT>(g.src + (o - g.dst_off));  // o in [dst_off, +len)
   }
@@ -249,7 +241,7 @@ __device__ __forceinline__ uint8_t unit_byte(const A& a, uint64_t o) {
 
 template <int U, int NT, class A>
 __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
-  const uint32_t nseg = args.nseg & ~kUnitChunks;
+  const uint32_t nseg = args.nseg;
   uint32_t s = 0;
   while (s + 1 < nseg && chunk >= args.chunk_end[s]) ++s;  // uniform, <= 32 steps
   const PackSeg sg = args.seg[s];
@@ -309,7 +301,7 @@ __device__ __forceinline__ void pack_chunk(const A& args, uint32_t chunk) {
   // aligned unit (kLine; segment_chunks counts them the same way).  Absolute addresses: O may
   // lie before the destination's base.
   const uint64_t E0 = base + a0, E1 = base + a1;  // the body, absolute (A0, A1 when non-empty)
-  const uint64_t O = (args.nseg & kUnitChunks) ? E0 : E0 & ~(kLine - 1);
+  const uint64_t O = E0 & ~(kLine - 1);
   const uint64_t B0 = O + uint64_t(c) * args.chunk_bytes;
   if (B0 >= E1) return;
   const uint64_t B1 = (E1 - B0) > args.chunk_bytes ? B0 + args.chunk_bytes : E1;
@@ -458,55 +450,6 @@ __device__ __forceinline__ void signal_batch(const AqlBatchArgs& a, uint32_t blk
   }
 }
 
-// Read signal of a synchronous send (aql.cpp read_signal; `flag` tagged with bit 0): the
-// command processor's completion signal reports the fill to receivers, and workgroup 0 tells
-// the sender as soon as every workgroup's stores — so every load of the source — are complete:
-// it polls the workgroups' done words (as signal_fill does) and stores the epoch into the flag
-// line's read_epoch (word 4, system scope), then stamps the fill's start and end (words 1, 2).
-// The sender returns on it without waiting for the end of the dispatch, the command
-// processor's end-of-pipe event and its signal write (the reference's send_output returns once
-// its copy has read the caller's buffer, arrow_utils.rs:48).  (A "loads returned" word
-// published before the store wait did not compile into one: the wait-count pass puts a
-// vmcnt(0) — every store of the wave complete — in front of any store after the copy loop.)
-template <class A>
-__device__ __forceinline__ void signal_read(const A& a, uint32_t blk, uint32_t nblk,
-                                            uint64_t t_start) {
-  uint64_t* const flag =
-      reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(a.flag) & ~uintptr_t(1));
-  const uint32_t e = static_cast<uint32_t>(a.epoch);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are complete
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(a.done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blk != 0) return;
-  constexpr int kPer = kMaxSignalWgs / kThreads;
-  __shared__ uint32_t missing;
-  for (uint32_t round = 0; round < (1u << 22); ++round) {
-    if (threadIdx.x == 0) missing = 0;
-    __syncthreads();
-    bool mine = true;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = threadIdx.x + k * kThreads;
-      if (i < nblk)
-        mine &= __hip_atomic_load(a.done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e;
-    }
-    if (!mine) missing = 1;
-    __syncthreads();
-    const bool all = missing == 0;
-    __syncthreads();
-    if (all) {
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(flag + 4, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        stamp_fill(flag, t_start);
-      }
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  // a lost workgroup: no read signal; the command processor's signal still reports the fill
-}
-
 // A pack launch: its workgroups stride over the chunks; a signalling launch (NT >= 2) then
 // signals the fill flag.
 template <int U, int NT, class A>
@@ -521,12 +464,11 @@ __device__ __forceinline__ void pack_body(const A& args, uint32_t blk, uint32_t 
       if constexpr (__is_same(A, AqlBatchArgs)) {
         signal_batch(args, blk, nblk, t_start);
       } else {
-        if (reinterpret_cast<uintptr_t>(args.flag) & 1) signal_read(args, blk, nblk, t_start);
-        else signal_fill(args, blk, nblk, t_start);
+        signal_fill(args, blk, nblk, t_start);
       }
     } else if (args.done) {
       // done words but no flag: the dispatch's completion signal reports the fill (the command
-      // processor's, aql.cpp cp_signal_window); every wave's stores are complete before it ends
+      // processor's, aql.cpp aql_cp_candidate); every wave's stores are complete before it ends
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (args.epoch) {
         // a pack inside a timed region: `epoch` is its stamp area (device memory, zeroed by the

@@ -1,8 +1,6 @@
 // Runtime plumbing of the C ABI: errors, devices, streams, events, memory.
 #include <hip/hip_runtime_api.h>
 
-#include <execinfo.h>
-#include <signal.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -41,37 +39,6 @@ int fail(int code, const char* fmt, ...) {
 
 void clear_error() { std::strcpy(g_last_error, "no error"); }
 
-namespace {
-
-struct sigaction g_prev_segv;
-
-void on_segv(int sig, siginfo_t* info, void* ctx) {
-  void* frames[64];
-  const int n = backtrace(frames, 64);
-  char head[128];
-  const int k = std::snprintf(head, sizeof(head), "dora-gpu: signal %d at address %p, backtrace:\n",
-                              sig, info ? info->si_addr : nullptr);
-  if (k > 0) (void)!write(2, head, size_t(k));
-  backtrace_symbols_fd(frames, n, 2);
-  sigaction(SIGSEGV, &g_prev_segv, nullptr);  // then whatever handled it before (faulthandler)
-  raise(sig);
-}
-
-// DORA_GPU_SEGV_TRACE=1: print a native backtrace on SIGSEGV (debugging aid on the GPU box,
-// where no debugger may attach).
-struct SegvTrace {
-  SegvTrace() {
-    const char* e = std::getenv("DORA_GPU_SEGV_TRACE");
-    if (!e || *e != '1') return;
-    struct sigaction sa;
-    std::memset(&sa, 0, sizeof(sa));
-    sa.sa_sigaction = on_segv;
-    sa.sa_flags = SA_SIGINFO;
-    sigaction(SIGSEGV, &sa, &g_prev_segv);
-  }
-} g_segv_trace;
-
-}  // namespace
 
 }  // namespace dora
 
@@ -94,19 +61,6 @@ int dora_gpu_aql_dispatch_counts(int device, uint64_t* counts, size_t cap, size_
   return DORA_OK;
 }
 
-int dora_gpu_test_fill_reached(const void* flag, uint64_t epoch) {
-  if (!flag || (reinterpret_cast<uintptr_t>(flag) & 63))
-    return dora::fail(DORA_ERR_INVALID, "fill flag must be 64-byte aligned");
-  return dora::fill_reached(static_cast<const std::atomic<uint64_t>*>(flag), epoch) ? 1 : 0;
-}
-
-int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
-  if (!flag || (reinterpret_cast<uintptr_t>(flag) & 63) || epoch == 0)
-    return dora::fail(DORA_ERR_INVALID, "fill flag must be 64-byte aligned, epoch > 0");
-  dora::cp_arm(static_cast<dora::FillFlag*>(flag), epoch);
-  return DORA_OK;
-}
-
 int dora_gpu_aql_cp_signalled(int device, uint64_t* count) {
   if (!count) return dora::fail(DORA_ERR_INVALID, "NULL count");
   *count = dora::aql_cp_signalled(device);
@@ -122,52 +76,6 @@ int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_ms
   if (backlogged) *backlogged = c;
   return DORA_OK;
 }
-
-int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
-
-int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank) {
-  if (!buf || !nranks || !rank) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  DORA_GUARD_BEGIN
-  DORA_HIP(hipSetDevice(device));
-  uint8_t uid[dora::kBcastIdBytes];
-  int rc = dora::bcast_unique_id(uid);
-  if (rc != DORA_OK) return rc;
-  dora::BcastComm* c = nullptr;
-  rc = dora::bcast_join(uid, 1, 0, 30000, &c);
-  if (rc != DORA_OK) return rc;
-  *nranks = dora::bcast_nranks(c);
-  *rank = dora::bcast_rank(c);
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-    dora::bcast_close(c, nullptr, 0);
-    return dora::fail(DORA_ERR_HIP, "hipStreamCreate");
-  }
-  rc = dora::bcast_enqueue(c, buf, bytes, st);
-  if (rc == DORA_OK && hipStreamSynchronize(st) != hipSuccess)
-    rc = dora::fail(DORA_ERR_HIP, "broadcast stream: %s", hipGetErrorString(hipGetLastError()));
-  dora::bcast_close(c, st, 10000);
-  (void)hipStreamDestroy(st);
-  return rc;
-  DORA_GUARD_END
-}
-
-int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
-                               double* us_per_msg) {
-  if (!us_per_msg) return dora::fail(DORA_ERR_INVALID, "us_per_msg is NULL");
-  return dora::aql_pipeline_bench(device, bytes, n, mode, queues, depth, us_per_msg);
-}
-
-int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out) {
-  if (!out) return dora::fail(DORA_ERR_INVALID, "out is NULL");
-  return dora::bar_alloc(device, bytes, out);
-}
-
-int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes) {
-  if ((!dst || !src) && bytes) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  return dora::bar_write(device, dst, src, bytes);
-}
-
-void dora_gpu_test_bar_free(void* ptr) { dora::bar_free(ptr); }
 
 const char* dora_gpu_aql_kernel_name(size_t k) {
   const char* s = dora::aql_kernel_name(k);

@@ -74,12 +74,12 @@ void parse_cpulist(const char* path, cpu_set_t* out) {
   }
 }
 
-// DORA_GPU_PIN_L3: 0 = NUMA node only; "fixed" = the domain by GPU ordinal (r03); default = the
-// least busy domain.
+// DORA_GPU_PIN (node.cpp numa_pinning: 0 = off): "numa" = NUMA node only; "fixed" = the L3
+// domain by GPU ordinal (r03); default = the least busy L3 domain.
 int l3_placement_mode() {
   static const int v = [] {
-    const char* e = std::getenv("DORA_GPU_PIN_L3");
-    if (e && *e == '0') return 0;
+    const char* e = std::getenv("DORA_GPU_PIN");
+    if (e && std::strcmp(e, "numa") == 0) return 0;
     if (e && std::strcmp(e, "fixed") == 0) return 1;
     return 2;
   }();
@@ -181,21 +181,9 @@ bool pin_to_numa(int numa, int device, std::atomic<int32_t>* l3_cpu, int procs) 
   return sched_setaffinity(0, sizeof(both), &both) == 0;
 }
 
-int64_t spin_budget_us() {
-  static int64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_SPIN_US");
-    return e ? std::atoll(e) : int64_t(200);
-  }();
-  return v;
-}
+int64_t spin_budget_us() { return 200; }
 
-int64_t spin_max_us() {
-  static int64_t v = [] {
-    const char* e = std::getenv("DORA_GPU_SPIN_MAX_US");
-    return e ? std::atoll(e) : int64_t(5000);
-  }();
-  return v;
-}
+int64_t spin_max_us() { return 5000; }
 
 int64_t AdaptiveSpin::budget_us() const {
   const int64_t base = spin_budget_us(), cap = spin_max_us();

@@ -66,10 +66,7 @@ struct FillFlag {
   alignas(64) std::atomic<uint64_t> epoch;
   uint64_t t_start, t_end;
   std::atomic<uint64_t> cp_epoch;  // epoch of the CP-signalled fill `cp` reports
-  // a synchronous send's pack has READ its whole source (aql.cpp read_signal): the epoch, stored
-  // by the pack's workgroup 0 before the fill completes; the sender may return on it
-  std::atomic<uint64_t> read_epoch;
-  uint64_t pad_[3];
+  uint64_t pad_[4];
   CpSignal cp;
 };
 static_assert(offsetof(FillFlag, cp) == 64 && sizeof(FillFlag) == 128, "FillFlag layout");
@@ -185,7 +182,7 @@ class RingWriter {
 // are short: budget = max(base, 2 x a fast-down / slow-up mean of the idle gaps that ended with
 // data) while that is within the cap, else the base.  A stream slower than the cap allows (e.g. 30 Hz
 // cameras) costs no more CPU than before; streams at >= ~400 Hz keep their waiters on-CPU.
-// DORA_GPU_SPIN_US = the base (200), DORA_GPU_SPIN_MAX_US = the cap (5000; 0: fixed base).
+// The base is 200 us, the cap 5 ms.
 class AdaptiveSpin {
  public:
   int64_t budget_us() const;
@@ -227,15 +224,15 @@ bool read_shmem(const std::string& name, uint64_t len, std::vector<uint8_t>* out
 // futex helpers on shared (non-private) words
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us);
 void futex_wake(std::atomic<uint32_t>* w);
-int64_t spin_budget_us();      // the base budget (DORA_GPU_SPIN_US)
-int64_t spin_max_us();         // the adaptive cap (DORA_GPU_SPIN_MAX_US)
+int64_t spin_budget_us();      // the base budget (200 us)
+int64_t spin_max_us();         // the adaptive cap (5 ms)
 uint64_t now_ns();          // CLOCK_REALTIME (timestamps that cross processes)
 uint64_t mono_ns();          // CLOCK_MONOTONIC
 // Restrict the calling thread (and threads it starts later) to the CPUs of NUMA node `numa`
 // within its current affinity; false when that would leave none or changes nothing.
 // Move the calling thread onto NUMA node `numa`'s CPUs (within its current affinity) and, when
 // `l3_cpu` is given and the node's L3 domains have room for `procs` processes, onto the one L3
-// domain the dataflow shares (DORA_GPU_PIN_L3=0: NUMA node only).
+// domain the dataflow shares (DORA_GPU_PIN=numa: NUMA node only).
 bool pin_to_numa(int numa, int device = -1, std::atomic<int32_t>* l3_cpu = nullptr,
                  int procs = 0);
 

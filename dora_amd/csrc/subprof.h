@@ -1,4 +1,5 @@
-// Host sub-phase profile of the per-message path (diagnostics only): DORA_GPU_SUBPHASES=1 makes
+// Host sub-phase profile of the per-message path (diagnostics only): DORA_GPU_TRACE (a trace
+// directory, or "subphases") makes
 // every process accumulate TSC ticks per named span of send / route / receive and print one JSON
 // line {"subphases": {name: [ns per call, calls]}} to stderr at exit.  Off by default: one
 // predictable branch per span.
@@ -36,7 +37,7 @@ enum SubPhase : int {
   SP_COUNT
 };
 
-extern const bool g_subprof_on;  // DORA_GPU_SUBPHASES, read at load time
+extern const bool g_subprof_on;  // DORA_GPU_TRACE set, read at load time
 inline bool subprof_enabled() { return g_subprof_on; }
 void subprof_add(int phase, uint64_t ticks);
 

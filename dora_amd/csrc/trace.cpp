@@ -5,6 +5,8 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <mutex>
 #include <vector>
 
@@ -20,8 +22,16 @@ struct Rec {
   uint8_t p;
 };
 
+// DORA_GPU_TRACE=<dir>: per-message trace files in <dir> (and the sub-phase profile below);
+// "subphases": the sub-phase profile alone
+const char* trace_dir() {
+  const char* e = std::getenv("DORA_GPU_TRACE");
+  if (!e || !*e || std::strcmp(e, "0") == 0 || std::strcmp(e, "subphases") == 0) return nullptr;
+  return e;
+}
+
 struct Tracer {
-  const char* dir = std::getenv("DORA_GPU_TRACE");
+  const char* dir = trace_dir();
   std::vector<Rec> buf;
   std::atomic<size_t> n{0};
   std::string who = "proc";
@@ -114,9 +124,10 @@ SubProf& subprof() {
 
 }  // namespace
 
+// DORA_GPU_TRACE set (a directory, or "subphases" for the sub-phase profile alone)
 const bool g_subprof_on = [] {
-  const char* e = std::getenv("DORA_GPU_SUBPHASES");
-  return e && *e && *e != '0';
+  const char* e = std::getenv("DORA_GPU_TRACE");
+  return e && *e && std::strcmp(e, "0") != 0;
 }();
 
 void subprof_add(int phase, uint64_t ticks) {

@@ -110,7 +110,7 @@ def aql_dispatch_counts(device: int = 0) -> dict:
 
 
 def aql_cp_signalled(device: int = 0) -> int:
-    """Packs whose fill the command processor signalled (DORA_GPU_AQL_CP_SIGNAL window)."""
+    """Packs whose fill the command processor signalled (aql.cpp aql_cp_candidate)."""
     a = c_uint64()
     call("dora_gpu_aql_cp_signalled", device, byref(a))
     return a.value

@@ -102,7 +102,7 @@ int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_ms
                              uint64_t* backlogged);
 /* Diagnostics: packs on HIP device `device` whose fill the command processor signalled (the
  * packet's completion signal instead of the in-kernel flag store; mid-size single-segment packs
- * sent alone, DORA_GPU_AQL_CP_SIGNAL). */
+ * of 1-32 MiB, and synchronous single-segment sends from 1 MiB). */
 int dora_gpu_aql_cp_signalled(int device, uint64_t* count);
 
 int dora_gpu_device_count(int* count);
@@ -181,16 +181,6 @@ int dora_gpu_plan_type_info(const dora_plan* plan, uint8_t* buf, size_t cap, siz
  * `dst` (device memory, `dst_len` >= plan size) on `stream`; async.  Padding is not written.
  */
 int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_t stream);
-/* Tuning knob of the pack kernel (process-wide): 16-B loads in flight per lane (0 = default,
- * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1; 2 = the signalling kernels'
- * write-through stores without a signal, a microbenchmark variant), bytes per workgroup (0 =
- * auto, else a multiple of 128: chunks start on cache lines). */
-int dora_gpu_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
-/* Tuning of packs that signal their fill from the kernel (node sends): workgroups of such a
- * launch, which then strides over the chunks (0: up to 4096).  With `bench_signal`,
- * dora_gpu_pack signals a scratch flag too (microbenchmarks). */
-int dora_gpu_pack_signal_tune(uint32_t grid, int bench_signal);
-
 /* ------------------------------------------------------------------------------------------ */
 /* Device-resident Arrow arrays                                                               */
 /* ------------------------------------------------------------------------------------------ */
@@ -226,70 +216,6 @@ int dora_gpu_csum64(const void* data, size_t len, uint64_t* out_dev, dora_stream
 int dora_gpu_csum64_sync(const void* data, size_t len, dora_stream_t stream, uint64_t* out);
 /* Fill `len` device bytes with the splitmix64 stream of `seed` (BASELINE.md §2 payloads). */
 int dora_gpu_fill_splitmix(void* dst, size_t len, uint64_t seed, dora_stream_t stream);
-/* Test tool (no reference counterpart): one workgroup per CU reads all of [data, data + len)
- * with plain cached loads, leaving the lines in every XCD's L2 (the acquire-fence negative
- * control of tests/test_gpu_fence.py). */
-int dora_gpu_l2_touch(const void* data, size_t len, dora_stream_t stream);
-/* Test tools (no reference counterpart): device memory of `device`'s coarse-grained pool that
- * the host writes directly through the PCIe BAR (stores + HDP flush + read-back), behind every
- * XCD's L2 — the source rewrite of the acquire-fence negative control. */
-int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
-/* Test tool: while `hold` is set, every batchable AQL send of this process on `device` waits in
- * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
- * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
-int dora_gpu_test_aql_hold(int device, int hold);
-/* Test tool (host only): the 640-byte argument block of a batch pack (dora_aql_packb_u4) for
- * `n_msgs` (<= 8) messages; message m has seg_counts[m] segments, given as (src, dst_off, len)
- * triples in `segs`, its slot at dsts[m] with dst_caps[m] writable bytes, and fill flag /
- * epoch flags[m] / epochs[m].  *grid = the workgroups the dispatch would launch. */
-int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
-                             const uint64_t* dsts, const uint64_t* dst_caps,
-                             const uint64_t* flags, const uint64_t* epochs, uint8_t* out,
-                             size_t cap, uint32_t* grid);
-int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes);
-/* Test tools (host only) of the fill-flag protocol (FillFlag, 128 bytes, 64-byte aligned): the
- * completion test of epoch `epoch` (1: complete) and the sender's set-up of a fill the command
- * processor signals. */
-int dora_gpu_test_fill_reached(const void* flag, uint64_t epoch);
-int dora_gpu_test_cp_arm(void* flag, uint64_t epoch);
-/* Test hook (microbenchmark): `n` single-segment AQL packs of `bytes` from rotating HBM sources,
- * round robin over `queues` of the device's AQL queues with at most `depth` outstanding per
- * queue; mode 0 completes them with the in-kernel fill signal, 1 with the packet's completion
- * signal (release fence none), 2 the same with an agent release fence, 3 and 4 as 0 and 1 without
- * the acquire fence, 5 as 1 with every wave waiting for its stores.  *us_per_msg = host time
- * per pack. */
-int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
-                               double* us_per_msg);
-void dora_gpu_test_bar_free(void* ptr);
-/* Test hook (RCCL path of the fan-out): form a broadcast group of one rank on
- * `device` (unique id -> join(nranks 1) -> ncclBroadcast of `bytes` at `buf` in place on a fresh
- * stream -> close), reporting the rank count and rank the communicator holds.  The one-GPU
- * exercise of bcast_unique_id / bcast_join / bcast_enqueue / bcast_close. */
-int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank);
-/* Test tool (the fence probe's failing control): one 64-lane workgroup per CU reads 64 words of
- * BAR-written device memory, the host rewrites them through the BAR, and the same waves read
- * them again within the same dispatch; `mode` 0 plain (L1-cached) loads, 1 non-temporal, 2
- * agent-coherent (sc1).  Workgroups whose first read was wrong, whose second read was stale,
- * and the workgroups launched. */
-int dora_gpu_test_l1_stale(int device, int mode, uint32_t* bad_first, uint32_t* stale,
-                           uint32_t* blocks);
-/* Test hooks of the inter-daemon wire, bincode of Timestamped<InterDaemonEvent> (replaces
- * bincode::serialize in binaries/daemon/src/inter_daemon.rs:66 and its deserialize at :156;
- * layouts in csrc/bincode.h): an Output event built from this library's type-info and parameter
- * encodings, an InputsClosed event of `n` (receiver, input) pairs, and a frame decoded into
- * JSON.  `hlc_id`: 16 bytes.  A buffer too small fails with *len set to the size needed. */
-int dora_gpu_test_ide_output(const char* dataflow_id, const char* node_id, const char* output_id,
-                             const uint8_t* type_info, size_t type_info_len, const uint8_t* params,
-                             size_t params_len, uint64_t meta_ns, uint64_t event_ns,
-                             const uint8_t* hlc_id, const uint8_t* data, size_t data_len,
-                             int has_data, uint8_t* out, size_t cap, size_t* out_len);
-int dora_gpu_test_ide_inputs_closed(const char* dataflow_id, const char* const* receivers,
-                                    const char* const* inputs, size_t n, uint64_t event_ns,
-                                    const uint8_t* hlc_id, uint8_t* out, size_t cap,
-                                    size_t* out_len);
-int dora_gpu_test_ide_decode(const uint8_t* frame, size_t len, char* json, size_t cap,
-                             size_t* json_len);
-
 /* ------------------------------------------------------------------------------------------ */
 /* Node API — replaces DoraNode / EventStream (apis/rust/node/src/node/mod.rs:42-503,         */
 /* apis/rust/node/src/event_stream/mod.rs:27-235) and the C node API (apis/c/node/node_api.h) */
@@ -315,13 +241,16 @@ int dora_node_init_from_env(dora_node** out);
 void dora_node_free(dora_node* node);
 /* The node's HIP stream; consumers must run their kernels on it so the drop token is only
  * returned after they have read the sample.  Sends spread their fills over the node's fill
- * streams (DORA_GPU_FILL_STREAMS, default 3): a fill runs after the work queued on this stream
+ * streams (three): a fill runs after the work queued on this stream
  * when the send is made, and the call orders every fill launched so far before the work the
  * caller queues on the returned stream next (a device source may be rewritten there). */
 dora_stream_t dora_node_stream(dora_node* node);
 
 /* allocate_data_sample (mod.rs:303-346): a device slot of `len` bytes (best-fit from the
- * 20-entry cache of recycled slots, else a new exported hipMalloc slot); len 0 -> empty Vec. */
+ * node's cache of recycled slots, else a new exported hipMalloc slot); len 0 -> empty Vec.  A
+ * host-only node (device < 0) gets the reference's samples instead: an inline Vec below 4096 B,
+ * else a POSIX shared-memory region (DataMessage::SharedMemory, mod.rs:321-346) it writes with
+ * the CPU; dora_sample_data is then a host pointer. */
 int dora_node_allocate_data_sample(dora_node* node, size_t len, dora_sample** out);
 void* dora_sample_data(dora_sample* sample); /* device pointer (slot) */
 size_t dora_sample_len(const dora_sample* sample);
@@ -334,7 +263,9 @@ int dora_node_send_output_sample(dora_node* node, const char* output_id, const u
                                  size_t type_info_len, const uint8_t* params, size_t params_len,
                                  dora_sample* sample);
 /* send_output (mod.rs:198-215): plan + allocate + HIP pack + send.  `device_type` as in
- * dora_gpu_plan.  Like the reference, which copies the array inside the call
+ * dora_gpu_plan; a host-resident array whose sample is < 4096 B travels inline as the
+ * reference's DataMessage::Vec (mod.rs:40,303-319: no slot, no GPU work).  Like the reference,
+ * which copies the array inside the call
  * (arrow_utils.rs:48), the call returns once the sample no longer needs the source: for a
  * device source it waits (after the descriptor has left) until the pack kernel has read it, so
  * the caller may rewrite or free the source on any stream right away. */
@@ -375,9 +306,11 @@ int dora_node_next_event(dora_node* node, int64_t timeout_us, dora_event** out);
 int dora_event_type(const dora_event* ev);
 const char* dora_event_id(const dora_event* ev);
 const char* dora_event_error(const dora_event* ev);
-/* Raw sample of an input: device pointer (mapped IPC slot) or host pointer for Vec data.  An
- * input whose slot lives on another GPU is pulled into local HBM on the first call (complete on
- * return; see dora_node_peer_stats). */
+/* Raw sample of an input: device pointer (mapped IPC slot) or host pointer for inline Vec data
+ * and for a host-only receiver's shared-memory samples (dora_event_is_device says which).  An
+ * input whose slot lives on another GPU, or a host-only producer's shared-memory sample at a
+ * device receiver, is pulled into local HBM on the first call (complete on return; the
+ * producer's token goes back at once; see dora_node_peer_stats). */
 int dora_event_data(const dora_event* ev, const void** ptr, size_t* len);
 int dora_event_is_device(const dora_event* ev);
 /* Serialized ArrowTypeInfo / MetadataParameters / timestamp of the input's Metadata. */
@@ -385,8 +318,9 @@ int dora_event_type_info(const dora_event* ev, const uint8_t** type_info, size_t
 int dora_event_parameters(const dora_event* ev, const uint8_t** params, size_t* len);
 uint64_t dora_event_timestamp_ns(const dora_event* ev);
 /* RawData::into_arrow_array (event.rs:35-91): zero-copy device ArrowArray over the sample; it
- * keeps the input (and its drop token) alive until released.  An inline Vec sample (host-only
- * node, < 4096 B) imports as a host ArrowArray over its bytes instead. */
+ * keeps the input (and its drop token) alive until released.  An inline Vec sample (< 4096 B
+ * from a host source) and a host-only receiver's shared-memory sample import as a host
+ * ArrowArray over their bytes instead. */
 int dora_event_array(const dora_event* ev, struct ArrowArray* out_array,
                      struct ArrowSchema* out_schema);
 /* Drop the event; the drop token is reported once no array references the data any more. */
@@ -400,7 +334,7 @@ int dora_node_forward(dora_node* node, const char* output_id, const dora_event* 
 /* A same-GPU device input is forwarded in place: the new message points at the producer's slot
  * under a token of this node, and the input (with the producer's token) is held until that token
  * returns — no copy, no new slot.  Cross-GPU inputs, broadcast-group inputs and
- * DORA_GPU_FORWARD_COPY=1 copy into a fresh slot instead.  Forwards done in place, and forwards
+ * copy into a fresh slot instead.  Forwards done in place, and forwards
  * whose token has not returned yet. */
 int dora_node_forward_stats(dora_node* node, uint64_t* in_place, uint64_t* held);
 
@@ -414,7 +348,7 @@ int dora_node_stats(dora_node* node, uint64_t* slots_created, uint64_t* cache_hi
 int dora_node_dataflow_counters(dora_node* node, const char* node_id, uint64_t* slots_created,
                                 uint64_t* ipc_opens, uint64_t* dropped_inputs);
 /* Fills (packs of sends) by dispatch path: raw AQL packets on the process's HSA queue (device
- * sources below DORA_GPU_AQL_MAX_BYTES, default 32 MiB, <= 8 segments) or hipLaunchKernel on
+ * sources of <= 8 segments) or hipLaunchKernel on
  * the node's fill streams (larger, host sources, compacting transforms, relays). */
 int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_packs);
 /* dora_node_send_output of device arrays keeps the plans of recent sends that read no array
@@ -445,7 +379,7 @@ int dora_node_bcast_stats(dora_node* node, uint64_t* groups_out, uint64_t* group
  * (producer included; 0 without a group). */
 int dora_node_bcast_ranks(dora_node* node, uint64_t* max_ranks);
 /* Pack-kernel timing: hipExtLaunchKernel start/stop stamps of every n-th pack launch
- * (dora_node_set_timing_period; 0 = DORA_GPU_TIMING_SAMPLE, default 8). */
+ * (dora_node_set_timing_period; 0 = the default, 8). */
 int dora_node_set_profiling(dora_node* node, int enable);
 int dora_node_set_timing_period(dora_node* node, uint64_t period);
 int dora_node_pack_stats(dora_node* node, uint64_t* count, double* total_ms, uint64_t* bytes);

@@ -48,7 +48,7 @@ def edge_mask(segs, dst, cap):
 
 def build(msgs):
     """msgs: [(dst, cap, flag, epoch, [(src, dst_off, len), ...])] -> (args bytes, grid)."""
-    lib = _lib.load()
+    lib = _lib.load_testing()
     n = len(msgs)
     counts = (ctypes.c_size_t * n)(*[len(m[4]) for m in msgs])
     flat = [x for m in msgs for s in m[4] for x in s]
@@ -120,15 +120,15 @@ def test_batch_args_sorted_segments_chunks_edges_and_flags():
 
 
 def test_batch_args_refuses_mixed_chunks_and_too_many_segments():
-    lib = _lib.load()
+    lib = _lib.load_testing()
     small = (0x7F0000000000, MiB2, 0x1000, 1, [(0x10000000, 0, 4096)])
     big = (0x7F0002000000, 1 << 25, 0x1040, 2, [(0x20000000, 0, 30 << 20)])  # 16 KiB chunks
     rc, _, _ = build([small, big])
-    assert rc == -1 and b"chunk" in lib.dora_gpu_last_error()
+    assert rc == -1 and b"chunk" in _lib.load().dora_gpu_last_error()
     many = [(0x7F0000000000 + m * MiB2, MiB2, 0x1000 + 64 * m, m,
              [(0x10000000, 4096 * j, 4096) for j in range(3)]) for m in range(6)]
     rc, _, _ = build(many)   # 18 segments > 16
-    assert rc == -1 and b"segments" in lib.dora_gpu_last_error()
+    assert rc == -1 and b"segments" in _lib.load().dora_gpu_last_error()
 
 
 @pytest.mark.parametrize("n", [1, 8])

@@ -136,23 +136,13 @@ def test_ladder_sources_rotate_past_the_caches():
     assert bench.native_sources(0) == 64 and bench.native_sources(4096) == 64
 
 
-def test_aql_kernel_name_follows_the_coherent_knob(monkeypatch):
+def test_aql_kernel_name_is_the_region_kernel():
     import bench
-    monkeypatch.delenv("DORA_GPU_AQL_COHERENT", raising=False)
-    monkeypatch.delenv("DORA_GPU_PACK_VARIANT", raising=False)
-    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u4 (AQL)"
-    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
-    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "1")
-    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
-    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_pack_u4 (AQL)"
-    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "all")
-    assert bench.aql_kernel_name("c3", 13000068) == "dora_aql_packc_u4 (AQL)"
-    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1c_u4 (AQL)"
-    monkeypatch.setenv("DORA_GPU_AQL_COHERENT", "0")
-    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u4 (AQL)"
-    monkeypatch.setenv("DORA_GPU_PACK_VARIANT", "u8nt")
-    monkeypatch.delenv("DORA_GPU_AQL_COHERENT")
-    assert bench.aql_kernel_name("c2", 40960000) == "dora_aql_pack1_u8 (AQL)"
+    assert bench.aql_kernel_name("c2") == "dora_aql_pack1_u4 (AQL)"
+    assert bench.aql_kernel_name("c3") == "dora_aql_pack_u4 (AQL)"
+    assert bench.aql_kernel_name("c2", {"dora_aql_pack1_u4": 18, "dora_aql_pack1c_u4": 2}) == \
+        "dora_aql_pack1_u4 (AQL)"
+    assert bench.aql_kernel_name("c2", {"dora_aql_pack1c_u4": 20}) == "dora_aql_pack1c_u4 (AQL)"
 
 
 def test_compact_line_fits_the_driver_tail():

@@ -29,7 +29,7 @@ def _set(base, off, v):
 
 
 def test_in_kernel_epochs_only_grow():
-    lib = _lib.load()
+    lib = _lib.load_testing()
     raw = ctypes.create_string_buffer(256)
     base = (ctypes.addressof(raw) + 63) & ~63
     _set(base, EPOCH, 7)
@@ -39,7 +39,7 @@ def test_in_kernel_epochs_only_grow():
 
 
 def test_cp_fill_completes_on_the_decrement(line):
-    lib = _lib.load()
+    lib = _lib.load_testing()
     _, base = line
     _set(base, EPOCH, 3)  # the flag's previous (in-kernel) fill
     assert lib.dora_gpu_test_cp_arm(base, 10) == 0
@@ -56,7 +56,7 @@ def test_cp_fill_completes_on_the_decrement(line):
 
 def test_flag_switches_between_rules(line):
     """A flag used by a CP-signalled fill, then an in-kernel one, then a CP one again."""
-    lib = _lib.load()
+    lib = _lib.load_testing()
     _, base = line
     lib.dora_gpu_test_cp_arm(base, 5)
     _set(base, VALUE, 0)
@@ -76,7 +76,7 @@ def test_flag_switches_between_rules(line):
 
 
 def test_misaligned_flag_is_rejected(line):
-    lib = _lib.load()
+    lib = _lib.load_testing()
     _, base = line
     assert lib.dora_gpu_test_fill_reached(base + 8, 1) < 0
     assert lib.dora_gpu_test_cp_arm(base + 8, 1) < 0

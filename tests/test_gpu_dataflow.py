@@ -69,10 +69,7 @@ def test_bench_sink_bit_exact_c2(launcher, tmp_path):
         assert got[size]["mismatches"] == 0
     assert stats["slots_created"] <= 5 * len(sizes), stats
     # every size went through raw AQL packets (40.96 MB in order per queue, aql.cpp)
-    if os.environ.get("DORA_GPU_AQL", "1") != "0":
-        assert paths == {"aql": 30, "hip": 0}, paths
-    else:
-        assert paths == {"aql": 0, "hip": 30}, paths
+    assert paths == {"aql": 30, "hip": 0}, paths
 
 
 def test_payload_beyond_4_gib_bit_exact(launcher, tmp_path):
@@ -118,8 +115,7 @@ def test_payload_beyond_4_gib_bit_exact(launcher, tmp_path):
     assert out["errors"] == 0
     got = {x["size"]: x for x in out["series"]}
     assert got[size]["verified"] == 2 and got[size]["mismatches"] == 0, got
-    if os.environ.get("DORA_GPU_AQL", "1") != "0":
-        assert paths["aql"] == 2, paths
+    assert paths["aql"] == 2, paths
 
 
 def test_slots_recycle_through_drop_tokens(launcher, tmp_path):
@@ -286,8 +282,7 @@ def test_c3_async_burst_batches_bit_exact(launcher):
         assert to_u64(results[seq]["csum"]) == want[seq], seq
     print(f"c3 async burst: {b1['batches'] - b0['batches']} batches carried "
           f"{b1['batched_msgs'] - b0['batched_msgs']} of {len(clouds)} clouds")
-    if os.environ.get("DORA_GPU_AQL_BATCH", "1") != "0":
-        assert b1["batched_msgs"] - b0["batched_msgs"] == len(clouds), (b0, b1)
+    assert b1["batched_msgs"] - b0["batched_msgs"] == len(clouds), (b0, b1)
 
 
 @pytest.mark.parametrize("peer_copy", ["kernel", "sdma"])
@@ -390,10 +385,9 @@ def test_many_small_sends_bit_exact(launcher, tmp_path, mode):
     assert sum(x["mismatches"] for x in out["series"]) == 0
     batched = b1["batched_msgs"] - b0["batched_msgs"]
     print(f"{mode}: {b1['batches'] - b0['batches']} batches carried {batched} of {n_msgs} sends")
-    if mode == "async" and os.environ.get("DORA_GPU_AQL_BATCH", "1") != "0":
+    if mode == "async":
         assert batched > 0, (b0, b1)
-    if os.environ.get("DORA_GPU_AQL", "1") != "0":
-        assert paths["aql"] == n_msgs, paths
+    assert paths["aql"] == n_msgs, paths
 
 
 def test_host_pyarrow_send_to_device_receiver(launcher):

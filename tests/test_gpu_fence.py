@@ -1,79 +1,32 @@
-"""Rewritten device sources and the AQL packets' acquire fence (verdict r02 item 2).
+"""Rewritten device sources and the AQL packets' acquire fence (verdict r02 item 2, ADVICE r04).
 
-r02 dropped the agent-scope acquire fence from single-segment packs, which read their source
-with agent-coherent (`sc1 nt`) loads (`dora_aql_pack1c_u4`).  On gfx950 that fence invalidates
-the CUs' vector L1s (MI355X_MICROARCH.md § visibility: `buffer_inv sc1`, no L2 eviction), so
-the hazard it guards against is a source line still cached after the source was rewritten.  Per
-trial the source (4 KB: one workgroup per pack) is read by every CU (`dora_gpu_l2_touch`) and
-packed 256 times (its lines stay in the caches of the CUs those packs ran on), rewritten behind
-the GPU's back (host stores through the BAR; SDMA; a blit copy), and sent; the receiver
-compares the sample with the new pattern.
+On gfx950 the packet's agent-scope acquire invalidates the CUs' vector L1s
+(MI355X_MICROARCH.md § visibility: `buffer_inv sc1`, no L2 eviction), so the hazard it guards
+against is a source line still cached from an earlier read after the source was rewritten.
+Lone packs (every synchronous send) and the command processor's mid-size packs (1-32 MiB) read
+their source with agent-coherent `sc1 nt` loads and carry no acquire fence
+(`dora_aql_pack1c_u4`, aql.cpp dispatch_locked); pipelined packs outside that window keep the
+fence (`dora_aql_pack1_u4`).
 
-The negative control — L1-cached plain loads (test kernel `dora_aql_pack1p_u4`) without the
-fence — never delivered a stale byte on MI355X (r03, 0 of 40 trials per writer).  With no
-evidence either way the fence went back on (plain non-temporal loads behind it,
-`dora_aql_pack1_u4`).  r04 added a control that does fail (test_in_dispatch_stale_read_control:
-plain loads re-read stale words inside one dispatch, nt and sc1 loads never), and since then
-lone and CP-signalled mid-size packs use the coherent no-fence kernel by default; pipelined
-packs keep the fence.  This test keeps every shipped configuration bit-exact under that sequence
-and reports the cross-dispatch negative control's outcome (a stale delivery there would be
-evidence, and is printed).
-
-Each configuration runs in its own process (tests/fence_probe.py), since the knobs are read once.
+* test_in_dispatch_stale_read_control — the control that can fail: inside ONE dispatch plain
+  loads re-read stale words after a BAR rewrite, nt and sc1 loads never (r04: 256 / 0 / 0 of 256
+  workgroups).
+* test_rewritten_sources_across_dispatches_bit_exact — the cross-dispatch test ADVICE r04 asked
+  for before the fence may stay off: per writer (host stores through the BAR; an SDMA copy from
+  pinned memory), more lone and mid-size packs than the AQL argument ring has slots (512), each
+  after the source's lines were loaded into every XCD's L2 and read by a pack of the previous
+  pattern, the source rewritten with a new pattern right before the send, into rotating slots
+  (the receiver holds its last inputs); every delivered payload is compared byte for byte.
 """
-import json
-import os
-import subprocess
-import sys
+import ctypes
+import threading
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-HERE = os.path.dirname(os.path.abspath(__file__))
-TRIALS = 40
-# bar: host stores through the BAR (the negative control's writer); h2d / d2d: HIP copies
-ENGINES = ("bar", "h2d", "d2d")
-
-CONFIGS = {
-    # negative control (reported, not shipped): L1-cached loads, no fence
-    "plain_no_fence": ({"DORA_GPU_AQL_COHERENT": "plain", "DORA_GPU_AQL_ACQUIRE": "none"},
-                       "dora_aql_pack1p_u4"),
-    "plain_fence": ({"DORA_GPU_AQL_COHERENT": "plain"}, "dora_aql_pack1p_u4"),
-    # the default of pipelined packs: non-temporal loads behind the agent-scope acquire fence
-    # (the probe's packs run alone, which by default take the coherent kernel: turned off here)
-    "default": ({"DORA_GPU_AQL_LONE_COHERENT": "0"}, "dora_aql_pack1_u4"),
-    # the default of lone packs (r04): agent-coherent loads, no fence
-    "lone": ({}, "dora_aql_pack1c_u4"),
-    # opt-in for every single-segment pack: agent-coherent loads, no fence
-    "coherent": ({"DORA_GPU_AQL_COHERENT": "1"}, "dora_aql_pack1c_u4"),
-}
-SHIPPED = ("plain_fence", "default", "lone", "coherent")
-SIZE = 4 << 10   # one chunk: one workgroup per pack
-WARM = 256       # fence_probe.WARM
-
-
-def _probe(cfg, engine):
-    env = dict(os.environ)
-    for k in ("DORA_GPU_AQL_COHERENT", "DORA_GPU_AQL_ACQUIRE", "DORA_GPU_AQL_LONE_COHERENT"):
-        env.pop(k, None)
-    env.update(CONFIGS[cfg][0])
-    r = subprocess.run([sys.executable, os.path.join(HERE, "fence_probe.py"), engine,
-                        str(TRIALS), str(SIZE)], env=env, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0, r.stdout + r.stderr
-    return json.loads(r.stdout.strip().splitlines()[-1])
-
-
-@pytest.mark.skipif(os.environ.get("DORA_GPU_AQL", "1") == "0", reason="AQL dispatch off")
-def test_acquire_fence_negative_control_and_coherent_loads():
-    res = {(c, e): _probe(c, e) for c in CONFIGS for e in ENGINES}
-    print(json.dumps({f"{c}/{e}": r for (c, e), r in res.items()}))
-    for (c, e), r in res.items():
-        assert r["kernels"].get(CONFIGS[c][1]) == TRIALS * (WARM + 1), r
-        if c in SHIPPED:
-            assert r["mismatched"] == 0, r   # every shipped configuration is bit-exact
-    stale = {e: res[("plain_no_fence", e)]["mismatched"] for e in ENGINES}
-    print(f"negative control (L1-cached loads, no acquire fence): stale trials {stale}")
+RING_SLOTS = 512  # aql.cpp kRingSlots
 
 
 def test_in_dispatch_stale_read_control():
@@ -97,3 +50,118 @@ def test_in_dispatch_stale_read_control():
     # the control fails: L1-cached loads read the old words (r04: 256 of 256 workgroups, twice)
     assert out[0][1] > 0, out
     assert out[1][1] == 0 and out[2][1] == 0, out
+
+
+def _kernel_counts(lib, _lib):
+    c = (ctypes.c_uint64 * 16)()
+    m = ctypes.c_size_t()
+    _lib.call("dora_gpu_aql_dispatch_counts", 0, c, 16, ctypes.byref(m))
+    return {lib.dora_gpu_aql_kernel_name(i).decode(): c[i] for i in range(m.value)}
+
+
+@pytest.mark.parametrize("writer", ["bar", "sdma"])
+def test_rewritten_sources_across_dispatches_bit_exact(writer):
+    from dora_amd import _lib, device
+    from dora_amd.dataflow import daemon_spec, parse_descriptor
+    from dora_amd.device import DeviceBuffer
+    from dora_amd.node import Node
+    lib = _lib.load()
+    device.set_device(0)
+    desc = {"nodes": [
+        {"id": "src", "outputs": ["raw", "warm"]},
+        {"id": "dst", "outputs": [], "inputs": {"raw": {"source": "src/raw", "queue_size": 64}}},
+    ]}
+    shm = f"/dora-gpu-fence-{writer}-{id(desc)}"
+    h = ctypes.c_void_p()
+    _lib.call("dora_daemon_create", shm.encode(), daemon_spec(parse_descriptor(desc)).encode(),
+              1 << 20, ctypes.byref(h))
+    t = threading.Thread(target=lambda: lib.dora_daemon_run(h.value, 300000), daemon=True)
+    t.start()
+    nodes = {}
+
+    def mk(i):
+        nodes[i] = Node(i, dataflow=shm, device=0)
+    ts = [threading.Thread(target=mk, args=(i,)) for i in ("src", "dst")]
+    [x.start() for x in ts]
+    [x.join(60) for x in ts]
+    src, dst = nodes["src"], nodes["dst"]
+    small, mid = 4096, (2 << 20) + 48  # a lone in-kernel-signalled pack; a CP-window pack
+    cap = mid + 64
+    s = device.Stream()
+    if writer == "bar":
+        bp = ctypes.c_void_p()
+        _lib.call("dora_gpu_test_bar_alloc", 0, cap, ctypes.byref(bp))
+        src_ptr = bp.value
+    else:
+        S = DeviceBuffer(cap)
+        src_ptr = S.ptr
+    hp = ctypes.c_void_p()
+    _lib.call("dora_gpu_host_alloc", ctypes.byref(hp), cap)
+    host = (ctypes.c_uint8 * cap).from_address(hp.value)
+    got = ctypes.create_string_buffer(cap)
+    rng = np.random.default_rng(0xFE9CE)
+    k0 = _kernel_counts(lib, _lib)
+    trials = RING_SLOTS + 88  # every argument-ring slot reused
+    held, bad, asyncs = [], [], 0
+    pat = rng.integers(0, 256, cap, dtype=np.uint8)
+    ctypes.memmove(host, pat.ctypes.data, cap)
+    if writer == "bar":
+        _lib.call("dora_gpu_test_bar_write", 0, src_ptr, hp.value, cap)
+    else:
+        _lib.call("dora_gpu_memcpy_async", src_ptr, hp.value, cap, s.handle)
+        s.sync()
+    for k in range(trials):
+        n = mid if k % 2 else small
+        # the source's current lines in every XCD's L2, and read by a pack of this pattern (on an
+        # output without receivers: its token comes back at once)
+        _lib.call("dora_gpu_test_l2_touch", src_ptr, n, s.handle)
+        s.sync()
+        src.send_output_device_bytes("warm", src_ptr, n)
+        # rewrite the source behind the GPU's caches
+        pat = rng.integers(0, 256, n, dtype=np.uint8)
+        ctypes.memmove(host, pat.ctypes.data, n)
+        if writer == "bar":
+            _lib.call("dora_gpu_test_bar_write", 0, src_ptr, hp.value, n)
+        else:
+            _lib.call("dora_gpu_memcpy_async", src_ptr, hp.value, n, s.handle)
+            s.sync()
+        # every fourth mid-size send asynchronous (pipelined into the CP window), the rest the
+        # default synchronous send (a lone pack)
+        if n == mid and k % 4 == 3:
+            src.send_output_device_bytes("raw", src_ptr, n, {"k": k}, asynchronous=True)
+            src.sync()
+            asyncs += 1
+        else:
+            src.send_output_device_bytes("raw", src_ptr, n, {"k": k})
+        ev = dst.next(timeout=30)
+        assert ev is not None and ev["type"] == "INPUT" and ev["metadata"] == {"k": k}, ev
+        _lib.call("dora_gpu_memcpy_async", got, ev["data_ptr"], n, None)
+        _lib.call("dora_gpu_device_sync")
+        if np.frombuffer(got.raw[:n], np.uint8).tobytes() != pat.tobytes():
+            bad.append((k, n))
+        held.append(ev)  # slots rotate: the sender cannot reuse the newest three
+        if len(held) > 3:
+            old = held.pop(0)
+            old["value"].close()
+            old["_event"].free()
+    for old in held:
+        old["value"].close()
+        old["_event"].free()
+    held.clear()
+    k1 = _kernel_counts(lib, _lib)
+    used = {x: k1[x] - k0.get(x, 0) for x in k1 if k1[x] - k0.get(x, 0)}
+    src.close()
+    dst.close()
+    t.join(60)
+    lib.dora_daemon_free(h.value)
+    if writer == "bar":
+        _lib.load_testing().dora_gpu_test_bar_free(src_ptr)
+    else:
+        S.free()
+    _lib.call("dora_gpu_host_free", hp.value)
+    s.close()
+    print(f"{writer}: {trials} rewritten sources ({asyncs} async), kernels {used}, stale {bad}")
+    assert not bad, bad
+    # the fenceless coherent kernel packed them all, through more dispatches than ring slots
+    assert used.get("dora_aql_pack1c_u4", 0) >= trials, used
+    assert sum(used.values()) > RING_SLOTS, used

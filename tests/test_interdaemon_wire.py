@@ -27,12 +27,12 @@ EVENT_NS = 1_700_000_000_223_456_789
 
 
 def _call(fn, *args):
-    lib = _lib.load()
+    lib = _lib.load_testing()
     n = ctypes.c_size_t()
     getattr(lib, fn)(*args, None, 0, ctypes.byref(n))
     buf = ctypes.create_string_buffer(max(1, n.value))
     rc = getattr(lib, fn)(*args, buf, n.value, ctypes.byref(n))
-    assert rc == 0, lib.dora_gpu_last_error()
+    assert rc == 0, _lib.load().dora_gpu_last_error()
     return buf.raw[:n.value]
 
 
@@ -50,12 +50,12 @@ def encode_closed(pairs, df=DF):
 
 
 def decode(frame: bytes) -> dict:
-    lib = _lib.load()
+    lib = _lib.load_testing()
     n = ctypes.c_size_t()
     buf = ctypes.create_string_buffer(1 << 20)
     rc = lib.dora_gpu_test_ide_decode(frame, len(frame), buf, len(buf), ctypes.byref(n))
     if rc != 0:
-        raise ValueError(lib.dora_gpu_last_error().decode())
+        raise ValueError(_lib.load().dora_gpu_last_error().decode())
     return json.loads(buf.value.decode())
 
 
@@ -228,10 +228,10 @@ def test_validity_left_in_the_sample_is_refused():
     sl = int.from_bytes(ti[:4], "little")
     tag_at = 4 + sl + 16
     assert ti[tag_at] == 1
-    lib = _lib.load()
+    lib = _lib.load_testing()
     n = ctypes.c_size_t()
     ti2 = bytes(ti[:tag_at]) + b"\x02" + (0).to_bytes(8, "little") + (1).to_bytes(8, "little") + \
         bytes(ti[tag_at + 1 + 8 + 1:])
     rc = lib.dora_gpu_test_ide_output(DF.encode(), b"s", b"o", ti2, len(ti2), b"", 0, 0, 0, HLC,
                                       b"", 0, 0, None, 0, ctypes.byref(n))
-    assert rc != 0 and b"validity" in lib.dora_gpu_last_error()
+    assert rc != 0 and b"validity" in _lib.load().dora_gpu_last_error()
