@@ -124,6 +124,7 @@ _SIGS = {
     "dora_node_send_output_bytes_ex": (c_int, [c_void_p, c_char_p, c_void_p, c_size_t, c_int32,
                                                c_char_p, c_size_t, ctypes.c_uint32]),
     "dora_node_set_async_sends": (c_int, [c_void_p, c_int]),
+    "dora_node_set_event_thread": (c_int, [c_void_p, c_int]),
     "dora_node_close_outputs": (c_int, [c_void_p, POINTER(c_char_p), c_size_t]),
     "dora_node_next_event": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
     "dora_event_type": (c_int, [c_void_p]),

@@ -19,6 +19,7 @@
 #include <x86intrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -521,6 +522,15 @@ struct NodeCore {
     (void)hipGetLastError();
   }
 
+  // Order stream `s` after the work queued on the node stream so far (producer kernels of a source).
+  void order_after_node_stream(hipStream_t s) {
+    if (hipStreamQuery(stream) == hipErrorNotReady) {
+      if (!node_ev) (void)hipEventCreateWithFlags(&node_ev, hipEventDisableTiming);
+      if (node_ev && hipEventRecord(node_ev, stream) == hipSuccess) (void)hipStreamWaitEvent(s, node_ev, 0);
+    }
+    (void)hipGetLastError();
+  }
+
   hipStream_t next_fill_stream() {
     ensure_fill_streams();
     if (fill_streams.empty()) return stream;
@@ -675,6 +685,17 @@ struct dora_node {
   uint64_t bytes_ti_len = 0;
   std::deque<std::unique_ptr<dora_event>> queue;
   bool ended = false;
+  // Event-stream thread (dora_node_set_event_thread; started by every node that joins an RCCL
+  // broadcast group as a receiver): the reference's event_stream_loop (event_stream/thread.rs:
+  // 81-188) — it drains the daemon's ring into `queue` continuously and applies the drop-oldest
+  // policy there (node_communication/mod.rs:320-359), so inputs keep arriving, their broadcast
+  // receives are posted and the tokens of dropped inputs go back while the user thread is busy
+  // elsewhere.  `qmu` guards `queue` and `ended` while it runs.
+  std::thread pump;
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::atomic<bool> pump_on{false}, pump_stop{false};
+  bool want_pump = false;  // a broadcast group was joined: start the thread at the next chance
   // profiling of the pack kernel on the node stream
   bool profile = false;
   std::vector<dora::TimingPair> timing;  // ring of kTimingPairs
@@ -733,8 +754,15 @@ struct dora_node {
   std::unordered_map<uint64_t, size_t> plan_index;  // hash of a key -> its plan_cache entry
   std::vector<uint64_t> plan_key_buf;
   uint64_t plan_clock = 0, plan_hits = 0;
-  // RCCL broadcast groups of this node's fan-out outputs (rank 0 of each), DORA_GPU_FANOUT=rccl
-  std::map<std::string, dora::BcastComm*> bcast_out;
+  // RCCL broadcast groups of this node's fan-out outputs (rank 0 of each), DORA_GPU_FANOUT=rccl.
+  // Each output packs and broadcasts on a stream of its own: a rank that stalls the collective
+  // holds up that output only (its slots, then its in-flight cap), not the node stream nor the
+  // node's other outputs.
+  struct BcastOut {
+    dora::BcastComm* comm = nullptr;
+    hipStream_t stream = nullptr;
+  };
+  std::map<std::string, BcastOut> bcast_out;
   uint64_t bcast_seq = 0;
   dora::StdoutCapture* stdout_capture = nullptr;  // send_stdout_as (DORA_GPU_SEND_STDOUT_AS)
   // zero-copy forwards: the input re-sent in place, kept (and its producer's token held) until
@@ -1072,6 +1100,10 @@ void join_bcast_group(dora_node* n, const std::string& input, const uint8_t* uid
   auto it = c->bcast_in.find(input);
   if (it != c->bcast_in.end()) bcast_close(it->second, c->bcast_stream, 10000);
   c->bcast_in[input] = comm;
+  // a rank that stops polling must not stall the collective for the others: post receives
+  // from the event-stream thread (started by the user thread when it next returns from the
+  // event loop, dora_node_next_event / init)
+  n->want_pump = true;
 }
 
 // A FILL_BCAST sample: post this rank's receive of the producer's broadcast into the receive
@@ -1440,14 +1472,17 @@ bool fill_in_transit(dora_node* n, const dora_event* e) {
   return mono_ns() - e->arrived_ns < kTransitLimitNs;
 }
 
-// drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input
-void drop_oldest_inputs(dora_node* n) {
+// drop_oldest_inputs (node_communication/mod.rs:320-359): newest first, keep queue_size per input.
+// `held_front`: the queue's first event counts as taken (the event-stream thread's: the one the
+// reference's thread holds in its channel, event_stream/thread.rs:139-157).
+void drop_oldest_inputs(dora_node* n, bool held_front = false) {
   // no input can exceed its queue size while the whole queue holds no more events than the
   // smallest one (the common case of a receiver keeping up): nothing to count
-  if (n->queue_size.empty() || n->queue.size() <= n->min_queue_size) return;
+  const size_t held = held_front ? 1 : 0;
+  if (n->queue_size.empty() || n->queue.size() <= n->min_queue_size + held) return;
   SubSpan sp(SP_RECV_DROPOLD);
   std::map<std::string, uint32_t> remaining = n->queue_size;
-  for (auto it = n->queue.rbegin(); it != n->queue.rend(); ++it) {
+  for (auto it = n->queue.rbegin(); it != n->queue.rend() - std::ptrdiff_t(held); ++it) {
     dora_event* e = it->get();
     if (!e || e->type != DORA_EVENT_INPUT) continue;
     auto q = remaining.find(e->id);
@@ -1478,6 +1513,34 @@ bool drain_events(dora_node* n) {
     got = true;
   }
   return got;
+}
+
+// The event-stream thread (dora_node::pump): drain, apply drop-oldest, wake the user thread.
+void pump_main(dora_node* n) {
+  while (!n->pump_stop.load(std::memory_order_acquire)) {
+    bool got;
+    {
+      std::lock_guard<std::mutex> g(n->qmu);
+      got = drain_events(n);
+      if (got) drop_oldest_inputs(n, /*held_front=*/true);
+    }
+    if (got) n->qcv.notify_all();
+    else n->core->ev.wait(10000);  // bounded: notices pump_stop
+  }
+}
+
+void start_pump(dora_node* n) {
+  if (n->pump_on.load()) return;
+  n->pump_stop.store(false);
+  n->pump_on.store(true);
+  n->pump = std::thread(pump_main, n);
+}
+
+void stop_pump(dora_node* n) {
+  if (!n->pump_on.load()) return;
+  n->pump_stop.store(true, std::memory_order_release);
+  if (n->pump.joinable()) n->pump.join();
+  n->pump_on.store(false);
 }
 
 // The Metadata of a send as WBuf::bytes(WBuf::metadata(m)) would write it, straight into `w`
@@ -1535,17 +1598,20 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
       d.ipc.fill = sample->fill;
       auto g = n->bcast_out.find(output_id);
       if (g != n->bcast_out.end()) {
-        // fan-out over the output's RCCL group: broadcast the slot on the node stream, after
-        // every fill so far (fills of other streams / the AQL queues are fenced first)
+        // fan-out over the output's RCCL group: broadcast the slot on the output's stream, after
+        // its pack there (pack_and_send), or — a sample the user filled — after the work queued on
+        // the node stream and every fill so far
+        hipStream_t bs = g->second.stream;
         if (sample->fill != FILL_DONE) n->core->fence_fills();
-        int rc = bcast_enqueue(g->second, slot->ptr, d.ipc.ext_len, n->core->stream);
-        // the broadcast reads the slot on the node stream: the slot is idle after it
+        n->core->order_after_node_stream(bs);
+        int rc = bcast_enqueue(g->second.comm, slot->ptr, d.ipc.ext_len, bs);
+        // the broadcast reads the slot on its stream: the slot is idle after it
         if (!slot->use_ev && hipEventCreateWithFlags(&slot->use_ev, hipEventDisableTiming) != hipSuccess)
           slot->use_ev = nullptr;
-        if (slot->use_ev && hipEventRecord(slot->use_ev, n->core->stream) == hipSuccess)
+        if (slot->use_ev && hipEventRecord(slot->use_ev, bs) == hipSuccess)
           slot->use_pending = true;
         else
-          (void)hipStreamSynchronize(n->core->stream);
+          (void)hipStreamSynchronize(bs);
         (void)hipGetLastError();
         if (rc != DORA_OK) {
           add_to_cache(n, slot);
@@ -1964,16 +2030,25 @@ void form_bcast_groups(dora_node* n) {
       continue;
     }
     BcastComm* comm = nullptr;
-    if (bcast_join(uid, static_cast<int>(nranks), 0, 30000, &comm) == DORA_OK)
-      n->bcast_out[o] = comm;
-    else
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      c->bcast_error = "broadcast stream of output `" + o + "`";
+      continue;
+    }
+    if (bcast_join(uid, static_cast<int>(nranks), 0, 30000, &comm) == DORA_OK) {
+      n->bcast_out[o] = {comm, st};
+    } else {
       c->bcast_error = dora_gpu_last_error();
+      (void)hipStreamDestroy(st);
+    }
   }
 }
 
 // What a synchronous send of a device source waits for: the pack has read the whole source.
 struct SourceWait {
   uint8_t kind = FILL_DONE;  // FILL_FLAG: flag >= epoch; FILL_EVENT: event; FILL_BCAST: stream
+  hipStream_t stream = nullptr;  // FILL_BCAST: the output's broadcast stream
   const std::atomic<uint64_t>* flag = nullptr;
   uint64_t epoch = 0;
   hipEvent_t event = nullptr;
@@ -1999,8 +2074,8 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
     }
   } else if (w.kind == FILL_EVENT && w.event) {
     DORA_HIP(hipEventSynchronize(w.event));
-  } else if (w.kind == FILL_BCAST) {
-    DORA_HIP(hipStreamSynchronize(n->core->stream));
+  } else if (w.kind == FILL_BCAST && w.stream) {
+    DORA_HIP(hipStreamSynchronize(w.stream));
   }
   return DORA_OK;
 }
@@ -2045,12 +2120,14 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
       ++n->region_packs;
       n->region_bytes += plan->size;
     }
-    // a broadcast-group output packs on the node stream, where its broadcast follows
-    const bool bcast = n->bcast_out.count(output_id) > 0;
+    // a broadcast-group output packs on its own stream, where its broadcast follows
+    auto bo = n->bcast_out.find(output_id);
+    const bool bcast = bo != n->bcast_out.end();
+    if (bcast) n->core->order_after_node_stream(bo->second.stream);
     const bool sync = plan->dev == ARROW_DEVICE_ROCM &&
                       !((flags & DORA_SEND_ASYNC) || n->async_default);
     rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
-                     bcast ? n->core->stream : nullptr, t_start, t_stop, !bcast, sync);
+                     bcast ? bo->second.stream : nullptr, t_start, t_stop, !bcast, sync);
     if (rc != DORA_OK) {
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
@@ -2076,7 +2153,9 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   const bool sync_src = plan->dev == ARROW_DEVICE_ROCM && s->slot && plan->size &&
                         !((flags & DORA_SEND_ASYNC) || n->async_default);
   if (sync_src) {
-    wait.kind = n->bcast_out.count(output_id) ? uint8_t(FILL_BCAST) : s->fill;
+    auto bo = n->bcast_out.find(output_id);
+    wait.kind = bo != n->bcast_out.end() ? uint8_t(FILL_BCAST) : s->fill;
+    if (bo != n->bcast_out.end()) wait.stream = bo->second.stream;
     wait.epoch = s->epoch;
     if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
     if (s->fill == FILL_EVENT) wait.event = s->slot->done;
@@ -2222,6 +2301,7 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     core->ev.wait(100000);
   }
   if (device >= 0 && dora::fanout_rccl() && !n->outputs.empty()) dora::form_bcast_groups(n);
+  if (n->want_pump) dora::start_pump(n);  // a broadcast group joined during init
   // send_stdout_as (spawn.rs:280-437): the descriptor names one of this node's outputs
   if (const char* so = std::getenv("DORA_GPU_SEND_STDOUT_AS")) {
     if (!n->outputs.count(so)) {
@@ -2259,6 +2339,7 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   } flush_trace_at_end;
   dora::stdout_capture_stop(n->stdout_capture);  // the last lines go out before the outputs close
   n->stdout_capture = nullptr;
+  dora::stop_pump(n);  // the event-stream thread first: the queue is this thread's again
   std::vector<std::string> outs(n->outputs.begin(), n->outputs.end());
   dora::WBuf w;
   w.u32(static_cast<uint32_t>(outs.size()));
@@ -2276,7 +2357,10 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
   n->forwarded.clear();  // inputs still held by unanswered forwards: their tokens go back
   (void)n->core->request(dora::REQ_OUTPUTS_DONE, {});
   // broadcasts read the slots: the groups go (after their streams drain, bounded) first
-  for (auto& kv : n->bcast_out) dora::bcast_close(kv.second, n->core->stream, 10000);
+  for (auto& kv : n->bcast_out) {
+    dora::bcast_close(kv.second.comm, kv.second.stream, 10000);
+    (void)hipStreamDestroy(kv.second.stream);
+  }
   n->bcast_out.clear();
   for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
   for (auto* s : n->cache) dora::free_slot(n, s);
@@ -2478,6 +2562,15 @@ int dora_node_set_async_sends(dora_node* n, int enable) {
   return DORA_OK;
 }
 
+int dora_node_set_event_thread(dora_node* n, int enable) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  DORA_GUARD_BEGIN
+  if (enable) dora::start_pump(n);
+  else dora::stop_pump(n);
+  return DORA_OK;
+  DORA_GUARD_END
+}
+
 int dora_node_set_compact(dora_node* n, int enable) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   n->compact = enable != 0;
@@ -2504,8 +2597,37 @@ int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
   *out = nullptr;
   DORA_GUARD_BEGIN
   const uint64_t t0 = dora::mono_ns();
+  if (n->want_pump && !n->pump_on.load()) dora::start_pump(n);
+  if (n->pump_on.load()) {
+    // the event-stream thread fills the queue: take its oldest event
+    std::unique_lock<std::mutex> g(n->qmu);
+    for (;;) {
+      if (!n->queue.empty()) {
+        *out = n->queue.front().release();
+        n->queue.pop_front();
+        if ((*out)->type == DORA_EVENT_ALL_INPUTS_CLOSED) n->ended = true;
+        g.unlock();
+        dora::finish_input(n, *out);
+        return DORA_OK;
+      }
+      if (n->ended) return dora::fail(DORA_ERR_CLOSED, "event stream closed");
+      if (timeout_us < 0) {
+        n->qcv.wait_for(g, std::chrono::milliseconds(100));
+        continue;
+      }
+      const int64_t left = timeout_us - int64_t(dora::mono_ns() - t0) / 1000;
+      if (left <= 0) return dora::fail(DORA_ERR_TIMEOUT, "no event within timeout");
+      n->qcv.wait_for(g, std::chrono::microseconds(left));
+    }
+  }
   for (;;) {
     const bool got = dora::drain_events(n);
+    if (n->want_pump && !n->pump_on.load()) {
+      // a broadcast group was joined while draining: the thread takes over from here
+      dora::start_pump(n);
+      return dora_node_next_event(n, timeout_us < 0 ? -1
+                                     : std::max<int64_t>(0, timeout_us - int64_t(dora::mono_ns() - t0) / 1000), out);
+    }
     if (!n->queue.empty()) {
       // The event handed over now is the node's, like the one the reference's event-stream
       // thread holds (event_stream/thread.rs:139-157: taken from the daemon's queue, in its
@@ -2514,6 +2636,7 @@ int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
       // a default receiver drop, whenever that receiver pauses.
       *out = n->queue.front().release();
       n->queue.pop_front();
+      if ((*out)->type == DORA_EVENT_ALL_INPUTS_CLOSED) n->ended = true;
       if (got) dora::drop_oldest_inputs(n);
       dora::finish_input(n, *out);
       return DORA_OK;
@@ -2843,7 +2966,7 @@ int dora_node_bcast_ranks(dora_node* n, uint64_t* max_ranks) {
   if (!n || !max_ranks) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   *max_ranks = 0;
   for (const auto& kv : n->bcast_out)
-    *max_ranks = std::max<uint64_t>(*max_ranks, uint64_t(dora::bcast_nranks(kv.second)));
+    *max_ranks = std::max<uint64_t>(*max_ranks, uint64_t(dora::bcast_nranks(kv.second.comm)));
   return DORA_OK;
 }
 

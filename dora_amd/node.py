@@ -184,6 +184,12 @@ class Node:
         """Make every send of this node asynchronous (dora_node_set_async_sends)."""
         call("dora_node_set_async_sends", self.handle, int(enable))
 
+    def set_event_thread(self, enable: bool = True):
+        """Drain the daemon's events on a background thread (the reference's event-stream thread;
+        dora_node_set_event_thread): inputs keep arriving, with the drop-oldest policy applied,
+        while this node's user thread is busy elsewhere."""
+        call("dora_node_set_event_thread", self.handle, int(enable))
+
     def send_output_device_bytes(self, output_id: str, ptr: int, n: int,
                                  metadata: Optional[dict] = None, *, asynchronous: bool = False):
         """send_output_raw with an HBM source: one pack kernel into a fresh device sample;

@@ -295,6 +295,14 @@ int dora_node_send_output_bytes_ex(dora_node* node, const char* output_id, const
                                    size_t params_len, uint32_t flags);
 /* Make DORA_SEND_ASYNC the default of every send of this node (also DORA_GPU_SEND_ASYNC=1). */
 int dora_node_set_async_sends(dora_node* node, int enable);
+/* Event-stream thread (the reference's event_stream_loop, apis/rust/node/src/event_stream/
+ * thread.rs:81-188; no counterpart in the C API): `enable` starts a thread that drains the
+ * daemon's events into the node's input queue continuously and applies the drop-oldest policy
+ * there (node_communication/mod.rs:320-359), so inputs keep arriving — broadcast receives posted,
+ * tokens of dropped inputs returned — while the user thread is busy; dora_node_next_event then
+ * takes events from that queue.  Nodes that receive over an RCCL broadcast group start it
+ * themselves.  0 stops it. */
+int dora_node_set_event_thread(dora_node* node, int enable);
 /* Use compacting plans (dora_gpu_plan_compact) in dora_node_send_output for device arrays. */
 int dora_node_set_compact(dora_node* node, int enable);
 /* close_outputs (mod.rs:277-289). */

@@ -223,6 +223,68 @@ def test_host_only_receiver_holding_shared_memory_inputs():
     d.join()
 
 
+def test_event_thread_decouples_a_receiver_that_never_polls():
+    """Verdict r04 item 3: a receiver whose event-stream thread runs (dora_node_set_event_thread,
+    the reference's event_stream_loop) but whose user thread never calls next_event keeps taking
+    events off the daemon and applies drop-oldest to them, as the reference's daemon-side queue
+    does (node_communication/mod.rs:320-359): the producer's tokens come back (its in-flight
+    samples stay bounded by that receiver's queue_size + the one its thread holds), the other
+    receiver gets every message, and the producer's sends do not slow down.  Without the thread
+    the same receiver holds every sample it was sent.  (An RCCL broadcast group posts its
+    receives from this thread; a group needs >= 2 GPUs.)"""
+    def run(thread):
+        d = InProcessDaemon({"nodes": [
+            {"id": "src", "outputs": ["o"]},
+            {"id": "idle", "inputs": {"i": {"source": "src/o", "queue_size": 2}}},
+            {"id": "busy", "inputs": {"i": {"source": "src/o", "queue_size": 1000}}}]})
+        nodes = _start_nodes(d.shm, ["src", "idle", "busy"])
+        src, idle, busy = nodes["src"], nodes["idle"], nodes["busy"]
+        if thread:
+            idle.set_event_thread(True)
+        n, got, t_send = 40, [], []
+        for k in range(n):
+            t0 = time.perf_counter()
+            src.send_output("o", bytes([k]) * 8192, {"k": k})  # shared-memory samples: tokens
+            t_send.append(time.perf_counter() - t0)
+            ev = busy.next(timeout=10)
+            got.append(ev["metadata"]["k"])
+            assert as_bytes(ev["value"]) == bytes([k]) * 8192
+            del ev
+        deadline = time.monotonic() + (5 if thread else 0.5)
+        while time.monotonic() < deadline:
+            src.send_output("o", b"", {"k": -1})  # the producer handles returned tokens
+            busy.next(timeout=5)
+            if src.stats()["in_flight"] <= 3:
+                break
+            time.sleep(0.01)
+        in_flight = src.stats()["in_flight"]
+        dropped = src.dataflow_counters("idle")["dropped_inputs"]
+        # what the idle receiver finally reads: the event its thread held, then the newest ones
+        seen = []
+        while True:
+            ev = idle.next(timeout=0.3)
+            if ev is None:
+                break
+            if ev["type"] == "INPUT" and ev["metadata"]["k"] >= 0:
+                seen.append(ev["metadata"]["k"])
+            del ev
+        for x in (src, idle, busy):
+            x.close()
+        d.join()
+        return got, in_flight, dropped, seen, sorted(t_send)[len(t_send) // 2]
+    got, in_flight, dropped, seen, t50 = run(thread=True)
+    assert got == list(range(40))
+    assert in_flight <= 3, in_flight
+    assert dropped >= 37, dropped
+    # the event its thread held (the oldest), then at most queue_size of the newest
+    assert seen[0] == 0 and len(seen) <= 3 and set(seen[1:]) <= {38, 39}, seen
+    got0, in_flight0, dropped0, seen0, t50_0 = run(thread=False)
+    assert got0 == list(range(40))
+    assert in_flight0 == 40 and dropped0 == 0, (in_flight0, dropped0)  # held until it polls
+    print(f"send p50 with / without the idle receiver's thread: {t50 * 1e6:.1f} / "
+          f"{t50_0 * 1e6:.1f} us")
+
+
 def test_busy_stats_count_blocked_time():
     """dora_gpu_busy_stats: a receiver blocked on its empty event ring accumulates idle time
     (the diagnostics the bench tools report as busy = wall - idle)."""
