@@ -14,9 +14,7 @@ from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int6
 from .arrow_c import ArrowArray, ArrowSchema
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-# DORA_GPU_LIB: another build of the library for this process (A/B of two builds on one box;
-# spawned tools keep the in-tree one through their rpath)
-LIB_PATH = os.environ.get("DORA_GPU_LIB") or os.path.join(LIB_DIR, "libdora_gpu.so")
+LIB_PATH = os.path.join(LIB_DIR, "libdora_gpu.so")
 TESTING_PATH = os.path.join(LIB_DIR, "libdora_gpu_testing.so")
 
 ARROW_DEVICE_CPU = 1

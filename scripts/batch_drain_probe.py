@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """GPU-side rate of batch packs: N async sends held in the AQL backlog (dora_gpu_test_aql_hold),
 then released at once — the time from the release to every fill complete is the device's rate
-for batches of up to 8 messages; with DORA_GPU_AQL_BATCH=0 the same N sends go out one packet
-each (4 queues, no depth limit).  Sources rotate past the caches.  Run with
+for batches of up to 8 messages.  Sources rotate past the caches.  Run with
 DORA_GPU_MAX_IN_FLIGHT >= N.
 
     DORA_GPU_MAX_IN_FLIGHT=64 python scripts/batch_drain_probe.py --sizes 4096000 --n 64
@@ -48,7 +47,7 @@ def main():
     [x.join(60) for x in ts]
     src, dst = nodes["src"], nodes["dst"]
     src.set_async_sends(True)
-    batch = os.environ.get("DORA_GPU_AQL_BATCH", "1") != "0"
+    batch = True
     for size in [int(x) for x in a.sizes.split(",")]:
         nsrc = max(2, min(64, (1 << 30) // size))
         bufs = [device.DeviceBuffer(size) for _ in range(nsrc)]

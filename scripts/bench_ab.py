@@ -2,7 +2,7 @@
 """Interleaved A/B of environment knobs on bench.py's headline (C2, 40.96 MB) and C3 workloads
 (no ladders, no CPU baseline); one JSON line per run.
 
-    python scripts/bench_ab.py --rounds 2 --steps 1000 --cfg base= --cfg fence_off=DORA_GPU_AQL_COHERENT=1
+    python scripts/bench_ab.py --rounds 2 --steps 1000 --cfg base= --cfg cap10=DORA_GPU_MAX_IN_FLIGHT=10:8
 """
 import argparse
 import json

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """The bench's C3 block alone (bench.run_c3_block: warm-up, 200-send steady region, 20-send
 burst) `--reps` times in one dataflow, printing per rep the burst's send-call times, pack starts
-and fraction of HBM; with DORA_GPU_SUBPHASES=1 the sender's host sub-phases follow at exit.
+and fraction of HBM; with DORA_GPU_TRACE=subphases the sender's host sub-phases follow at exit.
 Diagnoses the burst's host stall with CP-signalled multi-segment packs.
 
-    DORA_GPU_AQL_CP_MULTI=1 python scripts/c3_burst_probe.py --reps 3
+    python scripts/c3_burst_probe.py --reps 3
 """
 import argparse
 import json
@@ -42,7 +42,7 @@ def main():
 
         for r in range(a.reps):
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
-            print(json.dumps({"rep": r, "cp_multi": os.environ.get("DORA_GPU_AQL_CP_MULTI", "0"),
+            print(json.dumps({"rep": r, 
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
                               "send_calls_us": c3["send_calls_us"],

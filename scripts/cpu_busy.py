@@ -1,7 +1,7 @@
 """Per-CPU busy share between two /proc/stat snapshots (scripts/lat_tail_ab.sh).
 
 `snap` prints {cpu: [busy_ticks, total_ticks]}; busy() reduces two snapshots to the busy share
-of every CPU plus the CPUs of L3 domain 0 of NUMA node 0 (where DORA_GPU_PIN_L3 puts the
+of every CPU plus the CPUs of L3 domain 0 of NUMA node 0 (where DORA_GPU_PIN=fixed puts the
 dataflow of GPU 0) and of the whole box.
 """
 import json

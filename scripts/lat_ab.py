@@ -2,7 +2,7 @@
 """Interleaved A/B of environment knobs on bench.py's latency ladder (1000 messages per size,
 1 ms apart; no throughput ladders); one JSON line per run with p50 / p99 per size.
 
-    python scripts/lat_ab.py --rounds 2 --cfg base= --cfg prio=DORA_GPU_AQL_PRIORITY=high
+    python scripts/lat_ab.py --rounds 2 --cfg base= --cfg numa=DORA_GPU_PIN=numa
 """
 import argparse
 import json

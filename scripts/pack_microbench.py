@@ -77,12 +77,12 @@ def main():
             for v in variants:
                 kind, u, nt, ch = v
                 if kind == "pack":
-                    call("dora_gpu_pack_tune", u, nt, ch)
+                    call("dora_gpu_test_pack_tune", u, nt, ch)
                 elif kind == "wtgrid":  # write-through stores, no signal, grid capped at u
-                    call("dora_gpu_pack_tune", 0, 2, ch)
+                    call("dora_gpu_test_pack_tune", 0, 2, ch)
                 elif kind == "sig":  # (grid, unroll, chunk)
-                    call("dora_gpu_pack_tune", nt, -1, ch)
-                call("dora_gpu_pack_signal_tune", u if kind in ("sig", "wtgrid") else 0,
+                    call("dora_gpu_test_pack_tune", nt, -1, ch)
+                call("dora_gpu_test_pack_signal_tune", u if kind in ("sig", "wtgrid") else 0,
                      int(kind == "sig"))
 
                 def launch(k):
@@ -99,9 +99,9 @@ def main():
                 e1.record(s)
                 e1.sync()
                 res[v].append(e0.elapsed_ms(e1) / args.iters)
-        call("dora_gpu_pack_tune", 0, -1, 0)
-        call("dora_gpu_pack_signal_tune", 0, 0)
-        call("dora_gpu_pack_tune", 0, -1, 0)
+        call("dora_gpu_test_pack_tune", 0, -1, 0)
+        call("dora_gpu_test_pack_signal_tune", 0, 0)
+        call("dora_gpu_test_pack_tune", 0, -1, 0)
         for v in variants:
             ms = statistics.median(res[v])
             gbs = 2 * size / (ms * 1e-3) / 1e9

@@ -5,7 +5,7 @@ workgroup writes into the fill flag's line, and, per AQL queue (sends rotate ove
 the gap from one pack's signal to the next pack's start on the same queue (negative: the two
 overlapped).  Sources rotate past the caches.
 
-    DORA_GPU_AQL_QUEUES=1 python scripts/pack_timeline.py --size 4096000 --n 2000
+    python scripts/pack_timeline.py --size 4096000 --n 2000
 """
 import argparse
 import json
@@ -68,7 +68,7 @@ def main():
     node.sync()
     reg = node.region_end()
     iv = node.pack_intervals()[-a.n:]
-    nq = int(os.environ.get("DORA_GPU_AQL_QUEUES", "4"))
+    nq = 4  # aql.cpp kQueues
     own = [(b - x) * 1e3 for x, b in iv]
     gaps = [(iv[i + nq][0] - iv[i][1]) * 1e3 for i in range(len(iv) - nq)]
     starts = sorted(x for x, _ in iv)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput mode of the Python node (this process, dora_amd.node.Node via the CPython send path)
 -> the native bench sink, per size: the Python counterpart of scripts/native_tp.py, with the
-sink's and the daemon's host sub-phases when DORA_GPU_SUBPHASES=1 (this process prints its own to
+sink's and the daemon's host sub-phases when DORA_GPU_TRACE=subphases (this process prints its own to
 stderr at exit).
 
     python scripts/py_tp.py --sizes 1048576,4096000 --n 5000 [--sources 16]
