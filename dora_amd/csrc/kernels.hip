@@ -718,6 +718,12 @@ int pack_signal_tune(uint32_t grid, bool bench_signal) {
   return DORA_OK;
 }
 
+// Workgroup cap of the command processor's packs (0: the default, 3584).
+int pack_cp_grid_tune(uint32_t grid) {
+  g_cp_grid.store(grid ? grid : 3584u);
+  return DORA_OK;
+}
+
 int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
   if (!len) return DORA_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,

@@ -28,6 +28,7 @@ int launch_l2_touch(const void* p, size_t len, hipStream_t stream);
 int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks);
 int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
 int pack_signal_tune(uint32_t grid, bool bench_signal);
+int pack_cp_grid_tune(uint32_t grid);
 }  // namespace dora
 
 namespace dora {
@@ -82,6 +83,8 @@ int dora_gpu_test_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
 int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal) {
   return dora::pack_signal_tune(grid, bench_signal != 0);
 }
+
+int dora_gpu_test_cp_grid(uint32_t grid) { return dora::pack_cp_grid_tune(grid); }
 
 int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
                              const uint64_t* dsts, const uint64_t* dst_caps,

@@ -23,6 +23,9 @@ int dora_gpu_test_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
  * launch, which then strides over the chunks (0: up to 4096).  With `bench_signal`,
  * dora_gpu_pack signals a scratch flag too (microbenchmarks). */
 int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal);
+/* Workgroup cap of packs the command processor signals (0: the default, 3584; a pack has at most
+ * one workgroup per chunk). */
+int dora_gpu_test_cp_grid(uint32_t grid);
 
 /* Test tool (no reference counterpart): one workgroup per CU reads all of [data, data + len)
  * with plain cached loads, leaving the lines in every XCD's L2 (the acquire-fence negative

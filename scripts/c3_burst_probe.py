@@ -4,7 +4,10 @@ burst) `--reps` times in one dataflow, printing per rep the burst's send-call ti
 and fraction of HBM; with DORA_GPU_TRACE=subphases the sender's host sub-phases follow at exit.
 Diagnoses the burst's host stall with CP-signalled multi-segment packs.
 
-    python scripts/c3_burst_probe.py --reps 3
+    python scripts/c3_burst_probe.py --reps 3 [--grids 3584,1024,512]
+
+With --grids, every rep runs once per workgroup cap of the command processor's packs
+(dora_gpu_test_cp_grid: C3's clouds are CP-signalled), interleaved.
 """
 import argparse
 import json
@@ -19,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--steady", type=int, default=200)
+    ap.add_argument("--grids", default="0", help="CP grid caps to interleave (0: the default)")
     a = ap.parse_args()
     import bench
     from dora_amd import device
@@ -40,14 +44,19 @@ def main():
         def wait_ack(s, timeout=60.0):
             node.wait_input("ack", "seq", s, timeout)
 
-        for r in range(a.reps):
+        from dora_amd._lib import call
+        grids = [int(x) for x in a.grids.split(",")]
+        for r, g in [(r, g) for r in range(a.reps) for g in grids]:
+            call("dora_gpu_test_cp_grid", g)
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
-            print(json.dumps({"rep": r, 
+            print(json.dumps({"rep": r, "cp_grid": g,
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
+                              "us_per_cloud": c3["roofline"]["device_us_per_launch"],
                               "send_calls_us": c3["send_calls_us"],
-                              "pack_starts_us": [x for x, _ in c3["pack_intervals_us"]],
+                              "pack_intervals_us": c3["pack_intervals_us"],
                               "cp_signalled": device.aql_cp_signalled(0)}), flush=True)
+        call("dora_gpu_test_cp_grid", 0)
         stream.close()
         node.close()
         df.wait(60)
