@@ -166,6 +166,36 @@ PyObject* py_send_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return PyLong_FromLong(rc);
 }
 
+// send_buffer(handle, output_id, buffer, metadata) -> status: host bytes (any object with the
+// buffer protocol: bytes, bytearray, memoryview, numpy) as send_output_bytes of a host source,
+// read in place — the call copies them (inline below 4096 B, else into a slot) before it returns
+PyObject* py_send_buffer(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "send_buffer(handle, output_id, buffer, metadata)");
+    return nullptr;
+  }
+  void* h = nullptr;
+  if (!as_ptr(args[0], &h)) return nullptr;
+  const char* oid = as_cstr(args[1]);
+  if (!oid) return nullptr;
+  Py_buffer view;
+  if (PyObject_GetBuffer(args[2], &view, PyBUF_C_CONTIGUOUS) != 0) return nullptr;
+  std::string& params = t_params;
+  if (!encode(args[3], params)) {
+    PyBuffer_Release(&view);
+    return nullptr;
+  }
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = dora_node_send_output_bytes_ex(static_cast<dora_node*>(h), oid, view.buf,
+                                      static_cast<size_t>(view.len), ARROW_DEVICE_CPU,
+                                      reinterpret_cast<const uint8_t*>(params.data()),
+                                      params.size(), 0);
+  Py_END_ALLOW_THREADS
+  PyBuffer_Release(&view);
+  return PyLong_FromLong(rc);
+}
+
 // send_array(handle, output_id, array_addr, schema_addr, device_type, metadata[, flags])
 PyObject* py_send_array(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   if (nargs != 6 && nargs != 7) {
@@ -200,6 +230,8 @@ PyMethodDef methods[] = {
      METH_FASTCALL, "MetadataParameters bytes of a dict (bool / int / str, else str(v))."},
     {"send_bytes", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_bytes)),
      METH_FASTCALL, "dora_node_send_output_bytes with parameters encoded from a dict."},
+    {"send_buffer", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_buffer)),
+     METH_FASTCALL, "dora_node_send_output_bytes of host bytes read in place (buffer protocol)."},
     {"send_array", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_array)),
      METH_FASTCALL, "dora_node_send_output with parameters encoded from a dict."},
     {nullptr, nullptr, 0, nullptr}};

@@ -161,9 +161,8 @@ class Node:
             a, s = data.send_addrs()
             rc = _fast.send_array(self.handle, output_id, a, s, ARROW_DEVICE_ROCM, metadata, f)
         elif isinstance(data, (bytes, bytearray, memoryview)):
-            buf = ctypes.create_string_buffer(bytes(data), len(data))
-            rc = _fast.send_bytes(self.handle, output_id, ctypes.addressof(buf), len(data),
-                                  ARROW_DEVICE_CPU, metadata)
+            # read in place; the call copies them before it returns (inline below 4096 B)
+            rc = _fast.send_buffer(self.handle, output_id, data, metadata)
         elif isinstance(data, DeviceBuffer):
             rc = _fast.send_bytes(self.handle, output_id, data.ptr, data.size, ARROW_DEVICE_ROCM,
                                   metadata, f)
