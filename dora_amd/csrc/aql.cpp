@@ -1171,6 +1171,31 @@ int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
   return DORA_OK;
 }
 
+uint64_t aql_gpu_tick_to_realtime_ns(int device, uint64_t tick) {
+  AqlQueue* a = aql_queue(device);
+  if (!a || !a->ts_freq) return 0;
+  static std::once_flag once;
+  static double off_ns = 0;  // CLOCK_REALTIME - HSA system clock, ns
+  const double sys_ns = 1e9 / double(a->ts_freq);
+  std::call_once(once, [&] {
+    uint64_t best = ~uint64_t(0);
+    for (int i = 0; i < 16; ++i) {
+      uint64_t sys = 0;
+      const uint64_t r0 = now_ns();
+      hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &sys);
+      const uint64_t r1 = now_ns();
+      if (r1 - r0 < best) {
+        best = r1 - r0;
+        off_ns = double(r0 / 2 + r1 / 2) - double(sys) * sys_ns;
+      }
+    }
+  });
+  uint64_t sys = 0;
+  if (hsa_amd_profiling_convert_tick_to_system_domain(a->gpu, tick, &sys) != HSA_STATUS_SUCCESS)
+    return 0;
+  return uint64_t(double(sys) * sys_ns + off_ns);
+}
+
 int aql_profile_enable(AqlQueue* a, bool on) {
   if (!a) return DORA_OK;
   std::lock_guard<std::mutex> g(a->mu);

@@ -73,6 +73,11 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
                        double* us_per_msg);
 // Packs signalled by the command processor (cp_signal_window, aql.cpp).
 uint64_t aql_cp_signalled(int device);
+// A pack's own GPU stamp (s_memrealtime ticks) as CLOCK_REALTIME ns, for the message trace
+// (DORA_GPU_TRACE): the HSA runtime maps GPU ticks to its system clock, whose offset from
+// CLOCK_REALTIME is taken once per process from the tightest of 16 bracketed samples.  0 when
+// the device has no AQL queue or the runtime cannot convert.
+uint64_t aql_gpu_tick_to_realtime_ns(int device, uint64_t tick);
 // Batch packs dispatched, the sends they carried, and sends that waited in the backlog.
 int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint64_t* backlogged);
 

@@ -51,6 +51,8 @@ std::atomic<uint32_t> g_signal_grid{0};
 // rounds of 200 sends, profiles/r04_sync_ab.jsonl batches sy4-sy6; packs below 28 MiB have fewer
 // chunks than that)
 std::atomic<uint32_t> g_cp_grid{3584u};
+// workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid)
+std::atomic<uint32_t> g_cp_grid_multi{0};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
@@ -563,7 +565,11 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.nseg = static_cast<uint32_t>(n);
   a.edge_mask = edge_mask(segs, n, dst, dst_cap);
   a.n_chunks = static_cast<uint32_t>(chunks);
-  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, signal_grid_cap(sig)));
+  uint64_t grid_cap = signal_grid_cap(sig);
+  if (!sig.flag) {
+    if (const uint32_t m = g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
+  }
+  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, grid_cap));
   a.flag = sig.flag;
   a.done = sig.done;
   a.epoch = sig.epoch;
@@ -721,6 +727,12 @@ int pack_signal_tune(uint32_t grid, bool bench_signal) {
 // Workgroup cap of the command processor's packs (0: the default, 3584).
 int pack_cp_grid_tune(uint32_t grid) {
   g_cp_grid.store(grid ? grid : 3584u);
+  return DORA_OK;
+}
+
+// Workgroup cap of the command processor's multi-segment packs (0: the same as single-segment).
+int pack_cp_grid_multi_tune(uint32_t grid) {
+  g_cp_grid_multi.store(grid);
   return DORA_OK;
 }
 

@@ -190,7 +190,12 @@ constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
 // dropped one, 0-5 per bench run in the throughput ladders.  A cap of 10 instead cost 4 MB
 // sends ~6 %: 1.56-1.63 vs 1.41-1.50 us, profiles/r04_cap_ab.jsonl.)  DORA_GPU_MAX_IN_FLIGHT=N
 // sets both, `S:L` each.
+std::atomic<long> g_in_flight_small{0}, g_in_flight_big{0};  // test overrides (0: none)
+
 size_t max_in_flight(uint64_t len) {
+  if (const long o = (len < kSmallInFlightBytes ? g_in_flight_small : g_in_flight_big)
+                         .load(std::memory_order_relaxed))
+    return static_cast<size_t>(o);
   static const std::pair<long, long> env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
     if (!e) return std::make_pair(0L, 0L);
@@ -203,6 +208,17 @@ size_t max_in_flight(uint64_t len) {
   if (v > 0) return static_cast<size_t>(v);
   return len < kSmallInFlightBytes ? 11 : 8;
 }
+
+}  // namespace
+
+// The in-flight caps below / from 8 MiB (0: DORA_GPU_MAX_IN_FLIGHT or the defaults), for the
+// test library's dora_gpu_test_in_flight.
+void set_in_flight_caps(long small, long big) {
+  g_in_flight_small.store(small);
+  g_in_flight_big.store(big);
+}
+
+namespace {
 
 // Streams the HIP-launched fills of a node rotate over (host sources, compacting transforms,
 // relays; device-source packs go to the AQL queues, aql.h).  A pack ends in a drain tail (its
@@ -1330,9 +1346,12 @@ void finish_input(dora_node* n, dora_event* ev) {
       const FillFlag& ff = h->nodes[d.flag_node].fill[d.flag_index];
       if (ff.epoch.load(std::memory_order_acquire) == d.epoch &&
           ff.cp_epoch.load(std::memory_order_acquire) != d.epoch) {
+        // on the host's clock when the HSA runtime can map GPU ticks (aql.h), else GPU ns
+        const uint64_t s0 = aql_gpu_tick_to_realtime_ns(n->core->device, ff.t_start);
+        const uint64_t s1 = aql_gpu_tick_to_realtime_ns(n->core->device, ff.t_end);
         const double ns_per_tick = 1e9 / kRealtimeHz;
-        trace_at(TP_GPU_START, in->token, uint64_t(double(ff.t_start) * ns_per_tick));
-        trace_at(TP_GPU_SIGNAL, in->token, uint64_t(double(ff.t_end) * ns_per_tick));
+        trace_at(TP_GPU_START, in->token, s0 ? s0 : uint64_t(double(ff.t_start) * ns_per_tick));
+        trace_at(TP_GPU_SIGNAL, in->token, s1 ? s1 : uint64_t(double(ff.t_end) * ns_per_tick));
       }
     }
   } else if (d.fill == FILL_EVENT) {

@@ -23,8 +23,8 @@ enum TracePoint : uint8_t {
   TP_POPPED,           // receiver: event popped from the ring
   TP_FILLED,           // receiver: fill observed complete
   TP_RELEASED,         // receiver: drop token reported
-  TP_GPU_START,        // receiver: the pack's first workgroup started (GPU clock, ns)
-  TP_GPU_SIGNAL,       // receiver: the pack signalled its fill (GPU clock, ns)
+  TP_GPU_START,        // receiver: the pack's first workgroup started (host clock via HSA)
+  TP_GPU_SIGNAL,       // receiver: the pack signalled its fill (host clock via HSA)
 };
 
 bool trace_enabled();

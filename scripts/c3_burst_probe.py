@@ -7,7 +7,9 @@ Diagnoses the burst's host stall with CP-signalled multi-segment packs (DESIGN Â
     python scripts/c3_burst_probe.py --reps 3 [--grids 3584,1024,512]
 
 With --grids, every rep runs once per workgroup cap of the command processor's packs
-(dora_gpu_test_cp_grid: C3's clouds are CP-signalled), interleaved.
+(dora_gpu_test_cp_grid: C3's clouds are CP-signalled), interleaved; --multi-grids caps only the
+multi-segment ones (dora_gpu_test_cp_grid_multi) and --caps sets the sender's in-flight cap
+from 8 MiB (dora_gpu_test_in_flight); every combination runs once per rep.
 """
 import argparse
 import json
@@ -23,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--steady", type=int, default=200)
     ap.add_argument("--grids", default="0", help="CP grid caps to interleave (0: the default)")
+    ap.add_argument("--multi-grids", default="0", help="multi-segment CP grid caps (0: --grids)")
+    ap.add_argument("--caps", default="0", help="in-flight caps from 8 MiB (0: the default, 8)")
     a = ap.parse_args()
     import bench
     from dora_amd import device
@@ -46,10 +50,15 @@ def main():
 
         from dora_amd._lib import call
         grids = [int(x) for x in a.grids.split(",")]
-        for r, g in [(r, g) for r in range(a.reps) for g in grids]:
+        multis = [int(x) for x in a.multi_grids.split(",")]
+        caps = [int(x) for x in a.caps.split(",")]
+        combos = [(r, g, m, c) for r in range(a.reps) for g in grids for m in multis for c in caps]
+        for r, g, m, c in combos:
             call("dora_gpu_test_cp_grid", g)
+            call("dora_gpu_test_cp_grid_multi", m)
+            call("dora_gpu_test_in_flight", 0, c)
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
-            print(json.dumps({"rep": r, "cp_grid": g,
+            print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "big_cap": c,
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
                               "us_per_cloud": c3["roofline"]["device_us_per_launch"],
@@ -57,6 +66,8 @@ def main():
                               "pack_intervals_us": c3["pack_intervals_us"],
                               "cp_signalled": device.aql_cp_signalled(0)}), flush=True)
         call("dora_gpu_test_cp_grid", 0)
+        call("dora_gpu_test_cp_grid_multi", 0)
+        call("dora_gpu_test_in_flight", 0, 0)
         stream.close()
         node.close()
         df.wait(60)
