@@ -53,6 +53,8 @@ std::atomic<uint32_t> g_signal_grid{0};
 std::atomic<uint32_t> g_cp_grid{3584u};
 // workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid)
 std::atomic<uint32_t> g_cp_grid_multi{0};
+// the same for such a pack dispatched with every queue idle (0: g_cp_grid_multi)
+std::atomic<uint32_t> g_cp_grid_multi_lone{0};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
@@ -541,7 +543,7 @@ uint64_t signal_grid_cap(const FillSignal& sig) {
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid_out, uint64_t dst_cap) {
+                   uint8_t* out, size_t cap, uint32_t* grid_out, uint64_t dst_cap, bool lone) {
   if (n == 0 || n > size_t(kMaxAqlSegs)) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   if (cap < sizeof(AqlPackArgs)) return fail(DORA_ERR_INVALID, "AQL pack: argument buffer");
   AqlPackArgs a;
@@ -567,7 +569,8 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.n_chunks = static_cast<uint32_t>(chunks);
   uint64_t grid_cap = signal_grid_cap(sig);
   if (!sig.flag) {
-    if (const uint32_t m = g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
+    const uint32_t l = lone ? g_cp_grid_multi_lone.load(std::memory_order_relaxed) : 0u;
+    if (const uint32_t m = l ? l : g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
   }
   a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, grid_cap));
   a.flag = sig.flag;
@@ -731,8 +734,9 @@ int pack_cp_grid_tune(uint32_t grid) {
 }
 
 // Workgroup cap of the command processor's multi-segment packs (0: the same as single-segment).
-int pack_cp_grid_multi_tune(uint32_t grid) {
+int pack_cp_grid_multi_tune(uint32_t grid, uint32_t lone_grid) {
   g_cp_grid_multi.store(grid);
+  g_cp_grid_multi_lone.store(lone_grid);
   return DORA_OK;
 }
 
