@@ -188,7 +188,7 @@ _TEST_SIGS = {
     "dora_gpu_test_pack_signal_tune": (c_int, [ctypes.c_uint32, c_int]),
     "dora_gpu_test_pack_tune": (c_int, [c_int, c_int, ctypes.c_uint32]),
     "dora_gpu_test_cp_grid": (c_int, [ctypes.c_uint32]),
-    "dora_gpu_test_cp_grid_multi": (c_int, [ctypes.c_uint32, ctypes.c_uint32]),
+    "dora_gpu_test_cp_grid_multi": (c_int, [ctypes.c_uint32]),
     "dora_gpu_test_in_flight": (c_int, [ctypes.c_long, ctypes.c_long]),
     "dora_gpu_test_l2_touch": (c_int, [c_void_p, c_size_t, c_void_p]),
     "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),

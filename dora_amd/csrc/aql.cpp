@@ -41,7 +41,7 @@ namespace dora {
 
 // kernels.hip: the AQL kernels' argument block for `n` segments (<= aql_max_segments()).
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid, uint64_t dst_cap, bool lone);
+                   uint8_t* out, size_t cap, uint32_t* grid, uint64_t dst_cap);
 size_t aql_args_size();
 int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint8_t* out,
                     uint32_t* grid);
@@ -537,12 +537,11 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
     // no flag, done words non-null: per-wave store waits; `epoch` carries the stamp area
     const FillSignal per_wave{nullptr, reinterpret_cast<uintptr_t>(it0.cp_stamps), sig.done};
     rc = one ? build_aql_args1(segs[0], dst, per_wave, args, &grid)
-             : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, it0.dst_cap,
-                              it0.lone);
+             : build_aql_args(segs, it0.n, dst, per_wave, args, sizeof(args), &grid, it0.dst_cap);
   } else if (one) {
     rc = build_aql_args1(segs[0], dst, sig, args, &grid);
   } else {
-    rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, it0.dst_cap, it0.lone);
+    rc = build_aql_args(segs, it0.n, dst, sig, args, sizeof(args), &grid, it0.dst_cap);
   }
   if (rc != DORA_OK) return rc;
   hsa_signal_t done{0};

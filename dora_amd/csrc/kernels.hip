@@ -51,10 +51,12 @@ std::atomic<uint32_t> g_signal_grid{0};
 // rounds of 200 sends, profiles/r04_sync_ab.jsonl batches sy4-sy6; packs below 28 MiB have fewer
 // chunks than that)
 std::atomic<uint32_t> g_cp_grid{3584u};
-// workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid)
-std::atomic<uint32_t> g_cp_grid_multi{0};
-// the same for such a pack dispatched with every queue idle (0: g_cp_grid_multi)
-std::atomic<uint32_t> g_cp_grid_multi_lone{0};
+// workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid).  Such
+// packs (C3's 13 MB clouds) run up to four at once, one per queue: 640 workgroups each (2.5 per
+// CU) against the single-segment cap of 3584, C3's 20-cloud burst 0.69-0.72 -> 0.73-0.75 and its
+// 200-cloud steady state 0.71-0.72 -> 0.77-0.79 of HBM (caps 512-1536 interleaved over four
+// boxes, profiles/r05_c3_cp_grid_b.jsonl, r05_c3_multi_grid_*.jsonl)
+std::atomic<uint32_t> g_cp_grid_multi{640};
 std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
 
 // Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
@@ -543,7 +545,7 @@ uint64_t signal_grid_cap(const FillSignal& sig) {
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
 int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
-                   uint8_t* out, size_t cap, uint32_t* grid_out, uint64_t dst_cap, bool lone) {
+                   uint8_t* out, size_t cap, uint32_t* grid_out, uint64_t dst_cap) {
   if (n == 0 || n > size_t(kMaxAqlSegs)) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   if (cap < sizeof(AqlPackArgs)) return fail(DORA_ERR_INVALID, "AQL pack: argument buffer");
   AqlPackArgs a;
@@ -569,8 +571,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.n_chunks = static_cast<uint32_t>(chunks);
   uint64_t grid_cap = signal_grid_cap(sig);
   if (!sig.flag) {
-    const uint32_t l = lone ? g_cp_grid_multi_lone.load(std::memory_order_relaxed) : 0u;
-    if (const uint32_t m = l ? l : g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
+    if (const uint32_t m = g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
   }
   a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, grid_cap));
   a.flag = sig.flag;
@@ -733,10 +734,9 @@ int pack_cp_grid_tune(uint32_t grid) {
   return DORA_OK;
 }
 
-// Workgroup cap of the command processor's multi-segment packs (0: the same as single-segment).
-int pack_cp_grid_multi_tune(uint32_t grid, uint32_t lone_grid) {
-  g_cp_grid_multi.store(grid);
-  g_cp_grid_multi_lone.store(lone_grid);
+// Workgroup cap of the command processor's multi-segment packs (0: the default, 640).
+int pack_cp_grid_multi_tune(uint32_t grid) {
+  g_cp_grid_multi.store(grid ? grid : 640u);
   return DORA_OK;
 }
 

@@ -29,7 +29,7 @@ int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, u
 int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
 int pack_signal_tune(uint32_t grid, bool bench_signal);
 int pack_cp_grid_tune(uint32_t grid);
-int pack_cp_grid_multi_tune(uint32_t grid, uint32_t lone_grid);
+int pack_cp_grid_multi_tune(uint32_t grid);
 // node.cpp
 void set_in_flight_caps(long small, long big);
 }  // namespace dora
@@ -89,9 +89,7 @@ int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal) {
 
 int dora_gpu_test_cp_grid(uint32_t grid) { return dora::pack_cp_grid_tune(grid); }
 
-int dora_gpu_test_cp_grid_multi(uint32_t grid, uint32_t lone_grid) {
-  return dora::pack_cp_grid_multi_tune(grid, lone_grid);
-}
+int dora_gpu_test_cp_grid_multi(uint32_t grid) { return dora::pack_cp_grid_multi_tune(grid); }
 
 int dora_gpu_test_in_flight(long small, long big) {
   if (small < 0 || big < 0) return dora::fail(DORA_ERR_INVALID, "negative in-flight cap");

@@ -26,9 +26,8 @@ int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal);
 /* Workgroup cap of packs the command processor signals (0: the default, 3584; a pack has at most
  * one workgroup per chunk). */
 int dora_gpu_test_cp_grid(uint32_t grid);
-/* Workgroup cap of multi-segment packs the command processor signals (0: the default), and of
- * such packs dispatched while every queue is idle (0: as the others). */
-int dora_gpu_test_cp_grid_multi(uint32_t grid, uint32_t lone_grid);
+/* Workgroup cap of multi-segment packs the command processor signals (0: the default, 640). */
+int dora_gpu_test_cp_grid_multi(uint32_t grid);
 /* Samples a sender of this process may have in flight below / from 8 MiB before an allocation
  * waits for a returned token (0: DORA_GPU_MAX_IN_FLIGHT or the defaults 11 / 8). */
 int dora_gpu_test_in_flight(long small, long big);

@@ -25,9 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--steady", type=int, default=200)
     ap.add_argument("--grids", default="0", help="CP grid caps to interleave (0: the default)")
-    ap.add_argument("--multi-grids", default="0", help="multi-segment CP grid caps (0: --grids)")
-    ap.add_argument("--lone-grids", default="0",
-                    help="multi-segment CP grid caps with every queue idle (0: --multi-grids)")
+    ap.add_argument("--multi-grids", default="0", help="multi-segment CP grid caps (0: the default, 640)")
     ap.add_argument("--caps", default="0", help="in-flight caps from 8 MiB (0: the default, 8)")
     a = ap.parse_args()
     import bench
@@ -54,16 +52,13 @@ def main():
         grids = [int(x) for x in a.grids.split(",")]
         multis = [int(x) for x in a.multi_grids.split(",")]
         caps = [int(x) for x in a.caps.split(",")]
-        lones = [int(x) for x in a.lone_grids.split(",")]
-        combos = [(r, g, m, lo, c) for r in range(a.reps) for g in grids for m in multis
-                  for lo in lones for c in caps]
-        for r, g, m, lo, c in combos:
+        combos = [(r, g, m, c) for r in range(a.reps) for g in grids for m in multis for c in caps]
+        for r, g, m, c in combos:
             call("dora_gpu_test_cp_grid", g)
-            call("dora_gpu_test_cp_grid_multi", m, lo)
+            call("dora_gpu_test_cp_grid_multi", m)
             call("dora_gpu_test_in_flight", 0, c)
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
-            print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "lone_grid": lo,
-                              "big_cap": c,
+            print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "big_cap": c,
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
                               "us_per_cloud": c3["roofline"]["device_us_per_launch"],
@@ -71,7 +66,7 @@ def main():
                               "pack_intervals_us": c3["pack_intervals_us"],
                               "cp_signalled": device.aql_cp_signalled(0)}), flush=True)
         call("dora_gpu_test_cp_grid", 0)
-        call("dora_gpu_test_cp_grid_multi", 0, 0)
+        call("dora_gpu_test_cp_grid_multi", 0)
         call("dora_gpu_test_in_flight", 0, 0)
         stream.close()
         node.close()

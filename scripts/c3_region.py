@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--kernel", default="dora_aql_pack_u4")
     ap.add_argument("--size", type=int, default=C3_BYTES)
     ap.add_argument("--line", help="the bench.py stdout line of the same run (its c3 block)")
+    ap.add_argument("--detail", help="the bench.py detail file of the same run: its burst's pack "
+                    "intervals from the packs' own stamps, compared pack by pack with the trace")
     a = ap.parse_args()
     f = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(a.kernel)]
@@ -79,6 +81,23 @@ def main():
             out["burst_span_vs_line"] = round(out["burst"]["frac_span"] / c3["frac"], 4)
         if c3.get("steady_frac"):
             out["steady_span_vs_line"] = round(out["steady"]["frac_span"] / c3["steady_frac"], 4)
+    if a.detail:
+        # the packs' own stamps (first workgroup start -> last workgroup end, relative to the
+        # burst's first start) against the trace's packet intervals (command-processor start ->
+        # end of pipe), both aligned on the burst's first pack
+        st = json.load(open(a.detail)).get("c3", {}).get("pack_intervals_us") or []
+        if len(st) == len(burst):
+            t0 = burst[0][0]
+            tr = [((x - t0) / 1000.0, (y - t0) / 1000.0) for x, y in sorted(burst)]
+            st = sorted(st)
+            d_start = [t[0] - s_[0] for t, s_ in zip(tr, st)]
+            d_end = [t[1] - s_[1] for t, s_ in zip(tr, st)]
+            out["trace_minus_stamps_us"] = {
+                "start_median": round(statistics.median(d_start), 3),
+                "end_median": round(statistics.median(d_end), 3),
+                "last_end": round(tr[-1][1] - max(e for _, e in st), 3),
+                "span_trace": round(max(e for _, e in tr), 3),
+                "span_stamps": round(max(e for _, e in st), 3)}
     print(json.dumps(out))
 
 
