@@ -53,7 +53,7 @@ std::atomic<uint32_t> g_signal_grid{0};
 std::atomic<uint32_t> g_cp_grid{3584u};
 // workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid).  Such
 // packs (C3's 13 MB clouds) run up to four at once, one per queue: 640 workgroups each (2.5 per
-// CU) against the single-segment cap of 3584, C3's 20-cloud burst 0.69-0.72 -> 0.73-0.75 and its
+// CU) against the single-segment cap of 3584, C3's 20-cloud burst 0.67-0.72 -> 0.72-0.75 and its
 // 200-cloud steady state 0.71-0.72 -> 0.77-0.79 of HBM (caps 512-1536 interleaved over four
 // boxes, profiles/r05_c3_cp_grid_b.jsonl, r05_c3_multi_grid_*.jsonl)
 std::atomic<uint32_t> g_cp_grid_multi{640};
