@@ -122,9 +122,25 @@ constexpr uint64_t kBarrierBytes = uint64_t(8) << 20;
 constexpr size_t kDepth = 2, kCpDepth = 3;
 constexpr uint64_t kBatchBytes = uint64_t(32) << 20;
 
+// Publish an AQL packet whose body is written: its header last, then the doorbell.  In the
+// default packet ring (coherent system memory, x86 TSO) program order suffices.  A ring the
+// runtime put in device memory behind the PCIe BAR (HSA_ALLOCATE_QUEUE_DEV_MEM=1) is
+// write-combined, where x86 keeps no store order: fences put the body ahead of the header and
+// the header ahead of the doorbell.  (That placement was measured and is not recommended: the
+// synchronous 40.96 MB send gains ~1 us, pipelined sends lose 10-40 % to the fenced BAR writes,
+// DESIGN §9.1.)
+inline void publish_packet(hsa_queue_t* q, void* p, uint32_t header_setup, uint64_t idx,
+                           bool wc_ring) {
+  if (wc_ring) __builtin_ia32_sfence();
+  __atomic_store_n(reinterpret_cast<uint32_t*>(p), header_setup, __ATOMIC_RELEASE);
+  if (wc_ring) __builtin_ia32_sfence();
+  hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+}
+
 struct AqlQueue {
   std::mutex mu;
   hsa_agent_t gpu{};
+  bool wc_ring = true;  // packet rings not (known to be) in system memory: fenced publication
   // Packs rotate over these hardware queues: one queue overlaps consecutive packs only partly
   // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl),
   // and the command processor's per-queue dispatch rate bounds a pipeline of <= 8 messages in
@@ -350,6 +366,15 @@ AqlQueue* create(int device) {
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
       break;
     a->nq = i + 1;
+  }
+  // where the runtime put the packet rings (system memory unless HSA_ALLOCATE_QUEUE_DEV_MEM)
+  if (a->nq > 0) {
+    hsa_amd_pointer_info_t pi{};
+    pi.size = sizeof(pi);
+    if (hsa_amd_pointer_info(a->qs[0]->base_address, &pi, nullptr, nullptr, nullptr) ==
+            HSA_STATUS_SUCCESS &&
+        pi.type != HSA_EXT_POINTER_TYPE_UNKNOWN && pi.agentOwner.handle == f.cpu.handle)
+      a->wc_ring = false;
   }
   if (a->nq == 0) {
     hsa_amd_memory_pool_free(ring);
@@ -646,9 +671,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
                            << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
-                   __ATOMIC_RELEASE);
-  hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+  publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
   // every message of a batch signals at its end: the last one's flag stands for the packet
   u.flag = items[n - 1].flag_host;
   u.epoch = items[n - 1].sig.epoch;
@@ -898,6 +921,13 @@ size_t aql_kernel_count() { return kKernels; }
 
 const char* aql_kernel_name(size_t k) { return k < size_t(kKernels) ? kKernelNames[k] : nullptr; }
 
+int aql_ring_write_combined(int device, bool* wc) {
+  AqlQueue* a = aql_queue(device);
+  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
+  *wc = a->wc_ring;
+  return DORA_OK;
+}
+
 int aql_hold(int device, bool hold) {
   AqlQueue* a = aql_queue(device);
   if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
@@ -1068,9 +1098,7 @@ int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int de
                                << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                               (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
       const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-      __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
-                       __ATOMIC_RELEASE);
-      hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+      publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
       oq.push_back({sl, epoch});
     }
     for (auto& oq : outq) {
@@ -1156,9 +1184,7 @@ int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
                           (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  __atomic_store_n(reinterpret_cast<uint32_t*>(p), header | (uint32_t(setup) << 16),
-                   __ATOMIC_RELEASE);
-  hsa_signal_store_relaxed(q->doorbell_signal, hsa_signal_value_t(idx));
+  publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
   ++a->dispatched[k];
   if (hsa_signal_wait_scacquire(a->reduce_sig, HSA_SIGNAL_CONDITION_LT, 1,
                                 uint64_t(5) * 1000000000ull, HSA_WAIT_STATE_ACTIVE) != 0) {

@@ -147,6 +147,14 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
+int dora_gpu_test_aql_ring_wc(int device, int* wc) {
+  if (!wc) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  bool b = true;
+  const int rc = dora::aql_ring_write_combined(device, &b);
+  *wc = b ? 1 : 0;
+  return rc;
+}
+
 int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks, int* rank) {
   if (!buf || !nranks || !rank) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN

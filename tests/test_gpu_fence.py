@@ -165,3 +165,18 @@ def test_rewritten_sources_across_dispatches_bit_exact(writer):
     # the fenceless coherent kernel packed them all, through more dispatches than ring slots
     assert used.get("dora_aql_pack1c_u4", 0) >= trials, used
     assert sum(used.values()) > RING_SLOTS, used
+
+
+def test_packet_rings_in_system_memory_publish_unfenced():
+    """The AQL packet rings (aql.cpp publish_packet): ROCr puts them in coherent system memory by
+    default, where a packet's header store needs no fence after its body (x86 TSO); a ring the
+    runtime placed in device memory (HSA_ALLOCATE_QUEUE_DEV_MEM=1, write-combined through the
+    BAR) is published with store fences.  The placement is read back from the runtime."""
+    import ctypes
+    import os
+
+    from dora_amd._lib import call
+    wc = ctypes.c_int(-1)
+    call("dora_gpu_test_aql_ring_wc", 0, ctypes.byref(wc))
+    dev_ring = os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM", "0") not in ("", "0")
+    assert wc.value == (1 if dev_ring else 0), (wc.value, dev_ring)
