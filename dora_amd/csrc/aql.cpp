@@ -140,7 +140,8 @@ inline void publish_packet(hsa_queue_t* q, void* p, uint32_t header_setup, uint6
 struct AqlQueue {
   std::mutex mu;
   hsa_agent_t gpu{};
-  bool wc_ring = true;  // packet rings not (known to be) in system memory: fenced publication
+  bool wc_ring = false;  // packet rings in device memory (write-combined): fenced publication
+  int ring_where = 0;    // diagnostics: pointer type * 4 + owner (1 CPU agent, 2 this GPU, 3 other)
   // Packs rotate over these hardware queues: one queue overlaps consecutive packs only partly
   // (4 MB: 3.6 us per pack back to back on one queue, 1.9 on two; profiles/r01_aql_probe.jsonl),
   // and the command processor's per-queue dispatch rate bounds a pipeline of <= 8 messages in
@@ -367,14 +368,20 @@ AqlQueue* create(int device) {
       break;
     a->nq = i + 1;
   }
-  // where the runtime put the packet rings (system memory unless HSA_ALLOCATE_QUEUE_DEV_MEM)
+  // where the runtime put the packet rings: system memory unless HSA_ALLOCATE_QUEUE_DEV_MEM,
+  // which allocates them from this GPU's memory (owner: the GPU agent)
   if (a->nq > 0) {
     hsa_amd_pointer_info_t pi{};
     pi.size = sizeof(pi);
     if (hsa_amd_pointer_info(a->qs[0]->base_address, &pi, nullptr, nullptr, nullptr) ==
-            HSA_STATUS_SUCCESS &&
-        pi.type != HSA_EXT_POINTER_TYPE_UNKNOWN && pi.agentOwner.handle == f.cpu.handle)
-      a->wc_ring = false;
+        HSA_STATUS_SUCCESS) {
+      const int owner = pi.agentOwner.handle == f.cpu.handle   ? 1
+                        : pi.agentOwner.handle == f.gpu.handle ? 2
+                        : pi.agentOwner.handle                  ? 3
+                                                                : 0;
+      a->ring_where = int(pi.type) * 4 + owner;
+      a->wc_ring = owner == 2;
+    }
   }
   if (a->nq == 0) {
     hsa_amd_memory_pool_free(ring);
@@ -921,10 +928,11 @@ size_t aql_kernel_count() { return kKernels; }
 
 const char* aql_kernel_name(size_t k) { return k < size_t(kKernels) ? kKernelNames[k] : nullptr; }
 
-int aql_ring_write_combined(int device, bool* wc) {
+int aql_ring_write_combined(int device, bool* wc, int* where) {
   AqlQueue* a = aql_queue(device);
   if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
   *wc = a->wc_ring;
+  if (where) *where = a->ring_where;
   return DORA_OK;
 }
 

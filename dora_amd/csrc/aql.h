@@ -67,8 +67,9 @@ uint64_t aql_dispatched(int device, size_t k);
 // Test tool: while held, every batchable send of this process on `device` waits in the
 // backlog; releasing dispatches the backlog as batch packs (tests/test_gpu_dataflow.py).
 int aql_hold(int device, bool hold);
-// Whether the process's packet rings are published with fences (not known to be system memory).
-int aql_ring_write_combined(int device, bool* wc);
+// Whether the process's packet rings are published with fences (in device memory), and where
+// the runtime says they are (pointer type * 4 + owner: 1 CPU agent, 2 this GPU, 3 other).
+int aql_ring_write_combined(int device, bool* wc, int* where);
 // Test hook: packs pipelined over the queues with in-kernel or command-processor completion
 // signals (dora_gpu_test_aql_pipeline).
 int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,

@@ -147,10 +147,10 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
-int dora_gpu_test_aql_ring_wc(int device, int* wc) {
+int dora_gpu_test_aql_ring_wc(int device, int* wc, int* where) {
   if (!wc) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  bool b = true;
-  const int rc = dora::aql_ring_write_combined(device, &b);
+  bool b = false;
+  const int rc = dora::aql_ring_write_combined(device, &b, where);
   *wc = b ? 1 : 0;
   return rc;
 }

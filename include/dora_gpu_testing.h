@@ -44,9 +44,10 @@ int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
  * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
  * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
 int dora_gpu_test_aql_hold(int device, int hold);
-/* Test tool: 1 if `device`'s AQL packet rings are published with store fences (the runtime put
- * them in device memory, or their placement is unknown), 0 for rings in system memory. */
-int dora_gpu_test_aql_ring_wc(int device, int* wc);
+/* Test tool: `wc` 1 if `device`'s AQL packet rings are published with store fences (the runtime
+ * put them in this GPU's memory), 0 otherwise; `where` (may be NULL): the runtime's pointer type
+ * of the ring * 4 + its owner (0 none, 1 the CPU agent, 2 this GPU, 3 another agent). */
+int dora_gpu_test_aql_ring_wc(int device, int* wc, int* where);
 /* Test tool (host only): the 640-byte argument block of a batch pack (dora_aql_packb_u4) for
  * `n_msgs` (<= 8) messages; message m has seg_counts[m] segments, given as (src, dst_off, len)
  * triples in `segs`, its slot at dsts[m] with dst_caps[m] writable bytes, and fill flag /

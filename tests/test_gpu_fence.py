@@ -176,7 +176,8 @@ def test_packet_rings_in_system_memory_publish_unfenced():
     import os
 
     from dora_amd._lib import call
-    wc = ctypes.c_int(-1)
-    call("dora_gpu_test_aql_ring_wc", 0, ctypes.byref(wc))
+    wc, where = ctypes.c_int(-1), ctypes.c_int(-1)
+    call("dora_gpu_test_aql_ring_wc", 0, ctypes.byref(wc), ctypes.byref(where))
     dev_ring = os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM", "0") not in ("", "0")
-    assert wc.value == (1 if dev_ring else 0), (wc.value, dev_ring)
+    print(f"packet ring: pointer type {where.value // 4}, owner {where.value % 4}, fenced {wc.value}")
+    assert wc.value == (1 if dev_ring else 0), (wc.value, where.value, dev_ring)
