@@ -887,12 +887,19 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   return DORA_OK;
 }
 
+namespace {
+std::atomic<bool> g_cp_lone{true};  // lone single-segment packs above the window: CP-signalled
+}  // namespace
+
+void aql_cp_lone(bool on) { g_cp_lone.store(on); }
+
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone) {
   if (n == 0) return false;
   const bool single = n == 1 && segs[0].dst_off == 0;
   uint64_t bytes = 0;
   for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
-  return bytes >= kCpLo && (bytes < kCpHi || (lone && single));
+  return bytes >= kCpLo &&
+         (bytes < kCpHi || (lone && single && g_cp_lone.load(std::memory_order_relaxed)));
 }
 
 int bar_alloc(int device, size_t bytes, void** out) {

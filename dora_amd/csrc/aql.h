@@ -67,6 +67,9 @@ uint64_t aql_dispatched(int device, size_t k);
 // Test tool: while held, every batchable send of this process on `device` waits in the
 // backlog; releasing dispatches the backlog as batch packs (tests/test_gpu_dataflow.py).
 int aql_hold(int device, bool hold);
+// Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
+// in-kernel (test hook, probes of the synchronous send).
+void aql_cp_lone(bool on);
 // Whether the process's packet rings are published with fences (in device memory), and where
 // the runtime says they are (pointer type * 4 + owner: 1 CPU agent, 2 this GPU, 3 other).
 int aql_ring_write_combined(int device, bool* wc, int* where);

@@ -147,6 +147,11 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
+int dora_gpu_test_cp_lone(int on) {
+  dora::aql_cp_lone(on != 0);
+  return DORA_OK;
+}
+
 int dora_gpu_test_aql_ring_wc(int device, int* wc, int* where) {
   if (!wc) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   bool b = false;

@@ -44,6 +44,9 @@ int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
  * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
  * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
 int dora_gpu_test_aql_hold(int device, int hold);
+/* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
+ * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
+int dora_gpu_test_cp_lone(int on);
 /* Test tool: `wc` 1 if `device`'s AQL packet rings are published with store fences (the runtime
  * put them in this GPU's memory), 0 otherwise; `where` (may be NULL): the runtime's pointer type
  * of the ring * 4 + its owner (0 none, 1 the CPU agent, 2 this GPU, 3 another agent). */
