@@ -106,6 +106,8 @@ constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4", "dora_aql_pa
 // * four HSA queues per process: 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s against
 //   two (profiles/r01_aql_queues_ab.jsonl);
 constexpr int kQueues = 4;
+// test hooks (aql_mid_queues): queues a process creates, and how many take 8-32 MiB packs
+std::atomic<int> g_create_queues{kQueues}, g_mid_queues{4};
 // * packs of [1 MiB, 32 MiB) are signalled by the command processor (the packet's completion
 //   signal, every wave waiting for its own stores), so consecutive packets of a queue overlap:
 //   4 MB over 4 queues 1.95 -> 1.59-1.64 us each (profiles/r03_aql_pipeline_probe.jsonl), C3's
@@ -362,7 +364,8 @@ AqlQueue* create(int device) {
     std::memcpy(a->ring + size_t(r) * kSlotBytes, zero.data(), kSlotBytes);
   __builtin_ia32_sfence();
   (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
-  for (int i = 0; i < kQueues; ++i) {
+  const int create_queues = std::max(1, std::min(kMaxQueues, g_create_queues.load()));
+  for (int i = 0; i < create_queues; ++i) {
     if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
       break;
@@ -514,7 +517,7 @@ namespace {
 // profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
 // the 20-cloud burst, profiles/r04_full_ab.jsonl).
 int big_queues(int nq, uint64_t bytes) {
-  return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : 4);
+  return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : g_mid_queues.load());
 }
 
 // The number of the oldest dispatch still in an outstanding list (a->next when none is).
@@ -711,13 +714,13 @@ bool queues_idle(AqlQueue* a) {
   return true;
 }
 
-// The first queue in round-robin order, among the first `nq` (0: all), with fewer than `depth`
+// The first queue in round-robin order, among the first `nq` (0: the first kQueues), with fewer than `depth`
 // outstanding packets, or -1.  An idle queue is taken without loading anything; a busy one is
 // pruned first (one load of its oldest packet's flag line, which the GPU has written since: a
 // cache miss), and only as far as needed — r03 pruned all four queues on every send.
 int pick_queue(AqlQueue* a, int nq = 0, size_t depth = 0) {
   if (a->hold) return -1;
-  if (nq <= 0 || nq > a->nq) nq = a->nq;
+  if (nq <= 0 || nq > a->nq) nq = std::min(a->nq, kQueues);
   const size_t d = depth ? depth : kDepth;
   for (int j = 0; j < nq; ++j) {
     const int i = int((a->next + uint64_t(j)) % uint64_t(nq));
@@ -892,6 +895,11 @@ std::atomic<bool> g_cp_lone{true};  // lone single-segment packs above the windo
 }  // namespace
 
 void aql_cp_lone(bool on) { g_cp_lone.store(on); }
+
+void aql_mid_queues(int create, int use) {
+  if (create > 0) g_create_queues.store(create);
+  if (use > 0) g_mid_queues.store(use);
+}
 
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone) {
   if (n == 0) return false;

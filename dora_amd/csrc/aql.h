@@ -70,6 +70,9 @@ int aql_hold(int device, bool hold);
 // Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
 // in-kernel (test hook, probes of the synchronous send).
 void aql_cp_lone(bool on);
+// Test hook: HSA queues a process creates (before its first AQL use; 0 keeps 4) and how many
+// take packs of 8-32 MiB (0 keeps 4).
+void aql_mid_queues(int create, int use);
 // Whether the process's packet rings are published with fences (in device memory), and where
 // the runtime says they are (pointer type * 4 + owner: 1 CPU agent, 2 this GPU, 3 other).
 int aql_ring_write_combined(int device, bool* wc, int* where);

@@ -147,6 +147,13 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
+int dora_gpu_test_mid_queues(int create, int use) {
+  if (create < 0 || create > 8 || use < 0 || use > 8)
+    return dora::fail(DORA_ERR_INVALID, "queues: 0..8");
+  dora::aql_mid_queues(create, use);
+  return DORA_OK;
+}
+
 int dora_gpu_test_cp_lone(int on) {
   dora::aql_cp_lone(on != 0);
   return DORA_OK;

@@ -47,6 +47,9 @@ int dora_gpu_test_aql_hold(int device, int hold);
 /* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
  * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
 int dora_gpu_test_cp_lone(int on);
+/* Test tool: the AQL queues this process creates (effective before its first AQL use; 0 keeps
+ * 4, at most 8) and how many of them take packs of 8-32 MiB in turn (0 keeps 4). */
+int dora_gpu_test_mid_queues(int create, int use);
 /* Test tool: `wc` 1 if `device`'s AQL packet rings are published with store fences (the runtime
  * put them in this GPU's memory), 0 otherwise; `where` (may be NULL): the runtime's pointer type
  * of the ring * 4 + its owner (0 none, 1 the CPU agent, 2 this GPU, 3 another agent). */

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--grids", default="0", help="CP grid caps to interleave (0: the default)")
     ap.add_argument("--multi-grids", default="0", help="multi-segment CP grid caps (0: the default, 640)")
     ap.add_argument("--caps", default="0", help="in-flight caps from 8 MiB (0: the default, 8)")
+    ap.add_argument("--mid-queues", default="0",
+                    help="queues taking 8-32 MiB packs (0: the default, 4; up to 8 are created)")
     a = ap.parse_args()
     import bench
     from dora_amd import device
@@ -39,6 +41,10 @@ def main():
          "inputs": {"throughput": {"source": "node/throughput", "queue_size": 10}},
          "env": {"DORA_BENCH_RESULT": res}},
     ]}
+    mids = [int(x) for x in a.mid_queues.split(",")]
+    from dora_amd._lib import call
+    if max(mids) > 4:
+        call("dora_gpu_test_mid_queues", max(mids), 0)  # before this process's first AQL use
     with Dataflow(desc) as df:
         node = Node("node", dataflow=df.shm, device=0)
         node.set_async_sends(True)
@@ -48,17 +54,18 @@ def main():
         def wait_ack(s, timeout=60.0):
             node.wait_input("ack", "seq", s, timeout)
 
-        from dora_amd._lib import call
         grids = [int(x) for x in a.grids.split(",")]
         multis = [int(x) for x in a.multi_grids.split(",")]
         caps = [int(x) for x in a.caps.split(",")]
-        combos = [(r, g, m, c) for r in range(a.reps) for g in grids for m in multis for c in caps]
-        for r, g, m, c in combos:
+        combos = [(r, g, m, c, q) for r in range(a.reps) for g in grids for m in multis
+                  for c in caps for q in mids]
+        for r, g, m, c, q in combos:
+            call("dora_gpu_test_mid_queues", 0, q if q else 4)
             call("dora_gpu_test_cp_grid", g)
             call("dora_gpu_test_cp_grid_multi", m)
             call("dora_gpu_test_in_flight", 0, c)
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
-            print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "big_cap": c,
+            print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "big_cap": c, "mid_queues": q,
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
                               "us_per_cloud": c3["roofline"]["device_us_per_launch"],
