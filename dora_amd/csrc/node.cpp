@@ -52,6 +52,26 @@
 
 namespace dora {
 
+// HIP's current device is per thread, and the library acts on the node's GPU from whichever
+// thread calls it — an EventStream moved to another thread (the reference's is Send), an async
+// pump, the event-stream thread: slots, IPC mappings, events and receive buffers are created on
+// the current device.  Each entry point makes the node's device current for the call and gives
+// the caller's back afterwards.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int device) {
+    int cur = -1;
+    if (device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device &&
+        hipSetDevice(device) == hipSuccess)
+      prev = cur;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 // A received slot's identity as a hash key without a heap allocation per lookup: the
 // hipIpcMemHandle_t bytes plus the owner's pid and its process-unique slot id.  The handle alone
 // is not enough: a freed slot's handle encoding can recur for a new allocation of the same size.
@@ -1535,7 +1555,10 @@ bool drain_events(dora_node* n) {
 }
 
 // The event-stream thread (dora_node::pump): drain, apply drop-oldest, wake the user thread.
+// Draining allocates receive slots, opens IPC mappings, creates events and posts broadcast
+// receives, all on the current HIP device of the calling thread: this thread's is the node's.
 void pump_main(dora_node* n) {
+  if (n->core->device >= 0) (void)hipSetDevice(n->core->device);
   while (!n->pump_stop.load(std::memory_order_acquire)) {
     bool got;
     {
@@ -2407,6 +2430,7 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
 int dora_node_sync(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return DORA_OK;
+  dora::DeviceScope ds(n->core->device);
   dora::NodeCore* c = n->core.get();
   // Kernel-signalled fills (AQL and fill streams): their flags.  A stream query or synchronise
   // would wait for HIP to notice the kernels' completion, ~100-200 us after the flags are up.
@@ -2440,6 +2464,7 @@ dora_stream_t dora_node_stream(dora_node* n) {
 
 int dora_node_allocate_data_sample(dora_node* n, size_t len, dora_sample** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   return dora::alloc_sample(n, len, out);
   DORA_GUARD_END
@@ -2463,6 +2488,7 @@ int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint
                                  dora_sample* sample) {
   if (!n || !output_id || (!type_info && type_info_len))
     return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   std::vector<uint8_t> ti(type_info, type_info + type_info_len);
   return dora::send_sample(n, output_id, ti, params, params_len, sample);
@@ -2479,6 +2505,7 @@ int dora_node_send_output_ex(dora_node* n, const char* output_id, const struct A
                              const struct ArrowSchema* schema, ArrowDeviceType device_type,
                              const uint8_t* params, size_t params_len, uint32_t flags) {
   if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   const bool device = device_type == ARROW_DEVICE_ROCM && n->core->device >= 0;
   const bool cacheable = device && !n->compact && array && schema;
@@ -2541,6 +2568,7 @@ int dora_node_send_output_bytes_ex(dora_node* n, const char* output_id, const vo
                                    size_t len, ArrowDeviceType device_type, const uint8_t* params,
                                    size_t params_len, uint32_t flags) {
   if (!n || !output_id || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   dora::SubSpan sp(dora::SP_SEND_PLAN);
   // one UInt8 buffer: the plan and its type info are built once per node and re-pointed per send
@@ -2614,6 +2642,7 @@ int dora_node_close_outputs(dora_node* n, const char* const* ids, size_t count) 
 int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   *out = nullptr;
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   const uint64_t t0 = dora::mono_ns();
   if (n->want_pump && !n->pump_on.load()) dora::start_pump(n);
@@ -2680,6 +2709,7 @@ const char* dora_event_error(const dora_event* e) { return e ? e->error.c_str() 
 int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
   if (!e || !ptr || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!e->data) return dora::fail(DORA_ERR_INVALID, "event has no data");
+  dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
   DORA_GUARD_BEGIN
   int rc = dora::ensure_local(e->data.get());
   if (rc != DORA_OK) return rc;
@@ -2697,6 +2727,7 @@ int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
   if (!e || !ti || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!e->ti_checked && e->type == DORA_EVENT_INPUT && e->data && e->data->ext_len > e->data->len) {
     // bitmaps in the sample's tail: restore the reference's inline ArrowTypeInfo bytes
+    dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
     DORA_GUARD_BEGIN
     int rc = dora::ensure_local(e->data.get());
     if (rc != DORA_OK) return rc;
@@ -2729,6 +2760,7 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
     return dora::fail(DORA_ERR_INVALID, "not an input event");
   if (!e->data->ptr && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", e->error.c_str());
+  dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
   DORA_GUARD_BEGIN
   int rc = dora::ensure_local(e->data.get());
   if (rc != DORA_OK) return rc;
@@ -2752,6 +2784,7 @@ int dora_node_forward(dora_node* n, const char* output_id, const dora_event* ev,
     return dora::fail(DORA_ERR_INVALID, "only input events can be forwarded");
   if (!ev->data->ptr && ev->data->len)
     return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", ev->error.c_str());
+  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   return dora::forward_input(n, output_id, ev, params, params_len);
   DORA_GUARD_END
