@@ -1315,3 +1315,72 @@ def test_full_size_samples_byte_identical_to_the_oracle(launcher, mode):
         assert len(b) == S
         assert b == want_c2, (off, next(i for i in range(S) if b[i] != want_c2[i]))
     assert len(c3) == len(want_c3) and c3 == bytes(want_c3)
+
+
+@pytest.mark.parametrize("event_thread", [False, True])
+def test_events_consumed_on_another_thread_bit_exact(event_thread):
+    """The node is made on this thread; its events are taken, mapped and checksummed on a
+    worker thread that never selected a HIP device — as a Rust EventStream moved to another
+    thread, or the facade's async pump (node.cpp DeviceScope: every entry point makes the node's
+    GPU current for the call).  With `event_thread` the node also drains on its event-stream
+    thread.  One GPU cannot tell devices apart; this keeps the hand-over itself exact."""
+    import ctypes
+
+    from dora_amd import _lib, device
+    from dora_amd.dataflow import daemon_spec, parse_descriptor
+    from dora_amd.device import DeviceBuffer
+    from dora_amd.node import Node
+    lib = _lib.load()
+    device.set_device(0)
+    desc = {"nodes": [{"id": "src", "outputs": ["x"]},
+                      {"id": "dst", "inputs": {"x": {"source": "src/x", "queue_size": 64}}}]}
+    shm = f"/dora-gpu-xthread-{os.getpid()}-{int(event_thread)}"
+    h = ctypes.c_void_p()
+    _lib.call("dora_daemon_create", shm.encode(), daemon_spec(parse_descriptor(desc)).encode(),
+              1 << 20, ctypes.byref(h))
+    threading.Thread(target=lambda: lib.dora_daemon_run(h.value, 120000), daemon=True).start()
+    nodes = {}
+    ts = [threading.Thread(target=lambda i=i: nodes.update({i: Node(i, dataflow=shm, device=0)}))
+          for i in ("src", "dst")]
+    [t.start() for t in ts]
+    [t.join(60) for t in ts]
+    src, dst = nodes["src"], nodes["dst"]
+    if event_thread:
+        dst.set_event_thread(True)
+    sizes = [4096, 65536, 1 << 20, 4 << 20, 13000068]
+    s = device.Stream()
+    bufs = {z: DeviceBuffer(z) for z in sizes}
+    want = {}
+    for k, z in enumerate(sizes):
+        device.fill_splitmix(bufs[z].ptr, z, 0x7E + k, s)
+        want[z] = device.csum64(bufs[z].ptr, z, s)
+    got, errors = {}, []
+
+    def consume():
+        try:
+            ws = device.Stream()  # created on this thread's current device
+            for _ in range(3 * len(sizes)):
+                ev = dst.next(timeout=30)
+                assert ev is not None and ev["type"] == "INPUT", ev
+                z = ev["metadata"]["n"]
+                got.setdefault(z, []).append(device.csum64(ev["data_ptr"], z, ws))
+                ev["value"].close()
+                ev["_event"].free()
+            ws.close()
+        except Exception as e:  # noqa: BLE001 — reported below
+            errors.append(repr(e))
+    w = threading.Thread(target=consume)
+    w.start()
+    for r in range(3):
+        for z in sizes:
+            src.send_output_device_bytes("x", bufs[z].ptr, z, {"n": z, "r": r})
+    w.join(120)
+    src.close()
+    dst.close()
+    lib.dora_daemon_free(h.value)
+    for b in bufs.values():
+        b.free()
+    s.close()
+    assert not errors, errors
+    for z in sizes:
+        assert got.get(z) == [want[z]] * 3, (z, got.get(z), want[z])
