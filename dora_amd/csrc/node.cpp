@@ -34,6 +34,7 @@
 #include <thread>
 #include <set>
 #include <sstream>
+#include <random>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -1100,7 +1101,15 @@ int allocate_host_slot(dora_node* n, uint64_t len, Slot** out) {
   s->host = true;
   s->cap = need;
   s->id = own_slots().next_id.fetch_add(1);
-  s->shm_name = "/dora-gpu-s-" + std::to_string(self_pid()) + "-" + std::to_string(s->id);
+  // pid + a per-process nonce + slot id: a receiver's cached mapping of a region is keyed by its
+  // name, so a later process that got the same pid must not produce the same names
+  static const uint32_t nonce = [] {
+    std::random_device rd;
+    return static_cast<uint32_t>(rd());
+  }();
+  char nbuf[16];
+  std::snprintf(nbuf, sizeof(nbuf), "%08x", nonce);
+  s->shm_name = "/dora-gpu-s-" + std::to_string(self_pid()) + "-" + nbuf + "-" + std::to_string(s->id);
   s->ptr = shmem_create(s->shm_name, s->cap);
   if (!s->ptr) {
     const int err = errno;
