@@ -265,6 +265,18 @@ __global__ __launch_bounds__(64) void l1_stale_kernel(const uint32_t* src, uint3
   second[b * 64 + t] = probe_load<MODE>(src + t);
 }
 
+// One resident wave that keeps the GPU from idling (a latency probe): it sleeps in
+// s_sleep slices and leaves when the host sets `stop` or after `max_ticks` of s_memrealtime
+// (100 MHz) — every exit is bounded.
+__global__ __launch_bounds__(64) void keep_warm_kernel(const uint32_t* stop, uint64_t max_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+
 unsigned grid_for(uint64_t items) {
   uint64_t g = (items + kThreads - 1) / kThreads;
   return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 4096)));
@@ -634,6 +646,24 @@ int launch_l2_touch(const void* p, size_t len, hipStream_t stream) {
 // One run of l1_stale_kernel (see there): `src` holds 64 words of pattern A, the host rewrites
 // them to pattern B once every workgroup has read them.  Out: workgroups whose first read was
 // not A (setup failures), whose second read still held A words (stale), and the workgroups.
+// keep_warm_kernel on a stream of its own: `stop_host` is a pinned, mapped word the caller sets
+// to end it; at most `seconds` in any case.
+int keep_warm_start(int device, double seconds, uint32_t* stop_dev, hipStream_t* out) {
+  DORA_HIP(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  DORA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const double s = std::min(std::max(seconds, 0.0), 600.0);
+  hipLaunchKernelGGL(keep_warm_kernel, dim3(1), dim3(64), 0, st, stop_dev,
+                     uint64_t(s * 100e6));
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return fail(DORA_ERR_HIP, "keep-warm launch: %s", hipGetErrorString(e));
+  }
+  *out = st;
+  return DORA_OK;
+}
+
 int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks) {
   *bad_first = *stale = *blocks = 0;
   DORA_HIP(hipSetDevice(device));

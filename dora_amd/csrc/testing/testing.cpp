@@ -26,6 +26,7 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
                          uint32_t* grid);
 int launch_l2_touch(const void* p, size_t len, hipStream_t stream);
 int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks);
+int keep_warm_start(int device, double seconds, uint32_t* stop_dev, hipStream_t* out);
 int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
 int pack_signal_tune(uint32_t grid, bool bench_signal);
 int pack_cp_grid_tune(uint32_t grid);
@@ -152,6 +153,43 @@ int dora_gpu_test_mid_queues(int create, int use) {
     return dora::fail(DORA_ERR_INVALID, "queues: 0..8");
   dora::aql_mid_queues(create, use);
   return DORA_OK;
+}
+
+struct KeepWarm {
+  uint32_t* stop = nullptr;  // pinned, mapped
+  hipStream_t stream = nullptr;
+};
+
+int dora_gpu_test_keep_warm_start(int device, double seconds, void** out) {
+  if (!out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  auto* k = new KeepWarm();
+  if (hipHostMalloc(reinterpret_cast<void**>(&k->stop), 64,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    delete k;
+    return dora::fail(DORA_ERR_HIP, "keep-warm stop word");
+  }
+  __atomic_store_n(k->stop, 0u, __ATOMIC_SEQ_CST);
+  uint32_t* d = nullptr;
+  (void)hipHostGetDevicePointer(reinterpret_cast<void**>(&d), k->stop, 0);
+  const int rc = dora::keep_warm_start(device, seconds, d, &k->stream);
+  if (rc != DORA_OK) {
+    (void)hipHostFree(k->stop);
+    delete k;
+    return rc;
+  }
+  *out = k;
+  return DORA_OK;
+}
+
+int dora_gpu_test_keep_warm_stop(void* h) {
+  auto* k = static_cast<KeepWarm*>(h);
+  if (!k) return DORA_OK;
+  __atomic_store_n(k->stop, 1u, __ATOMIC_SEQ_CST);
+  const hipError_t e = hipStreamSynchronize(k->stream);
+  (void)hipStreamDestroy(k->stream);
+  (void)hipHostFree(k->stop);
+  delete k;
+  return e == hipSuccess ? DORA_OK : dora::fail(DORA_ERR_HIP, "keep-warm: %s", hipGetErrorString(e));
 }
 
 int dora_gpu_test_cp_lone(int on) {

@@ -47,6 +47,10 @@ int dora_gpu_test_aql_hold(int device, int hold);
 /* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
  * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
 int dora_gpu_test_cp_lone(int on);
+/* Test tool (latency probe): one resident wave on `device` that sleeps until
+ * dora_gpu_test_keep_warm_stop (or `seconds`, at most 600) so the GPU never idles. */
+int dora_gpu_test_keep_warm_start(int device, double seconds, void** out);
+int dora_gpu_test_keep_warm_stop(void* handle);
 /* Test tool: the AQL queues this process creates (effective before its first AQL use; 0 keeps
  * 4, at most 8) and how many of them take packs of 8-32 MiB in turn (0 keeps 4). */
 int dora_gpu_test_mid_queues(int create, int use);

@@ -48,6 +48,9 @@ def spin(us):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=400)
+    ap.add_argument("--warm", action="store_true",
+                    help="one resident sleeping wave keeps the GPU from idling during the cases "
+                         "(dora_gpu_test_keep_warm_start)")
     a = ap.parse_args()
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
@@ -78,6 +81,13 @@ def main():
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
     seq += 1
+    warm = None
+    if a.warm:
+        import ctypes
+
+        from dora_amd._lib import call
+        warm = ctypes.c_void_p()
+        call("dora_gpu_test_keep_warm_start", 0, 120.0, ctypes.byref(warm))
     t_case = {}
     for label, z, gap, spun in CASES:
         t0 = time.time_ns()
@@ -92,6 +102,8 @@ def main():
         t_case[label] = (t0, time.time_ns())
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
+    if warm is not None:
+        call("dora_gpu_test_keep_warm_stop", warm)
     buf.free()
     stream.close()
     node.close()
@@ -105,7 +117,7 @@ def main():
             ev.setdefault(r["token"], {}).setdefault(int(r["point"]), int(r["t_ns"]))
     for label, z, gap, _ in CASES:
         s = series.get(z, {})
-        row = {"case": label, "bytes": z, "gap_us": gap, "n": s.get("n"),
+        row = {"case": label, "warm": a.warm, "bytes": z, "gap_us": gap, "n": s.get("n"),
                "latency_p50_us": s.get("p50_us"), "latency_p99_us": s.get("p99_us"),
                "incl_send_p50_us": s.get("full_p50_us")}
         lo, hi = t_case[label]
