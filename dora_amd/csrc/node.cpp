@@ -55,9 +55,11 @@ namespace dora {
 
 // HIP's current device is per thread, and the library acts on the node's GPU from whichever
 // thread calls it — an EventStream moved to another thread (the reference's is Send), an async
-// pump, the event-stream thread: slots, IPC mappings, events and receive buffers are created on
-// the current device.  Each entry point makes the node's device current for the call and gives
-// the caller's back afterwards.
+// pump, the event-stream thread: slots, IPC mappings, events, streams and receive buffers are
+// created on the current device.  Every place that creates one (or launches through HIP) makes
+// the node's device current for that step and gives the caller's back afterwards.  The steady
+// send and receive paths (cached slot, cached mapping, AQL dispatch) create nothing and take no
+// scope: hipGetDevice alone costs ~54 ns per call (scripts/get_device_probe.cpp).
 struct DeviceScope {
   int prev = -1;
   explicit DeviceScope(int device) {
@@ -424,8 +426,10 @@ struct NodeCore {
         *err = "shared-memory sample `" + name + "`: " + std::strerror(errno);
         return nullptr;
       }
-      if (device >= 0)
+      if (device >= 0) {
+        DeviceScope ds(device);
         m->registered = hipHostRegister(m->base, m->len, hipHostRegisterDefault) == hipSuccess;
+      }
       (void)hipGetLastError();
       shm_cache.emplace(name, m);
       while (shm_cache.size() > kMaxIpcMappings) {
@@ -481,6 +485,7 @@ struct NodeCore {
     }
     void* p = nullptr;
     const uint64_t c = (len + 4095) / 4096 * 4096;
+    DeviceScope ds(device);
     if (hipMalloc(&p, c) != hipSuccess) return nullptr;
     *cap = c;
     return p;
@@ -541,6 +546,7 @@ struct NodeCore {
   void ensure_fill_streams() {
     if (!fill_streams.empty() || fill_streams_tried) return;
     fill_streams_tried = true;
+    DeviceScope ds(device);
     if (hipEventCreateWithFlags(&node_ev, hipEventDisableTiming) == hipSuccess) {
       for (size_t i = 0; i < kFillStreams; ++i) {
         hipStream_t s = nullptr;
@@ -562,7 +568,10 @@ struct NodeCore {
   // Order stream `s` after the work queued on the node stream so far (producer kernels of a source).
   void order_after_node_stream(hipStream_t s) {
     if (hipStreamQuery(stream) == hipErrorNotReady) {
-      if (!node_ev) (void)hipEventCreateWithFlags(&node_ev, hipEventDisableTiming);
+      if (!node_ev) {
+        DeviceScope ds(device);
+        (void)hipEventCreateWithFlags(&node_ev, hipEventDisableTiming);
+      }
       if (node_ev && hipEventRecord(node_ev, stream) == hipSuccess) (void)hipStreamWaitEvent(s, node_ev, 0);
     }
     (void)hipGetLastError();
@@ -1055,6 +1064,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
   auto* s = new Slot();
   s->cap = slot_bytes(len);
   s->id = own_slots().next_id.fetch_add(1);
+  DeviceScope ds(n->core->device);
   hipError_t e = hipMalloc(&s->ptr, slot_bytes(len));
   if (e == hipSuccess) e = hipIpcGetMemHandle(&s->handle, s->ptr);
   if (e == hipSuccess) {
@@ -1131,6 +1141,7 @@ void join_bcast_group(dora_node* n, const std::string& input, const uint8_t* uid
     c->bcast_error = "host-only node cannot join a broadcast group";
     return;
   }
+  DeviceScope ds(c->device);
   if (!c->bcast_stream && hipStreamCreateWithFlags(&c->bcast_stream, hipStreamNonBlocking) != hipSuccess) {
     (void)hipGetLastError();
     c->bcast_stream = nullptr;
@@ -1159,6 +1170,7 @@ int post_bcast_receive(NodeCore* c, InputData* in, const std::string& input) {
   if (it == c->bcast_in.end())
     return fail(DORA_ERR_INVALID, "input `%s`: broadcast sample but no group joined (%s)",
                 input.c_str(), c->bcast_error.c_str());
+  DeviceScope ds(c->device);
   uint64_t cap = 0;
   void* local = c->recv_pool_get(in->ext_len, &cap);
   if (!local)
@@ -1256,6 +1268,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           } else {
             hipIpcMemHandle_t h;
             std::memcpy(&h, d.ipc.handle, sizeof(h));
+            DeviceScope ds(c->device);
             hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
             if (e != hipSuccess) {
               ev->type = DORA_EVENT_ERROR;
@@ -1395,6 +1408,7 @@ void finish_input(dora_node* n, dora_event* ev) {
       } else {
         hipIpcEventHandle_t h;
         std::memcpy(&h, d.event, sizeof(h));
+        DeviceScope ds(n->core->device);
         if (hipIpcOpenEventHandle(&fill, h) == hipSuccess) n->core->ipc_events[key] = fill;
         else fill = nullptr;
       }
@@ -1457,6 +1471,7 @@ int enqueue_peer_copy(NodeCore* c, void* dst, const void* src, int src_device, u
 int ensure_local(InputData* in) {
   if (!in || (in->remote_device < 0 && !in->host_pull)) return DORA_OK;
   NodeCore* c = in->core.get();
+  DeviceScope ds(c->device);
   uint64_t cap = 0;
   void* local = c->recv_pool_get(in->ext_len, &cap);
   if (!local)
@@ -1653,6 +1668,7 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
         // its pack there (pack_and_send), or — a sample the user filled — after the work queued on
         // the node stream and every fill so far
         hipStream_t bs = g->second.stream;
+        DeviceScope ds(n->core->device);
         if (sample->fill != FILL_DONE) n->core->fence_fills();
         n->core->order_after_node_stream(bs);
         int rc = bcast_enqueue(g->second.comm, slot->ptr, d.ipc.ext_len, bs);
@@ -1837,6 +1853,7 @@ void harvest_all(dora_node* n) {
 
 int ensure_timing(dora_node* n) {
   if (!n->timing.empty()) return DORA_OK;
+  DeviceScope ds(n->core->device);
   DORA_HIP(hipEventCreate(&n->timing_ref));
   n->timing.resize(kTimingPairs);
   for (auto& p : n->timing) {
@@ -1881,6 +1898,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
                 bool signal = true, bool sync = false) {
   if (!signal) {
     // the caller orders what follows on `st` (a broadcast-group send): no fill flag
+    DeviceScope ds(n->core->device);
     ++n->hip_packs;
     return launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start, t_stop,
                        nullptr, nullptr, slot_bytes(s->slot->cap));
@@ -1930,6 +1948,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       }
     }
   }
+  DeviceScope ds(n->core->device);  // HIP launches and event records below
   if (!st) st = n->core->next_fill_stream();
   ++n->hip_packs;
   bool signalled = false;
@@ -2042,6 +2061,7 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
 // Outputs without a group keep the pull path.  Every wait is bounded.
 void form_bcast_groups(dora_node* n) {
   NodeCore* c = n->core.get();
+  DeviceScope ds(c->device);  // the groups' streams and communicators belong to the node's GPU
   std::string why;
   if (!bcast_available(&why)) {
     c->bcast_error = why;
@@ -2473,7 +2493,6 @@ dora_stream_t dora_node_stream(dora_node* n) {
 
 int dora_node_allocate_data_sample(dora_node* n, size_t len, dora_sample** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   return dora::alloc_sample(n, len, out);
   DORA_GUARD_END
@@ -2497,7 +2516,6 @@ int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint
                                  dora_sample* sample) {
   if (!n || !output_id || (!type_info && type_info_len))
     return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   std::vector<uint8_t> ti(type_info, type_info + type_info_len);
   return dora::send_sample(n, output_id, ti, params, params_len, sample);
@@ -2514,7 +2532,6 @@ int dora_node_send_output_ex(dora_node* n, const char* output_id, const struct A
                              const struct ArrowSchema* schema, ArrowDeviceType device_type,
                              const uint8_t* params, size_t params_len, uint32_t flags) {
   if (!n || !output_id) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   const bool device = device_type == ARROW_DEVICE_ROCM && n->core->device >= 0;
   const bool cacheable = device && !n->compact && array && schema;
@@ -2577,7 +2594,6 @@ int dora_node_send_output_bytes_ex(dora_node* n, const char* output_id, const vo
                                    size_t len, ArrowDeviceType device_type, const uint8_t* params,
                                    size_t params_len, uint32_t flags) {
   if (!n || !output_id || (!data && len)) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   dora::SubSpan sp(dora::SP_SEND_PLAN);
   // one UInt8 buffer: the plan and its type info are built once per node and re-pointed per send
@@ -2651,7 +2667,6 @@ int dora_node_close_outputs(dora_node* n, const char* const* ids, size_t count) 
 int dora_node_next_event(dora_node* n, int64_t timeout_us, dora_event** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   *out = nullptr;
-  dora::DeviceScope ds(n->core->device);
   DORA_GUARD_BEGIN
   const uint64_t t0 = dora::mono_ns();
   if (n->want_pump && !n->pump_on.load()) dora::start_pump(n);
@@ -2718,7 +2733,6 @@ const char* dora_event_error(const dora_event* e) { return e ? e->error.c_str() 
 int dora_event_data(const dora_event* e, const void** ptr, size_t* len) {
   if (!e || !ptr || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!e->data) return dora::fail(DORA_ERR_INVALID, "event has no data");
-  dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
   DORA_GUARD_BEGIN
   int rc = dora::ensure_local(e->data.get());
   if (rc != DORA_OK) return rc;
@@ -2736,7 +2750,6 @@ int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
   if (!e || !ti || !len) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!e->ti_checked && e->type == DORA_EVENT_INPUT && e->data && e->data->ext_len > e->data->len) {
     // bitmaps in the sample's tail: restore the reference's inline ArrowTypeInfo bytes
-    dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
     DORA_GUARD_BEGIN
     int rc = dora::ensure_local(e->data.get());
     if (rc != DORA_OK) return rc;
@@ -2769,7 +2782,6 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
     return dora::fail(DORA_ERR_INVALID, "not an input event");
   if (!e->data->ptr && e->data->len)
     return dora::fail(DORA_ERR_INVALID, "input data is not mapped: %s", e->error.c_str());
-  dora::DeviceScope ds(e->data->core ? e->data->core->device : -1);
   DORA_GUARD_BEGIN
   int rc = dora::ensure_local(e->data.get());
   if (rc != DORA_OK) return rc;
@@ -2853,6 +2865,7 @@ int dora_node_set_timing_period(dora_node* n, uint64_t period) {
 int dora_node_region_begin(dora_node* n) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (n->core->device < 0) return dora::fail(DORA_ERR_INVALID, "host-only node");
+  dora::DeviceScope ds(n->core->device);
   if (!n->region_start) DORA_HIP(hipEventCreate(&n->region_start));
   n->region_cp_next = 0;
   n->region_cp_used.clear();
@@ -2869,6 +2882,7 @@ namespace {
 // Record the region's stop events: one after the last pack queued on each fill stream and on
 // the node stream.  No wait.
 int region_record_stops(dora_node* n) {
+  DeviceScope ds(n->core->device);
   std::vector<hipStream_t> ss = n->core->fill_streams;
   ss.push_back(n->core->stream);
   while (n->region_stop.size() < ss.size()) {  // fill streams are created lazily
@@ -2893,6 +2907,7 @@ int dora_node_region_mark(dora_node* n) {
 int dora_node_region_end(dora_node* n, double* span_ms, uint64_t* packs, uint64_t* bytes) {
   if (!n || !span_ms) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   if (!n->region_armed) return dora::fail(DORA_ERR_INVALID, "no region begun");
+  dora::DeviceScope ds(n->core->device);
   n->region_armed = false;
   const bool marked = n->region_marked;
   n->region_marked = false;
