@@ -855,7 +855,9 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // send that finds the queues idle usually opens a burst: given the whole GPU (3584 workgroups)
   // it delays the packs queued right behind it, so it keeps the in-kernel signal (the 20-step
   // headline 0.778 vs 0.786 mean over six interleaved rounds, profiles/r04_headline20_ab.jsonl).
-  p.lone = sync || queues_idle(a);
+  // (lone only shapes a single-segment pack — its argument ring and kernel — so a multi-segment
+  // one skips the idle check, which loads a GPU-written flag line per queue)
+  p.lone = sync || (n == 1 && segs[0].dst_off == 0 && queues_idle(a));
   p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, sync);
   // HBM-bound packs (>= kBarrierBytes) run in order per queue (barrier bit) over at most three
   // (four below 32 MiB) queues, big_queues: more concurrent 40 MB copies only contend (14.1-14.5
@@ -864,7 +866,9 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   if (big) {
     const size_t qi = size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)));
     const int rc = dispatch_locked(a, qi, &p, 1, true);
-    prune(a, int(qi));
+    // pruning loads the oldest packet's flag line (a cache miss the GPU caused): only once the
+    // queue holds more than the two it runs in turn
+    if (a->outq[qi].size() > 2) prune(a, int(qi));
     return rc;
   }
   // Below that, a queue holds at most kDepth packets (one running, one ready): the command

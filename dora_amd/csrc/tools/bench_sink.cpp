@@ -77,7 +77,11 @@ int main() {
   (void)csum_buf_dummy;
   uint64_t* csum_dev = nullptr;
   dora_gpu_malloc(reinterpret_cast<void**>(&csum_dev), 8);
-  dora_stream_t st = dora_node_stream(node);
+  // a stream of its own: every checksum below is synchronised before its input is released, so
+  // the node stream stays unused and no release has to query it (node.cpp stream_used)
+  dora_stream_t st = nullptr;
+  const bool own_stream = dora_gpu_stream_create(&st) == 0;
+  if (!own_stream) st = dora_node_stream(node);
   // the first checksum loads the kernel's code object (milliseconds): do it now, not while a
   // burst waits on this sink
   {
@@ -268,5 +272,6 @@ int main() {
   if (f != stdout) std::fclose(f);
   dora_gpu_free(csum_dev);
   dora_node_free(node);
+  if (own_stream) (void)dora_gpu_stream_destroy(st);
   return errors ? 1 : 0;
 }

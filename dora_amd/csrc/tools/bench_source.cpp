@@ -87,7 +87,11 @@ int main() {
   const long tp_n = env_long("DORA_BENCH_TP_N", 100);
   const long acks = env_long("DORA_BENCH_ACKS", 1);
   const long verify_n = env_long("DORA_BENCH_VERIFY", 2);
-  dora_stream_t st = dora_node_stream(node);
+  // the payloads are made (and synchronised) on a stream of its own before any send: the node
+  // stream stays unused, so sends need not query it (node.cpp stream_used)
+  dora_stream_t st = nullptr;
+  const bool own_stream = dora_gpu_stream_create(&st) == 0;
+  if (!own_stream) st = dora_node_stream(node);
   int errors = 0;
 
   // throughput mode: rotating source copies, so the sources of a burst are not all served from the
@@ -248,5 +252,6 @@ int main() {
     for (void* p : kv.second.extra) dora_gpu_free(p);
   }
   dora_node_free(node);
+  if (own_stream) (void)dora_gpu_stream_destroy(st);
   return errors || !ok ? 1 : 0;
 }
