@@ -337,7 +337,7 @@ class Node:
         return {"aql": a.value, "hip": h.value}
 
     def set_timing_period(self, period: int):
-        """Stamp every `period`-th pack launch (0: DORA_GPU_TIMING_SAMPLE, default 8)."""
+        """Stamp every `period`-th pack launch (0: the default, every 8th)."""
         call("dora_node_set_timing_period", self.handle, int(period))
 
     def pack_intervals(self, cap: int = 1 << 16):
