@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--size", type=int, default=40960000)
     ap.add_argument("--modes", default="cp,k1024,k2048,k3584")
+    ap.add_argument("--chunks", default="0",
+                    help="bytes per workgroup chunk (dora_gpu_test_pack_tune; 0: the default 8 KiB)")
     a = ap.parse_args()
     import bench
     from dora_amd import device
@@ -57,16 +59,19 @@ def main():
         wait_ack(seq)
         seq += 1
         modes = a.modes.split(",")
+        chunks = [int(x) for x in a.chunks.split(",")]
         for r in range(a.reps):
-            for m in modes:
+            for m, ch in [(m, ch) for m in modes for ch in chunks]:
+                call("dora_gpu_test_pack_tune", 0, -1, ch)
                 call("dora_gpu_test_cp_lone", 1 if m == "cp" else 0)
                 call("dora_gpu_test_pack_signal_tune", 0 if m in ("cp", "k1024") else int(m[1:]), 0)
                 out = bench.run_sync_leg(node, send, wait_ack, seq, S, a.n)
                 seq = out.pop("seq")
                 out.pop("send_calls_us", None)
-                print(json.dumps({"rep": r, "mode": m, **out}), flush=True)
+                print(json.dumps({"rep": r, "mode": m, "chunk": ch, **out}), flush=True)
         call("dora_gpu_test_cp_lone", 1)
         call("dora_gpu_test_pack_signal_tune", 0, 0)
+        call("dora_gpu_test_pack_tune", 0, -1, 0)
         for b in bufs:
             b.free()
         stream.close()
