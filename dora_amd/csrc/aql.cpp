@@ -118,7 +118,6 @@ constexpr uint64_t kCpLo = uint64_t(1) << 20, kCpHi = uint64_t(32) << 20;
 //   32 MiB: C3 0.68-0.70 -> 0.72-0.75 (profiles/r04_full_ab.jsonl), 40.96 MB 14.1-14.5 ->
 //   12.9-13.0 us per pack (profiles/r02_aql_big_ab.jsonl);
 constexpr uint64_t kBarrierBytes = uint64_t(8) << 20;
-std::atomic<bool> g_defer_doorbell{false};  // test hook aql_defer_doorbell
 // * a queue holds at most two in-kernel-signalled packets (one running, one ready) and three
 //   CP-signalled ones (they overlap: 4 MB 1.88 -> 1.66 us at depth 3, r03_cp_signal_ab.jsonl);
 //   sends finding every queue that deep leave together as a batch pack of <= 32 MiB.
@@ -531,8 +530,7 @@ uint64_t oldest_outstanding(const AqlQueue* a) {
 
 // Write and ring one packet on queue `qi` (a->mu held): one message with the single- or
 // multi-segment kernels, or a batch of `n` > 1 messages with dora_aql_packb_u4.
-int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big,
-                    AqlDeferred* defer = nullptr) {
+int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big) {
   const Pending& it0 = items[0];
   const Segment* segs = it0.segs;
   uint8_t* const dst = it0.dst;
@@ -683,18 +681,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
                            << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  const bool dev_ring = !(one && !dev_args1);
-  if (defer && dev_ring) {
-    // published by aql_commit, after the caller's descriptor send: the HDP flush drains meanwhile
-    defer->q = a;
-    defer->packet = p;
-    defer->hsa_queue = q;
-    defer->header_setup = header | (uint32_t(setup) << 16);
-    defer->index = idx;
-    defer->pending = true;
-  } else {
-    publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
-  }
+  publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
   // every message of a batch signals at its end: the last one's flag stands for the packet
   u.flag = items[n - 1].flag_host;
   u.epoch = items[n - 1].sig.epoch;
@@ -846,7 +833,7 @@ void dispatcher_main(AqlQueue* a) {
 
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
-             uint64_t* cp_stamps, bool sync, AqlDeferred* defer) {
+             uint64_t* cp_stamps, bool sync) {
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -860,7 +847,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.profile = profile;
   p.cp_stamps = cp_stamps;
   for (size_t i = 0; i < n; ++i) p.bytes += segs[i].len;
-  std::unique_lock<std::mutex> g(a->mu);
+  std::lock_guard<std::mutex> g(a->mu);
   // lone: runs alone on the GPU (a synchronous send, or every queue idle): its arguments go to
   // the device ring and it reads without the acquire fence (dispatch_locked).  Signalled by the
   // command processor (inside a timed region only with a stamp area for the pack's own stamps):
@@ -878,12 +865,10 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   const bool big = p.bytes >= kBarrierBytes;
   if (big) {
     const size_t qi = size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)));
-    const int rc = dispatch_locked(
-        a, qi, &p, 1, true, defer && g_defer_doorbell.load(std::memory_order_relaxed) ? defer : nullptr);
+    const int rc = dispatch_locked(a, qi, &p, 1, true);
     // pruning loads the oldest packet's flag line (a cache miss the GPU caused): only once the
     // queue holds more than the two it runs in turn
     if (a->outq[qi].size() > 2) prune(a, int(qi));
-    if (defer && defer->pending) g.release();  // aql_commit unlocks
     return rc;
   }
   // Below that, a queue holds at most kDepth packets (one running, one ready): the command
@@ -914,16 +899,6 @@ std::atomic<bool> g_cp_lone{true};  // lone single-segment packs above the windo
 }  // namespace
 
 void aql_cp_lone(bool on) { g_cp_lone.store(on); }
-
-void aql_defer_doorbell(bool on) { g_defer_doorbell.store(on); }
-
-void aql_commit(AqlDeferred* d) {
-  if (!d || !d->pending) return;
-  publish_packet(static_cast<hsa_queue_t*>(d->hsa_queue), d->packet, d->header_setup, d->index,
-                 d->q->wc_ring);
-  d->pending = false;
-  d->q->mu.unlock();
-}
 
 void aql_mid_queues(int create, int use) {
   if (create > 0) g_create_queues.store(create);

@@ -43,29 +43,9 @@ bool aql_usable(const AqlQueue* q);
 // without the acquire fence; a synchronous one is also signalled by the command processor at any
 // size >= 1 MiB, with a grid of up to 3584 workgroups (no done words to poll, so no
 // 1024-workgroup signalling cap).
-// A dispatch written but not yet published (aql_pack with `defer`): its packet header and the
-// queue's doorbell go out in aql_commit, which must follow at once (the queue's lock is held until
-// then, and the command processor waits at the unpublished packet).  Only packs >= 8 MiB whose
-// arguments go through the device ring defer: the ring's HDP flush then drains while the caller
-// sends the message's descriptor, instead of stalling the doorbell store.
-struct AqlDeferred;
-void aql_commit(AqlDeferred* d);
-struct AqlDeferred {
-  AqlDeferred() = default;
-  AqlDeferred(const AqlDeferred&) = delete;
-  AqlDeferred& operator=(const AqlDeferred&) = delete;
-  ~AqlDeferred() { aql_commit(this); }  // never left unpublished (error and exception paths)
-  AqlQueue* q = nullptr;
-  void* packet = nullptr;
-  void* hsa_queue = nullptr;
-  uint32_t header_setup = 0;
-  uint64_t index = 0;
-  bool pending = false;
-};
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
-             uint64_t* cp_stamps = nullptr, bool sync = false, AqlDeferred* defer = nullptr);
-// aql_commit: publish a deferred dispatch (no-op unless pending) and release the queue.
+             uint64_t* cp_stamps = nullptr, bool sync = false);
 // Would a pack of these segments be signalled by the command processor: [1 MiB, 32 MiB), or
 // (`lone`: a synchronous send) a single-segment pack of any size from 1 MiB.
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);
@@ -90,8 +70,6 @@ int aql_hold(int device, bool hold);
 // Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
 // in-kernel (test hook, probes of the synchronous send).
 void aql_cp_lone(bool on);
-// Test hook: packs that may defer their doorbell (aql_pack `defer`) do (1) or not (0, default).
-void aql_defer_doorbell(bool on);
 // Test hook: HSA queues a process creates (before its first AQL use; 0 keeps 4) and how many
 // take packs of 8-32 MiB (0 keeps 4).
 void aql_mid_queues(int create, int use);

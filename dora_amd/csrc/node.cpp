@@ -1635,8 +1635,7 @@ void put_metadata(WBuf& w, const std::vector<uint8_t>& ti, const uint8_t* params
 
 int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>& ti,
                 const uint8_t* params, size_t params_len, dora_sample* sample,
-                DropToken* token_out = nullptr, uint64_t ts_override = 0,
-                AqlDeferred* defer = nullptr) {
+                DropToken* token_out = nullptr, uint64_t ts_override = 0) {
   {
     SubSpan sp(SP_SEND_TOKENS);
     handle_finished_drop_tokens(n);
@@ -1718,7 +1717,6 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
   put_metadata(w, ti, params, params_len, ts);
   w.data(d);
   int rc = n->core->request(REQ_SEND_MESSAGE, w.data(), w.size());
-  aql_commit(defer);  // the pack's packet, written before the descriptor (fill_sample `defer`)
   sp_req.stop();
   if (rc != DORA_OK) {
     if (slot) add_to_cache(n, slot);
@@ -1909,7 +1907,7 @@ hipError_t order_fill(dora_node* n, dora_sample* s, hipStream_t st) {
 // completion signal.
 int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
                 ArrowDeviceType dev, hipStream_t st, hipEvent_t t_start, hipEvent_t t_stop,
-                bool signal = true, bool sync = false, AqlDeferred* defer = nullptr) {
+                bool signal = true, bool sync = false) {
   if (!signal) {
     // the caller orders what follows on `st` (a broadcast-group send): no fill flag
     DeviceScope ds(n->core->device);
@@ -1950,8 +1948,7 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       }
       s->slot->region_cp_area = area;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync,
-                   sync ? nullptr : defer) == DORA_OK) {
+                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -2178,7 +2175,6 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   if (rc != DORA_OK) return rc;
   const uint64_t t1 = mono_ns();
   uint64_t t2 = t1, t3 = t1;
-  AqlDeferred deferred;  // a pack whose packet goes out after the descriptor (send_sample)
   if (plan->size && (!s->slot || s->slot->host)) {
     // an inline Vec or a host-only node's shared-memory slot: the host copies the buffers
     // (copy_array_into_sample, arrow_utils.rs:48)
@@ -2215,10 +2211,8 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     const bool sync = plan->dev == ARROW_DEVICE_ROCM &&
                       !((flags & DORA_SEND_ASYNC) || n->async_default);
     rc = fill_sample(n, s, plan->segs.data(), plan->segs.size(), plan->dev,
-                     bcast ? bo->second.stream : nullptr, t_start, t_stop, !bcast, sync,
-                     bcast ? nullptr : &deferred);
+                     bcast ? bo->second.stream : nullptr, t_start, t_stop, !bcast, sync);
     if (rc != DORA_OK) {
-      aql_commit(&deferred);
       if (tp) tp->pending = false;
       add_to_cache(n, s->slot);
       delete s;
@@ -2250,8 +2244,7 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
     if (s->fill == FILL_EVENT) wait.event = s->slot->done;
   }
-  rc = send_sample(n, output_id, ti, params, params_len, s, &tok, 0, &deferred);
-  aql_commit(&deferred);  // (done by send_sample unless it failed before its request)
+  rc = send_sample(n, output_id, ti, params, params_len, s, &tok);
   if (rc == DORA_OK && sync_src) rc = wait_source_read(n, wait);
   const uint64_t t4 = mono_ns();
   if (traced && rc == DORA_OK) {

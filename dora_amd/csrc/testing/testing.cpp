@@ -192,11 +192,6 @@ int dora_gpu_test_keep_warm_stop(void* h) {
   return e == hipSuccess ? DORA_OK : dora::fail(DORA_ERR_HIP, "keep-warm: %s", hipGetErrorString(e));
 }
 
-int dora_gpu_test_defer_doorbell(int on) {
-  dora::aql_defer_doorbell(on != 0);
-  return DORA_OK;
-}
-
 int dora_gpu_test_cp_lone(int on) {
   dora::aql_cp_lone(on != 0);
   return DORA_OK;

@@ -47,10 +47,6 @@ int dora_gpu_test_aql_hold(int device, int hold);
 /* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
  * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
 int dora_gpu_test_cp_lone(int on);
-/* Test tool: 1 = asynchronous sends of >= 8 MiB whose pack arguments go through the device ring
- * publish the packet after the message's descriptor (the HDP flush drains meanwhile); 0 (default)
- * = before it. */
-int dora_gpu_test_defer_doorbell(int on);
 /* Test tool (latency probe): one resident wave on `device` that sleeps until
  * dora_gpu_test_keep_warm_stop (or `seconds`, at most 600) so the GPU never idles. */
 int dora_gpu_test_keep_warm_start(int device, double seconds, void** out);

@@ -9,8 +9,7 @@ Diagnoses the burst's host stall with CP-signalled multi-segment packs (DESIGN Â
 With --grids, every rep runs once per workgroup cap of the command processor's packs
 (dora_gpu_test_cp_grid: C3's clouds are CP-signalled), interleaved; --multi-grids caps only the
 multi-segment ones (dora_gpu_test_cp_grid_multi) and --caps sets the sender's in-flight cap
-from 8 MiB (dora_gpu_test_in_flight); --defer 0,1 publishes the packs' packets before (0) or
-after (1) their descriptors (dora_gpu_test_defer_doorbell); every combination runs once per rep.
+from 8 MiB (dora_gpu_test_in_flight); every combination runs once per rep.
 """
 import argparse
 import json
@@ -30,7 +29,6 @@ def main():
     ap.add_argument("--caps", default="0", help="in-flight caps from 8 MiB (0: the default, 8)")
     ap.add_argument("--mid-queues", default="0",
                     help="queues taking 8-32 MiB packs (0: the default, 4; up to 8 are created)")
-    ap.add_argument("--defer", default="0", help="deferred doorbells off (0) / on (1)")
     a = ap.parse_args()
     import bench
     from dora_amd import device
@@ -59,18 +57,15 @@ def main():
         grids = [int(x) for x in a.grids.split(",")]
         multis = [int(x) for x in a.multi_grids.split(",")]
         caps = [int(x) for x in a.caps.split(",")]
-        defers = [int(x) for x in a.defer.split(",")]
-        combos = [(r, g, m, c, q, d) for r in range(a.reps) for g in grids for m in multis
-                  for c in caps for q in mids for d in defers]
-        for r, g, m, c, q, d in combos:
-            call("dora_gpu_test_defer_doorbell", d)
+        combos = [(r, g, m, c, q) for r in range(a.reps) for g in grids for m in multis
+                  for c in caps for q in mids]
+        for r, g, m, c, q in combos:
             call("dora_gpu_test_mid_queues", 0, q if q else 4)
             call("dora_gpu_test_cp_grid", g)
             call("dora_gpu_test_cp_grid_multi", m)
             call("dora_gpu_test_in_flight", 0, c)
             seq, c3 = bench.run_c3_block(node, stream, wait_ack, seq, steady_steps=a.steady)
             print(json.dumps({"rep": r, "cp_grid": g, "multi_grid": m, "big_cap": c, "mid_queues": q,
-                              "defer": d,
                               "frac": c3["roofline"]["frac"],
                               "steady_frac": (c3["steady"] or {}).get("frac"),
                               "us_per_cloud": c3["roofline"]["device_us_per_launch"],
@@ -80,7 +75,6 @@ def main():
         call("dora_gpu_test_cp_grid", 0)
         call("dora_gpu_test_cp_grid_multi", 0)
         call("dora_gpu_test_in_flight", 0, 0)
-        call("dora_gpu_test_defer_doorbell", 0)
         stream.close()
         node.close()
         df.wait(60)
