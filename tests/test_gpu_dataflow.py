@@ -980,6 +980,56 @@ def test_device_array_send_waits_for_its_source(launcher):
         assert to_u64(results[seq]["csum"]) == want[seq], seq
 
 
+def test_big_multi_segment_async_sends_bit_exact(launcher):
+    """Asynchronous 16 MiB Struct<x,y:i64> sends (two-segment packs >= 8 MiB, on the barrier
+    queues with their arguments in the device ring): every array arrives with its own checksum."""
+    import numpy as np
+    import pyarrow as pa
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceArray
+    from dora_amd.node import Node
+    from dora_amd.verify import to_u64
+    from oracle.arrow_ffi import import_array
+    from oracle.checksum_ref import regions_csum
+    from oracle.pack_ref import node_regions
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["pc"], "inputs": {"result": "recv/result"}},
+        {"id": "recv", "path": sys.executable,
+         "args": [os.path.join(ROOT, "examples", "verify_receiver.py")],
+         "inputs": {"pc": {"source": "src/pc", "queue_size": 100}}, "outputs": ["result"]},
+    ]}
+    n, k_msgs = 1 << 20, 12
+    rng = np.random.default_rng(11)
+    arrs = [pa.StructArray.from_arrays([pa.array(rng.integers(-2**62, 2**62, n)),
+                                        pa.array(rng.integers(-2**62, 2**62, n))],
+                                       names=["x", "y"]) for _ in range(k_msgs)]
+    want = [regions_csum(node_regions(import_array(a))) for a in arrs]
+    devs = [DeviceArray.from_pyarrow(a) for a in arrs]
+    try:
+        with Dataflow(desc, launcher=launcher) as df:
+            node = Node("src", dataflow=df.shm, device=0)
+            node.set_async_sends(True)
+            for seq in range(k_msgs):
+                node.send_output("pc", devs[seq], {"seq": seq})
+            results = {}
+            deadline = time.time() + 120
+            while len(results) < k_msgs and time.time() < deadline:
+                ev = node.next(timeout=5)
+                if ev is None:
+                    break
+                if ev["type"] == "INPUT":
+                    results[ev["metadata"]["seq"]] = ev["metadata"]
+            node.close()
+            codes = df.wait(60)
+            log = df.log("recv")
+    finally:
+        for d in devs:
+            d.close()
+    assert codes["recv"] == 0, log
+    for seq in range(k_msgs):
+        assert to_u64(results[seq]["csum"]) == want[seq], seq
+
+
 def test_host_source_reused_right_after_send_bit_exact(launcher, tmp_path):
     """send_output_raw semantics for host data (examples/benchmark/node/src/main.rs:46-48: the
     closure copies `data` before send returns): one host buffer overwritten with the next payload
