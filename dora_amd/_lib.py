@@ -196,6 +196,9 @@ _TEST_SIGS = {
     "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
     "dora_gpu_test_cp_lone": (c_int, [c_int]),
+    "dora_gpu_test_heartbeat_start": (c_int, [c_int, c_int, ctypes.c_double, ctypes.c_double,
+                                              ctypes.POINTER(c_void_p)]),
+    "dora_gpu_test_heartbeat_stop": (c_int, [c_void_p]),
     "dora_gpu_test_keep_warm_start": (c_int, [c_int, ctypes.c_double, ctypes.POINTER(c_void_p)]),
     "dora_gpu_test_keep_warm_stop": (c_int, [c_void_p]),
     "dora_gpu_test_mid_queues": (c_int, [c_int, c_int]),

@@ -10,6 +10,7 @@
 #include <hsa/hsa.h>
 #include <hsa/amd_hsa_signal.h>
 #include <hsa/hsa_ext_amd.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -185,6 +186,12 @@ struct AqlQueue {
   hipStream_t fallback = nullptr;
   uint64_t fallbacks = 0;
   hsa_signal_t reduce_sig{0};  // completion of aql_stamp_reduce's dispatch
+  // Keeping the dispatch side awake (warm_main): packets dispatched so far (written under mu),
+  // and whether the warm thread is parked (no dispatch for kWarmWindow)
+  std::atomic<uint64_t> activity{0};
+  std::atomic<bool> warm_parked{false};
+  std::mutex warm_mu;
+  std::condition_variable warm_cv;
 };
 
 namespace {
@@ -417,6 +424,8 @@ AqlQueue* create(int device) {
 }  // namespace
 
 namespace {
+std::chrono::nanoseconds warm_period();
+void warm_main(AqlQueue* a);
 std::mutex g_queues_mu;
 AqlQueue* g_queues[64] = {};
 }  // namespace
@@ -430,6 +439,8 @@ AqlQueue* aql_queue(int device) {
   if (!tried[device]) {
     tried[device] = true;
     queues[device] = create(device);
+    // the warm thread (warm_main) lives as long as the process, like the queues
+    if (queues[device] && warm_period().count() > 0) std::thread(warm_main, queues[device]).detach();
   }
   AqlQueue* q = queues[device];
   return (q && !q->failed.load()) ? q : nullptr;
@@ -530,6 +541,8 @@ uint64_t oldest_outstanding(const AqlQueue* a) {
 
 // Write and ring one packet on queue `qi` (a->mu held): one message with the single- or
 // multi-segment kernels, or a batch of `n` > 1 messages with dora_aql_packb_u4.
+void wake_warm(AqlQueue* a);
+
 int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big) {
   const Pending& it0 = items[0];
   const Segment* segs = it0.segs;
@@ -682,6 +695,8 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
                           (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
+  a->activity.store(a->next + 1, std::memory_order_relaxed);  // the warm thread's clock
+  if (a->warm_parked.load(std::memory_order_relaxed)) wake_warm(a);
   // every message of a batch signals at its end: the last one's flag stands for the packet
   u.flag = items[n - 1].flag_host;
   u.epoch = items[n - 1].sig.epoch;
@@ -796,6 +811,87 @@ void pump_locked(AqlQueue* a) {
       return;
     }
   }
+}
+
+// One empty barrier-AND packet (no dependencies, no completion signal) on the first queue
+// (a->mu held); nothing if that queue's ring is full.
+void heartbeat_locked(AqlQueue* a) {
+  hsa_queue_t* const q = a->qs[0];
+  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+  if (idx - a->rd[0] >= q->size && idx - (a->rd[0] = hsa_queue_load_read_index_scacquire(q)) >= q->size)
+    return;
+  hsa_queue_store_write_index_relaxed(q, idx + 1);
+  auto* p = static_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  std::memset(reinterpret_cast<uint8_t*>(p) + 4, 0, sizeof(*p) - 4);
+  const uint16_t header = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                          (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                          (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+  publish_packet(q, p, header, idx, a->wc_ring);
+}
+
+// Keeping the dispatch side awake.  Once no packet of the process has reached the GPU for
+// 50-200 us, the next one takes ~5.5 us longer from doorbell to completion: a device message 1 ms
+// after the previous one arrives in 11.5-11.8 us instead of 5.6-6.1.  A resident
+// sleeping wave does not prevent that, nor do PCIe reads or writes of device memory; an empty
+// barrier-AND packet every 40 us does (5.4-5.9 us, profiles/r05_small_lat_heartbeat_zb.jsonl).
+// So while the process is sending, this thread wakes every `period` and, when nothing was
+// dispatched since its last wake, publishes one such packet; kWarmWindow after the last dispatch
+// it parks until the next.  DORA_GPU_WARM_US sets the period (default 25; 0 turns it off).
+constexpr auto kWarmWindow = std::chrono::milliseconds(100);
+
+std::chrono::nanoseconds warm_period() {
+  static const std::chrono::nanoseconds p = [] {
+    const char* e = std::getenv("DORA_GPU_WARM_US");
+    const double us = e ? std::atof(e) : 25.0;
+    return std::chrono::nanoseconds(us > 0 ? int64_t(std::max(us, 5.0) * 1000) : 0);
+  }();
+  return p;
+}
+
+void warm_main(AqlQueue* a) {
+  (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // wake on time, not up to 50 us late
+  const auto period = warm_period();
+  using clock = std::chrono::steady_clock;
+  uint64_t seen = a->activity.load(std::memory_order_relaxed);
+  auto last_change = clock::now();
+  auto next = last_change;
+  while (!a->failed.load(std::memory_order_relaxed)) {
+    next += period;
+    std::this_thread::sleep_until(next);
+    auto now = clock::now();
+    if (next + period < now) next = now;  // descheduled: resume the beat, do not catch up
+    const uint64_t c = a->activity.load(std::memory_order_relaxed);
+    if (c != seen) {
+      seen = c;
+      last_change = now;
+      continue;
+    }
+    if (now - last_change > kWarmWindow) {
+      // park; a dispatch wakes it (wake_warm).  The 10 ms bound covers a dispatch that raced
+      // the parking.
+      std::unique_lock<std::mutex> lk(a->warm_mu);
+      a->warm_parked.store(true);
+      while (a->warm_parked.load() && a->activity.load(std::memory_order_relaxed) == seen &&
+             !a->failed.load(std::memory_order_relaxed))
+        a->warm_cv.wait_for(lk, std::chrono::milliseconds(10));
+      a->warm_parked.store(false);
+      seen = a->activity.load(std::memory_order_relaxed);
+      last_change = next = clock::now();
+      continue;
+    }
+    if (a->mu.try_lock()) {  // busy: a send is being dispatched right now
+      heartbeat_locked(a);
+      a->mu.unlock();
+    }
+  }
+}
+
+void wake_warm(AqlQueue* a) {
+  {
+    std::lock_guard<std::mutex> g(a->warm_mu);
+    a->warm_parked.store(false);
+  }
+  a->warm_cv.notify_one();
 }
 
 // The dispatcher thread: dispatches the backlog as queues drain while no send is being made.
@@ -980,6 +1076,14 @@ int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint6
   *batches = a->batches;
   *batched_msgs = a->batched_msgs;
   *backlogged = a->backlogged;
+  return DORA_OK;
+}
+
+int aql_heartbeat(int device) {
+  AqlQueue* a = aql_queue(device);
+  if (!aql_usable(a)) return fail(DORA_ERR_HIP, "AQL queue unavailable");
+  std::lock_guard<std::mutex> g(a->mu);
+  heartbeat_locked(a);
   return DORA_OK;
 }
 

@@ -70,6 +70,9 @@ int aql_hold(int device, bool hold);
 // Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
 // in-kernel (test hook, probes of the synchronous send).
 void aql_cp_lone(bool on);
+// Test tool: one empty barrier-AND packet (no dependencies, no completion signal) on the first
+// queue of `device` (latency probe: does a packet keep the dispatch side awake).
+int aql_heartbeat(int device);
 // Test hook: HSA queues a process creates (before its first AQL use; 0 keeps 4) and how many
 // take packs of 8-32 MiB (0 keeps 4).
 void aql_mid_queues(int create, int use);

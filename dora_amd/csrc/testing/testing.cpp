@@ -5,10 +5,14 @@
 // bincode.cpp, bcast.cpp, shm.h).
 #include <hip/hip_runtime_api.h>
 
+#include <sys/prctl.h>
+
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "aql.h"
@@ -190,6 +194,53 @@ int dora_gpu_test_keep_warm_stop(void* h) {
   (void)hipHostFree(k->stop);
   delete k;
   return e == hipSuccess ? DORA_OK : dora::fail(DORA_ERR_HIP, "keep-warm: %s", hipGetErrorString(e));
+}
+
+struct Heartbeat {
+  std::atomic<bool> stop{false};
+  std::thread th;
+  void* bar = nullptr;
+};
+
+int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double seconds,
+                                  void** out) {
+  if (!out || mode < 1 || mode > 3 || !(period_us >= 5) || !(seconds > 0) || seconds > 600)
+    return dora::fail(DORA_ERR_INVALID, "heartbeat: mode 1..3, period >= 5 us, 0 < seconds <= 600");
+  auto* h = new Heartbeat();
+  if (mode != 1 && dora::bar_alloc(device, 4096, &h->bar) != DORA_OK) {
+    delete h;
+    return dora::fail(DORA_ERR_HIP, "heartbeat: no host-visible device memory");
+  }
+  h->th = std::thread([h, device, mode, period_us, seconds] {
+    (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(seconds);
+    const auto period = std::chrono::nanoseconds(int64_t(period_us * 1000));
+    auto next = std::chrono::steady_clock::now();
+    uint32_t v = 0;
+    while (!h->stop.load(std::memory_order_relaxed) && std::chrono::steady_clock::now() < t_end) {
+      if (mode == 1) {
+        (void)dora::aql_heartbeat(device);
+      } else if (mode == 2) {
+        v += *static_cast<volatile uint32_t*>(h->bar);  // one uncached read over PCIe
+      } else {
+        *static_cast<volatile uint32_t*>(h->bar) = ++v;  // one posted write over PCIe
+        __builtin_ia32_sfence();
+      }
+      next += period;
+      std::this_thread::sleep_until(next);
+    }
+  });
+  *out = h;
+  return DORA_OK;
+}
+
+int dora_gpu_test_heartbeat_stop(void* p) {
+  auto* h = static_cast<Heartbeat*>(p);
+  if (!h) return DORA_OK;
+  h->stop.store(true);
+  if (h->th.joinable()) h->th.join();
+  delete h;  // the BAR word stays (bar_alloc has no free; 4 KiB)
+  return DORA_OK;
 }
 
 int dora_gpu_test_cp_lone(int on) {

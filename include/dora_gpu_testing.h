@@ -47,6 +47,13 @@ int dora_gpu_test_aql_hold(int device, int hold);
 /* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
  * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
 int dora_gpu_test_cp_lone(int on);
+/* Test tool (latency probe): a host thread that every `period_us` either publishes an empty
+ * barrier-AND packet on this process's first AQL queue of `device` (mode 1), reads (2) or writes
+ * (3) one word of host-visible device memory over PCIe; until dora_gpu_test_heartbeat_stop or
+ * `seconds` (at most 600). */
+int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double seconds,
+                                  void** out);
+int dora_gpu_test_heartbeat_stop(void* h);
 /* Test tool (latency probe): one resident wave on `device` that sleeps until
  * dora_gpu_test_keep_warm_stop (or `seconds`, at most 600) so the GPU never idles. */
 int dora_gpu_test_keep_warm_start(int device, double seconds, void** out);

@@ -51,6 +51,11 @@ def main():
     ap.add_argument("--warm", action="store_true",
                     help="one resident sleeping wave keeps the GPU from idling during the cases "
                          "(dora_gpu_test_keep_warm_start)")
+    ap.add_argument("--heartbeat", type=int, default=0,
+                    help="a host thread keeps touching the GPU during the cases "
+                         "(dora_gpu_test_heartbeat_start): 1 empty AQL packet, 2 PCIe read, "
+                         "3 PCIe write; 0 none")
+    ap.add_argument("--period", type=float, default=40.0, help="heartbeat period, us")
     a = ap.parse_args()
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
@@ -88,6 +93,13 @@ def main():
         from dora_amd._lib import call
         warm = ctypes.c_void_p()
         call("dora_gpu_test_keep_warm_start", 0, 120.0, ctypes.byref(warm))
+    beat = None
+    if a.heartbeat:
+        import ctypes
+
+        from dora_amd._lib import call
+        beat = ctypes.c_void_p()
+        call("dora_gpu_test_heartbeat_start", 0, a.heartbeat, a.period, 120.0, ctypes.byref(beat))
     t_case = {}
     for label, z, gap, spun in CASES:
         t0 = time.time_ns()
@@ -102,6 +114,8 @@ def main():
         t_case[label] = (t0, time.time_ns())
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
+    if beat is not None:
+        call("dora_gpu_test_heartbeat_stop", beat)
     if warm is not None:
         call("dora_gpu_test_keep_warm_stop", warm)
     buf.free()
@@ -117,7 +131,7 @@ def main():
             ev.setdefault(r["token"], {}).setdefault(int(r["point"]), int(r["t_ns"]))
     for label, z, gap, _ in CASES:
         s = series.get(z, {})
-        row = {"case": label, "warm": a.warm, "bytes": z, "gap_us": gap, "n": s.get("n"),
+        row = {"case": label, "warm": a.warm, "heartbeat": a.heartbeat, "period_us": a.period, "bytes": z, "gap_us": gap, "n": s.get("n"),
                "latency_p50_us": s.get("p50_us"), "latency_p99_us": s.get("p99_us"),
                "incl_send_p50_us": s.get("full_p50_us")}
         lo, hi = t_case[label]

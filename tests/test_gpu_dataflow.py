@@ -955,6 +955,9 @@ def test_device_array_send_waits_for_its_source(launcher):
         node = Node("src", dataflow=df.shm, device=0)
         with DeviceArray.from_pyarrow(arrs[0]) as da:
             for seq in range(k_msgs):
+                # the rewrite queued after the previous send has landed (it races that send's pack,
+                # not this one's: the stream is not ordered with the node's packs)
+                other.sync()
                 node.send_output("pc", da, {"seq": seq})
                 if seq + 1 < k_msgs:   # the next array's bytes into the sent one's buffers, no sync
                     for c in range(2):
