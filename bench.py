@@ -58,6 +58,9 @@ def parse():
                     help="throughput ladder: back-to-back messages per size, at least 2000 up "
                          "to 4 MiB (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--keep-awake-us", type=float, default=None,
+                    help="period of the senders' keep-awake packets (dora_gpu_set_keep_awake; "
+                         "0: off; default: the library's, 25)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 block the default C2 run reports beside the headline")
     ap.add_argument("--c3-steps", type=int, default=20)
@@ -639,6 +642,10 @@ def main():
     gpu_of = (lambda g: g % vis) if vis > 0 else (lambda g: g)
     local_rank = gpu_of(local_rank)
     affinity = sorted(os.sched_getaffinity(0))
+    if args.keep_awake_us is not None:  # this process, and the native sources it spawns
+        os.environ["DORA_BENCH_KEEP_AWAKE_US"] = str(args.keep_awake_us)
+        from dora_amd import device as _device
+        _device.set_keep_awake(args.keep_awake_us)
 
     # ---- CPU-only work and process spawning first: nothing below touches HIP until Node() ----
     base = None

@@ -56,6 +56,7 @@ _SIGS = {
     "dora_gpu_aql_batch_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_uint64),
                                          POINTER(c_uint64)]),
     "dora_gpu_aql_cp_signalled": (c_int, [c_int, POINTER(c_uint64)]),
+    "dora_gpu_set_keep_awake": (c_int, [ctypes.c_double]),
     "dora_gpu_device_count": (c_int, [POINTER(c_int)]),
     "dora_gpu_set_device": (c_int, [c_int]),
     "dora_gpu_get_device": (c_int, [POINTER(c_int)]),
@@ -199,6 +200,7 @@ _TEST_SIGS = {
     "dora_gpu_test_heartbeat_start": (c_int, [c_int, c_int, ctypes.c_double, ctypes.c_double,
                                               ctypes.POINTER(c_void_p)]),
     "dora_gpu_test_heartbeat_stop": (c_int, [c_void_p]),
+    "dora_gpu_test_keep_awake_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_int)]),
     "dora_gpu_test_keep_warm_start": (c_int, [c_int, ctypes.c_double, ctypes.POINTER(c_void_p)]),
     "dora_gpu_test_keep_warm_stop": (c_int, [c_void_p]),
     "dora_gpu_test_mid_queues": (c_int, [c_int, c_int]),

@@ -190,6 +190,7 @@ struct AqlQueue {
   // and whether the warm thread is parked (no dispatch for kWarmWindow)
   std::atomic<uint64_t> activity{0};
   std::atomic<bool> warm_parked{false};
+  std::atomic<uint64_t> heartbeats{0};  // empty packets published (aql_heartbeats)
   std::mutex warm_mu;
   std::condition_variable warm_cv;
 };
@@ -424,7 +425,6 @@ AqlQueue* create(int device) {
 }  // namespace
 
 namespace {
-std::chrono::nanoseconds warm_period();
 void warm_main(AqlQueue* a);
 std::mutex g_queues_mu;
 AqlQueue* g_queues[64] = {};
@@ -440,7 +440,7 @@ AqlQueue* aql_queue(int device) {
     tried[device] = true;
     queues[device] = create(device);
     // the warm thread (warm_main) lives as long as the process, like the queues
-    if (queues[device] && warm_period().count() > 0) std::thread(warm_main, queues[device]).detach();
+    if (queues[device]) std::thread(warm_main, queues[device]).detach();
   }
   AqlQueue* q = queues[device];
   return (q && !q->failed.load()) ? q : nullptr;
@@ -827,6 +827,7 @@ void heartbeat_locked(AqlQueue* a) {
                           (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   publish_packet(q, p, header, idx, a->wc_ring);
+  a->heartbeats.fetch_add(1, std::memory_order_relaxed);
 }
 
 // Keeping the dispatch side awake.  Once no packet of the process has reached the GPU for
@@ -836,26 +837,24 @@ void heartbeat_locked(AqlQueue* a) {
 // barrier-AND packet every 40 us does (5.4-5.9 us, profiles/r05_small_lat_heartbeat_zb.jsonl).
 // So while the process is sending, this thread wakes every `period` and, when nothing was
 // dispatched since its last wake, publishes one such packet; kWarmWindow after the last dispatch
-// it parks until the next.  DORA_GPU_WARM_US sets the period (default 25; 0 turns it off).
+// it parks until the next.  dora_gpu_set_keep_awake sets the period (default 25 us; 0: off).
 constexpr auto kWarmWindow = std::chrono::milliseconds(100);
-
-std::chrono::nanoseconds warm_period() {
-  static const std::chrono::nanoseconds p = [] {
-    const char* e = std::getenv("DORA_GPU_WARM_US");
-    const double us = e ? std::atof(e) : 25.0;
-    return std::chrono::nanoseconds(us > 0 ? int64_t(std::max(us, 5.0) * 1000) : 0);
-  }();
-  return p;
-}
+std::atomic<int64_t> g_warm_period_ns{25000};
 
 void warm_main(AqlQueue* a) {
   (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // wake on time, not up to 50 us late
-  const auto period = warm_period();
   using clock = std::chrono::steady_clock;
   uint64_t seen = a->activity.load(std::memory_order_relaxed);
   auto last_change = clock::now();
   auto next = last_change;
   while (!a->failed.load(std::memory_order_relaxed)) {
+    const auto period = std::chrono::nanoseconds(g_warm_period_ns.load(std::memory_order_relaxed));
+    if (period.count() <= 0) {  // off: look again every 10 ms
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      seen = a->activity.load(std::memory_order_relaxed);
+      last_change = next = clock::now();
+      continue;
+    }
     next += period;
     std::this_thread::sleep_until(next);
     auto now = clock::now();
@@ -995,6 +994,22 @@ std::atomic<bool> g_cp_lone{true};  // lone single-segment packs above the windo
 }  // namespace
 
 void aql_cp_lone(bool on) { g_cp_lone.store(on); }
+
+uint64_t aql_heartbeats(int device, bool* parked) {
+  if (device < 0 || device >= 64) return 0;
+  AqlQueue* a;
+  {
+    std::lock_guard<std::mutex> g(g_queues_mu);
+    a = g_queues[device];
+  }
+  if (!a) return 0;
+  if (parked) *parked = a->warm_parked.load();
+  return a->heartbeats.load();
+}
+
+void aql_keep_awake(double period_us) {
+  g_warm_period_ns.store(period_us > 0 ? int64_t(std::max(period_us, 5.0) * 1000) : 0);
+}
 
 void aql_mid_queues(int create, int use) {
   if (create > 0) g_create_queues.store(create);

@@ -70,6 +70,10 @@ int aql_hold(int device, bool hold);
 // Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
 // in-kernel (test hook, probes of the synchronous send).
 void aql_cp_lone(bool on);
+// Period of the warm thread's empty packets (aql.cpp warm_main; 0: off; at least 5 us).
+void aql_keep_awake(double period_us);
+// Test tool: empty packets the warm thread of `device` has published, and whether it is parked.
+uint64_t aql_heartbeats(int device, bool* parked);
 // Test tool: one empty barrier-AND packet (no dependencies, no completion signal) on the first
 // queue of `device` (latency probe: does a packet keep the dispatch side awake).
 int aql_heartbeat(int device);

@@ -67,6 +67,12 @@ int dora_gpu_aql_cp_signalled(int device, uint64_t* count) {
   return DORA_OK;
 }
 
+int dora_gpu_set_keep_awake(double period_us) {
+  if (!(period_us >= 0)) return dora::fail(DORA_ERR_INVALID, "keep-awake period must be >= 0");
+  dora::aql_keep_awake(period_us);
+  return DORA_OK;
+}
+
 int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs,
                              uint64_t* backlogged) {
   uint64_t a = 0, b = 0, c = 0;

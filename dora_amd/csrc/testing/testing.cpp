@@ -234,6 +234,14 @@ int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double
   return DORA_OK;
 }
 
+int dora_gpu_test_keep_awake_stats(int device, uint64_t* heartbeats, int* parked) {
+  if (!heartbeats || !parked) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  bool pk = false;
+  *heartbeats = dora::aql_heartbeats(device, &pk);
+  *parked = pk ? 1 : 0;
+  return DORA_OK;
+}
+
 int dora_gpu_test_heartbeat_stop(void* p) {
   auto* h = static_cast<Heartbeat*>(p);
   if (!h) return DORA_OK;

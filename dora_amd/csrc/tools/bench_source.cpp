@@ -79,6 +79,8 @@ int main() {
   // the benchmark node never rewrites its sources: sends return as soon as their pack is queued
   // (DORA_SEND_ASYNC; DORA_BENCH_SYNC_SENDS=1 measures the default synchronous sends instead)
   if (env_long("DORA_BENCH_SYNC_SENDS", 0) == 0) dora_node_set_async_sends(node, 1);
+  // bench.py --keep-awake-us: the warm thread's period (dora_gpu_set_keep_awake; 0: off)
+  if (const char* v = std::getenv("DORA_BENCH_KEEP_AWAKE_US")) dora_gpu_set_keep_awake(std::atof(v));
   const char* out_path = std::getenv("DORA_BENCH_RESULT");
   const auto lat_sizes = env_sizes("DORA_BENCH_LAT_SIZES");
   const long lat_n = env_long("DORA_BENCH_LAT_N", 30);

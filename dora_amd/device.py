@@ -109,6 +109,13 @@ def aql_dispatch_counts(device: int = 0) -> dict:
     return {lib.dora_gpu_aql_kernel_name(k).decode(): c[k] for k in range(n.value)}
 
 
+def set_keep_awake(period_us: float = 25.0) -> None:
+    """While this process sends device samples, keep the GPU's command processor from idling:
+    an empty AQL packet whenever nothing was dispatched for `period_us` (0: off;
+    dora_gpu_set_keep_awake).  Process-wide."""
+    call("dora_gpu_set_keep_awake", float(period_us))
+
+
 def aql_cp_signalled(device: int = 0) -> int:
     """Packs whose fill the command processor signalled (aql.cpp aql_cp_candidate)."""
     a = c_uint64()

@@ -104,6 +104,12 @@ int dora_gpu_aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_ms
  * packet's completion signal instead of the in-kernel flag store; mid-size single-segment packs
  * of 1-32 MiB, and synchronous single-segment sends from 1 MiB). */
 int dora_gpu_aql_cp_signalled(int device, uint64_t* count);
+/* Latency control (no reference counterpart): while this process sends device samples, a thread
+ * per GPU publishes an empty AQL packet whenever nothing was dispatched for `period_us`, so the
+ * command processor never idles long enough to need waking (~5.5 us per message otherwise, for
+ * messages more than ~50 us apart); it parks 100 ms after the last send.  Default 25 us; 0 turns
+ * it off (saves the thread's wake-ups); values below 5 are raised to 5.  Process-wide. */
+int dora_gpu_set_keep_awake(double period_us);
 
 int dora_gpu_device_count(int* count);
 int dora_gpu_set_device(int ordinal);

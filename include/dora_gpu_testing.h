@@ -54,6 +54,9 @@ int dora_gpu_test_cp_lone(int on);
 int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double seconds,
                                   void** out);
 int dora_gpu_test_heartbeat_stop(void* h);
+/* Test tool: empty packets the keep-awake thread of `device` has published in this process
+ * (dora_gpu_set_keep_awake), and whether it is parked (no send for 100 ms). */
+int dora_gpu_test_keep_awake_stats(int device, uint64_t* heartbeats, int* parked);
 /* Test tool (latency probe): one resident wave on `device` that sleeps until
  * dora_gpu_test_keep_warm_stop (or `seconds`, at most 600) so the GPU never idles. */
 int dora_gpu_test_keep_warm_start(int device, double seconds, void** out);

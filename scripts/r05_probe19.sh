@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-5 probes, nineteenth set: the warm thread against a HIP stream of the same process
 # (scripts/warm_copy_probe.py, off / on, two rounds), then the GPU tests with it on.
+# (profiles/r05_warm_copy_zd.jsonl was run at commit 395dc61, where an environment variable set
+# the period; --keep-awake-us does the same.)
 # usage: bash scripts/r05_probe19.sh <out dir under gpurun_out>
 set -euo pipefail
 out=${1:?out dir}
@@ -8,7 +10,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 for r in 0 1; do
   for w in 0 25; do
-    DORA_GPU_WARM_US=$w timeout -k 10 120 python -u scripts/warm_copy_probe.py --n 300 \
+    timeout -k 10 120 python -u scripts/warm_copy_probe.py --n 300 --keep-awake-us $w \
       >> "$out/warm_copy.jsonl" 2>> "$out/warm_copy.err"
   done
 done

@@ -56,6 +56,8 @@ def main():
                          "(dora_gpu_test_heartbeat_start): 1 empty AQL packet, 2 PCIe read, "
                          "3 PCIe write; 0 none")
     ap.add_argument("--period", type=float, default=40.0, help="heartbeat period, us")
+    ap.add_argument("--keep-awake-us", type=float, default=None,
+                    help="dora_gpu_set_keep_awake period (0: off; default: the library's)")
     a = ap.parse_args()
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
@@ -71,6 +73,8 @@ def main():
                     "throughput": {"source": "node/throughput", "queue_size": 10}},
          "env": {"DORA_BENCH_RESULT": res}, "_unstable_deploy": {"gpu": 0}},
     ]}
+    if a.keep_awake_us is not None:
+        device.set_keep_awake(a.keep_awake_us)
     df = Dataflow(desc).start()
     node = Node("node", dataflow=df.shm, device=0)
     stream = device.Stream()
@@ -131,7 +135,8 @@ def main():
             ev.setdefault(r["token"], {}).setdefault(int(r["point"]), int(r["t_ns"]))
     for label, z, gap, _ in CASES:
         s = series.get(z, {})
-        row = {"case": label, "warm": a.warm, "heartbeat": a.heartbeat, "period_us": a.period, "bytes": z, "gap_us": gap, "n": s.get("n"),
+        row = {"case": label, "warm": a.warm, "heartbeat": a.heartbeat, "period_us": a.period,
+               "keep_awake_us": a.keep_awake_us, "bytes": z, "gap_us": gap, "n": s.get("n"),
                "latency_p50_us": s.get("p50_us"), "latency_p99_us": s.get("p99_us"),
                "incl_send_p50_us": s.get("full_p50_us")}
         lo, hi = t_case[label]

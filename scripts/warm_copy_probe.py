@@ -3,9 +3,9 @@
 process's other GPU work?  The pattern of tests/test_gpu_dataflow.py
 test_device_array_send_waits_for_its_source, timed: a synchronous device send, then a 4 MiB
 hipMemcpyAsync on a HIP stream of the same process and its synchronize (timed), 1 ms apart.
-Run once per DORA_GPU_WARM_US setting.
+Run once per setting of the warm thread's period (dora_gpu_set_keep_awake).
 
-    DORA_GPU_WARM_US=0 python scripts/warm_copy_probe.py --n 300
+    python scripts/warm_copy_probe.py --n 300 --keep-awake-us 0
 """
 import argparse
 import json
@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=300)
     ap.add_argument("--bytes", type=int, default=4 << 20)
+    ap.add_argument("--keep-awake-us", type=float, default=None)
     a = ap.parse_args()
     from dora_amd import device
     from dora_amd._lib import call
@@ -33,6 +34,9 @@ def main():
          "env": {"DORA_BENCH_RESULT": os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                                    f"warm-copy-{os.getpid()}.json")}},
     ]}
+    if a.keep_awake_us is not None:
+        device.set_keep_awake(a.keep_awake_us)
+    cpu0 = time.process_time()
     with Dataflow(desc) as df:
         node = Node("node", dataflow=df.shm, device=0)
         src, dst = device.DeviceBuffer(a.bytes), device.DeviceBuffer(a.bytes)
@@ -49,6 +53,7 @@ def main():
                 send_us.append((t1 - t0) * 1e6)
                 copy_us.append((t2 - t1) * 1e6)
             time.sleep(0.001)
+        cpu_s = time.process_time() - cpu0
         other.close()
         src.free()
         dst.free()
@@ -58,7 +63,8 @@ def main():
     def q(xs, f):
         xs = sorted(xs)
         return round(xs[min(len(xs) - 1, int(f * len(xs)))], 2)
-    print(json.dumps({"warm_us": os.environ.get("DORA_GPU_WARM_US", "default"), "n": a.n,
+    print(json.dumps({"keep_awake_us": a.keep_awake_us, "n": a.n,
+                      "process_cpu_s": round(cpu_s, 3),
                       "copy_bytes": a.bytes,
                       "copy_sync_us": {"p50": q(copy_us, 0.5), "p90": q(copy_us, 0.9),
                                        "p99": q(copy_us, 0.99), "max": round(max(copy_us), 2)},
