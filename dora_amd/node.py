@@ -217,31 +217,28 @@ class Node:
     # ------------------------------------------------------------------------------ receiving
     def next(self, timeout: Optional[float] = None):
         """Next event dict, or None when the stream has ended (or on timeout)."""
-        h = c_void_p()
-        rc = self._lib.dora_node_next_event(self.handle, -1 if timeout is None
-                                            else int(timeout * 1e6), byref(h))
-        if rc in (-5, -6):   # closed / timeout
-            return None
-        _lib.check(rc)
-        ev = _EventHandle(h.value)
-        kind = EVENT_TYPES.get(self._lib.dora_event_type(ev.ptr), "UNKNOWN")
+        # one native call: the event's fields, its decoded parameters and its data's address
+        r = _fast.next_event(self.handle, -1 if timeout is None else int(timeout * 1e6))
+        if r.__class__ is int:
+            if r in (-5, -6):   # closed / timeout
+                return None
+            _lib.check(r)
+        ptr, t, eid, params, ts, dptr, dlen, on_dev, err = r
+        ev = _EventHandle(ptr)
+        kind = EVENT_TYPES.get(t, "UNKNOWN")
         if kind == "ALL_INPUTS_CLOSED":
             ev.free()
             return None
-        out = _Event(type=kind, id=self._lib.dora_event_id(ev.ptr).decode())
+        out = _Event(type=kind, id=eid)
         if kind == "ERROR":
-            out["error"] = self._lib.dora_event_error(ev.ptr).decode()
+            out["error"] = err
         if kind == "INPUT":
-            p, n = ctypes.POINTER(c_uint8)(), c_size_t()
-            call("dora_event_parameters", ev.ptr, byref(p), byref(n))
-            out["metadata"] = decode_parameters(ctypes.string_at(p, n.value) if n.value else b"")
-            out["timestamp_ns"] = self._lib.dora_event_timestamp_ns(ev.ptr)
+            out["metadata"] = params
+            out["timestamp_ns"] = ts
             out["_event"] = ev  # "type_info" is decoded on first access (_Event)
-            dp, dn = c_void_p(), c_size_t()
-            call("dora_event_data", ev.ptr, byref(dp), byref(dn))
-            out["data_ptr"], out["data_len"] = dp.value, dn.value
-            out["on_device"] = bool(self._lib.dora_event_is_device(ev.ptr))
-            if dn.value == 0:       # RawData::Vec(empty) -> ArrayData::new_empty(data_type)
+            out["data_ptr"], out["data_len"] = (dptr or None), dlen
+            out["on_device"] = bool(on_dev)
+            if dlen == 0:       # RawData::Vec(empty) -> ArrayData::new_empty(data_type)
                 import pyarrow as pa
                 out["value"] = pa.array([], type=out["type_info"].arrow_type())
             elif out["on_device"]:
@@ -266,28 +263,15 @@ class Node:
     def wait_input(self, input_id: str, key: str, value, timeout: float = 60.0) -> dict:
         """Wait for an input event on `input_id` whose parameters have `key == value` and return
         its parameters; other events are skipped.  A control-message fast path: only the id and
-        the parameters are decoded (no data mapping, no Arrow value), so the wait costs about one
-        ring hop, not a Python event construction."""
-        lib, h = self._lib, c_void_p()
-        p, n = ctypes.POINTER(c_uint8)(), c_size_t()
-        want = input_id.encode()
-        deadline = time.monotonic() + timeout
-        while True:
-            left = deadline - time.monotonic()
-            if left <= 0:
+        the parameters are decoded (no data mapping, no Arrow value), in one native call
+        (_dora_node.wait_input), so the wait costs about one ring hop, not a Python event
+        construction."""
+        r = _fast.wait_input(self.handle, input_id, key, value, int(timeout * 1e6))
+        if r.__class__ is int:
+            if r == -6:
                 raise TimeoutError(f"no `{input_id}` input with {key}={value!r}")
-            rc = lib.dora_node_next_event(self.handle, int(left * 1e6), byref(h))
-            if rc == -6:
-                continue
-            _lib.check(rc)
-            try:
-                if lib.dora_event_type(h) == 1 and lib.dora_event_id(h) == want:
-                    call("dora_event_parameters", h, byref(p), byref(n))
-                    meta = decode_parameters(ctypes.string_at(p, n.value) if n.value else b"")
-                    if meta.get(key) == value:
-                        return meta
-            finally:
-                lib.dora_event_free(h)
+            _lib.check(r)
+        return r
 
     def __iter__(self):
         while True:

@@ -85,6 +85,40 @@ def test_native_parameter_encoding_matches_python():
         encode_parameters([("a", 1)])
 
 
+def test_native_receive_decodes_parameters_and_waits():
+    """Node.next and Node.wait_input decode parameters natively (csrc/pyext.cpp next_event /
+    wait_input): every value kind arrives as decode_parameters reads the same bytes; wait_input
+    skips other inputs and ids, returns the matching parameters and raises TimeoutError."""
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["o", "p"]},
+        {"id": "b", "inputs": {"i": {"source": "a/o", "queue_size": 100},
+                               "j": {"source": "a/p", "queue_size": 100}}}]})
+    nodes = _start_nodes(d.shm, ["a", "b"])
+    a, b = nodes["a"], nodes["b"]
+    cases = [None, {}, {"seq": 0}, {"b": False, "a": True, "c": -1},
+             {"t_start": 1760000000123456789, "seq": 2 ** 63 - 1, "neg": -2 ** 63},
+             {"s": "", "u": "héllo ☃", "f": 2.5}, {"k" * 300: "v" * 5000}]
+    for k, p in enumerate(cases):
+        a.send_output("o", bytes([k]) * 3, p)
+    for k, p in enumerate(cases):
+        ev = b.next(timeout=5)
+        assert ev["type"] == "INPUT" and ev["id"] == "i"
+        assert ev["metadata"] == decode_parameters(encode_parameters(p)), p
+        assert as_bytes(ev["value"]) == bytes([k]) * 3
+    for s in range(5):
+        a.send_output("p", b"", {"seq": s})
+        a.send_output("o", b"x", {"seq": s})
+    assert b.wait_input("i", "seq", 3, 5.0) == {"seq": 3}
+    assert b.wait_input("j", "seq", 4, 5.0) == {"seq": 4}   # the rest were consumed
+    t0 = time.monotonic()
+    with pytest.raises(TimeoutError):
+        b.wait_input("i", "seq", 99, 0.2)
+    assert time.monotonic() - t0 < 2.0
+    a.close()
+    b.close()
+    d.join()
+
+
 def test_descriptor_validation():
     with pytest.raises(ValueError, match="unknown output"):
         parse_descriptor({"nodes": [{"id": "a", "inputs": {"x": "b/y"}}, {"id": "b"}]})
