@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -407,7 +408,55 @@ PyObject* py_wait_input(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   }
 }
 
+// export_array(event_ptr) -> status (int) | (array_addr, schema_addr): the input's Arrow C
+// structs (dora_event_array) in memory of this module, for pyarrow's _import_from_c, which moves
+// their contents out; free_arrow(array_addr, schema_addr) then releases what is left and frees
+// them (one native call each instead of two ctypes structures and a ctypes call).
+PyObject* py_export_array(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 1) {
+    PyErr_SetString(PyExc_TypeError, "export_array(event_ptr)");
+    return nullptr;
+  }
+  void* ev = nullptr;
+  if (!as_ptr(args[0], &ev)) return nullptr;
+  auto* a = static_cast<ArrowArray*>(std::calloc(1, sizeof(ArrowArray)));
+  auto* s = static_cast<ArrowSchema*>(std::calloc(1, sizeof(ArrowSchema)));
+  if (!a || !s) {
+    std::free(a);
+    std::free(s);
+    return PyErr_NoMemory();
+  }
+  const int rc = dora_event_array(static_cast<const dora_event*>(ev), a, s);
+  if (rc != 0) {
+    std::free(a);
+    std::free(s);
+    return PyLong_FromLong(rc);
+  }
+  return Py_BuildValue("(KK)", static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(a)),
+                       static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(s)));
+}
+
+PyObject* py_free_arrow(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2) {
+    PyErr_SetString(PyExc_TypeError, "free_arrow(array_addr, schema_addr)");
+    return nullptr;
+  }
+  void *a = nullptr, *s = nullptr;
+  if (!as_ptr(args[0], &a) || !as_ptr(args[1], &s)) return nullptr;
+  auto* arr = static_cast<ArrowArray*>(a);
+  auto* sch = static_cast<ArrowSchema*>(s);
+  if (arr && arr->release) arr->release(arr);  // not imported (an error before the move)
+  if (sch && sch->release) sch->release(sch);
+  std::free(arr);
+  std::free(sch);
+  Py_RETURN_NONE;
+}
+
 PyMethodDef methods[] = {
+    {"export_array", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_export_array)),
+     METH_FASTCALL, "An input's Arrow C structs (dora_event_array), for pyarrow's _import_from_c."},
+    {"free_arrow", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_free_arrow)),
+     METH_FASTCALL, "Release what is left of export_array's structs and free them."},
     {"next_event", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_next_event)),
      METH_FASTCALL, "dora_node_next_event with the event's fields and decoded parameters."},
     {"wait_input", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_wait_input)),

@@ -253,10 +253,14 @@ class Node:
                 # an inline DataMessage::Vec sample (< 4096 B from a host source), or a host-only
                 # producer's shared memory read in place: a host pyarrow array over its bytes,
                 # as the reference's PyEvent::value; it keeps the input alive
-                a, s = ArrowArray(), ArrowSchema()
-                call("dora_event_array", ev.ptr, byref(a), byref(s))
+                r = _fast.export_array(ev.ptr)
+                if r.__class__ is int:
+                    _lib.check(r)
                 import pyarrow as pa
-                out["value"] = pa.Array._import_from_c(ctypes.addressof(a), ctypes.addressof(s))
+                try:
+                    out["value"] = pa.Array._import_from_c(r[0], r[1])
+                finally:
+                    _fast.free_arrow(r[0], r[1])
         out["_event"] = ev
         return out
 
