@@ -408,6 +408,124 @@ PyObject* py_wait_input(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   }
 }
 
+// A pyarrow type's exported ArrowSchema, kept: a send lends it (dora_node_send_output borrows
+// the schema), so a node sending arrays of one type exports each array only, not its type again
+// (~3 us for a struct).  Looked up by the type object itself first, then by equality (a new
+// array of an equal type) confirmed with field metadata (DataType.__eq__ ignores it, the
+// serialized type keeps it); at most 64 types are kept.
+void free_schema_capsule(PyObject* cap) {
+  auto* s = static_cast<ArrowSchema*>(PyCapsule_GetPointer(cap, "dora_schema"));
+  if (s && s->release) s->release(s);
+  std::free(s);
+}
+
+PyObject* g_schemas = nullptr;   // type -> (type, capsule)
+PyObject* g_last_type = nullptr;  // the last type sent and its capsule (strong references)
+PyObject* g_last_cap = nullptr;
+
+// A new reference to the capsule of `type`'s schema.  The caller keeps it for as long as the
+// schema is in use (a send releases the GIL: another thread may evict the entry meanwhile).
+PyObject* schema_for(PyObject* type) {
+  if (type == g_last_type) {
+    Py_INCREF(g_last_cap);
+    return g_last_cap;
+  }
+  if (!g_schemas && !(g_schemas = PyDict_New())) return nullptr;
+  PyObject* cap = nullptr;
+  PyObject* hit = PyDict_GetItemWithError(g_schemas, type);  // borrowed (type, capsule)
+  if (!hit && PyErr_Occurred()) return nullptr;
+  if (hit) {
+    PyObject* key = PyTuple_GET_ITEM(hit, 0);
+    int same = key == type;
+    if (!same) {
+      // type.equals(key, check_metadata=True)
+      static PyObject* kw = Py_BuildValue("{s:O}", "check_metadata", Py_True);
+      PyObject* eq = kw ? PyObject_GetAttrString(type, "equals") : nullptr;
+      PyObject* a = eq ? PyTuple_Pack(1, key) : nullptr;
+      PyObject* r = a ? PyObject_Call(eq, a, kw) : nullptr;
+      Py_XDECREF(a);
+      Py_XDECREF(eq);
+      if (!r) return nullptr;
+      same = PyObject_IsTrue(r);
+      Py_DECREF(r);
+      if (same < 0) return nullptr;
+    }
+    if (same) {
+      cap = PyTuple_GET_ITEM(hit, 1);
+      Py_INCREF(cap);
+    }
+  }
+  if (!cap) {  // export it (replacing an entry equal but for field metadata)
+    if (PyDict_GET_SIZE(g_schemas) >= 64) PyDict_Clear(g_schemas);
+    auto* sc = static_cast<ArrowSchema*>(std::calloc(1, sizeof(ArrowSchema)));
+    if (!sc) return PyErr_NoMemory();
+    PyObject* r = PyObject_CallMethod(type, "_export_to_c", "K",
+                                      static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(sc)));
+    if (!r) {
+      std::free(sc);
+      return nullptr;
+    }
+    Py_DECREF(r);
+    cap = PyCapsule_New(sc, "dora_schema", free_schema_capsule);
+    if (!cap) {
+      if (sc->release) sc->release(sc);
+      std::free(sc);
+      return nullptr;
+    }
+    PyObject* entry = PyTuple_Pack(2, type, cap);
+    if (!entry || PyDict_SetItem(g_schemas, type, entry) < 0) {
+      Py_XDECREF(entry);
+      Py_DECREF(cap);
+      return nullptr;
+    }
+    Py_DECREF(entry);
+  }
+  Py_INCREF(type);
+  Py_XSETREF(g_last_type, type);
+  Py_INCREF(cap);
+  Py_XSETREF(g_last_cap, cap);
+  return cap;
+}
+
+// send_pyarrow(handle, output_id, array, metadata) -> status: a host pyarrow.Array, exported
+// (its type's schema from schema_for) and sent as dora_node_send_output of a host source, which
+// copies it before returning (apis/python/node/src/lib.rs:157-185 -> arrow_utils.rs:23-71).
+PyObject* py_send_pyarrow(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "send_pyarrow(handle, output_id, array, metadata)");
+    return nullptr;
+  }
+  void* h = nullptr;
+  if (!as_ptr(args[0], &h)) return nullptr;
+  const char* oid = as_cstr(args[1]);
+  if (!oid) return nullptr;
+  PyObject* type = PyObject_GetAttrString(args[2], "type");
+  if (!type) return nullptr;
+  PyObject* cap = schema_for(type);
+  Py_DECREF(type);
+  if (!cap) return nullptr;
+  auto* schema = static_cast<ArrowSchema*>(PyCapsule_GetPointer(cap, "dora_schema"));
+  std::string& params = t_params;
+  ArrowArray a{};
+  PyObject* r = encode(args[3], params) && schema
+                    ? PyObject_CallMethod(args[2], "_export_to_c", "K",
+                                          static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(&a)))
+                    : nullptr;
+  if (!r) {
+    Py_DECREF(cap);
+    return nullptr;
+  }
+  Py_DECREF(r);
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = dora_node_send_output_ex(static_cast<dora_node*>(h), oid, &a, schema, ARROW_DEVICE_CPU,
+                                reinterpret_cast<const uint8_t*>(params.data()), params.size(), 0);
+  Py_END_ALLOW_THREADS
+  if (a.release) a.release(&a);
+  Py_DECREF(cap);
+  return PyLong_FromLong(rc);
+}
+
 // export_array(event_ptr) -> status (int) | (array_addr, schema_addr): the input's Arrow C
 // structs (dora_event_array) in memory of this module, for pyarrow's _import_from_c, which moves
 // their contents out; free_arrow(array_addr, schema_addr) then releases what is left and frees
@@ -453,6 +571,8 @@ PyObject* py_free_arrow(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
 }
 
 PyMethodDef methods[] = {
+    {"send_pyarrow", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_send_pyarrow)),
+     METH_FASTCALL, "dora_node_send_output of a host pyarrow.Array (its type's schema kept)."},
     {"export_array", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_export_array)),
      METH_FASTCALL, "An input's Arrow C structs (dora_event_array), for pyarrow's _import_from_c."},
     {"free_arrow", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(py_free_arrow)),

@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes
 import os
 import struct
+import sys
 import time
 from ctypes import byref, c_double, c_size_t, c_uint8, c_uint64, c_void_p
 from typing import Optional
@@ -101,6 +102,11 @@ def decode_parameters(raw: bytes) -> dict:
     return out
 
 
+def _is_pyarrow_array(data) -> bool:
+    pa = sys.modules.get("pyarrow")  # an Array exists only once pyarrow is imported
+    return pa is not None and isinstance(data, pa.Array)
+
+
 class _EventHandle:
     """Owns a C dora_event; freeing it (explicitly or by GC) releases the drop token once no
     DeviceArray view references the sample any more."""
@@ -166,6 +172,9 @@ class Node:
         elif isinstance(data, DeviceBuffer):
             rc = _fast.send_bytes(self.handle, output_id, data.ptr, data.size, ARROW_DEVICE_ROCM,
                                   metadata, f)
+        elif _is_pyarrow_array(data):
+            # exported natively; the type's schema is exported once and lent to later sends
+            rc = _fast.send_pyarrow(self.handle, output_id, data, metadata)
         elif hasattr(data, "_export_to_c"):
             with CArray.from_pyarrow(data) as c:
                 rc = _fast.send_array(self.handle, output_id, ctypes.addressof(c.array),

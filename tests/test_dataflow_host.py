@@ -119,6 +119,56 @@ def test_native_receive_decodes_parameters_and_waits():
     d.join()
 
 
+def test_native_pyarrow_send_matches_export_path():
+    """send_output of a host pyarrow.Array goes through _dora_node.send_pyarrow (its type's
+    schema exported once and lent to later sends): every input equals the one the generic
+    _export_to_c path delivers for the same array — value and ArrowTypeInfo — for primitive,
+    nullable, sliced, string, struct and list<struct> arrays, and for two struct types equal but
+    for their field metadata sent alternately."""
+    import pyarrow as pa
+
+    class Exported:  # not a pyarrow.Array: takes the generic CArray.from_pyarrow path
+        def __init__(self, a):
+            self.a = a
+
+        def _export_to_c(self, *args):
+            return self.a._export_to_c(*args)
+    pts = pa.StructArray.from_arrays(
+        [pa.array([1.5, None, 3.0], pa.float32()), pa.array([7, 8, 9], pa.uint8())],
+        names=["x", "i"], mask=pa.array([False, False, True]))
+    f1 = pa.struct([pa.field("a", pa.int32(), metadata={"u": "m"})])
+    f2 = pa.struct([pa.field("a", pa.int32(), metadata={"u": "mm"})])
+    arrays = [pa.array(list(range(100)), pa.uint8()),
+              pa.array([1, None, -3, 2 ** 40], pa.int64()),
+              pa.array(list(range(50)), pa.int16()).slice(7, 20),
+              pa.array(["a", None, "héllo", ""]),
+              pts, pa.array([[{"x": 1.0, "i": 2}], None, [], [{"x": None, "i": 5}] * 3],
+                            pa.list_(pa.struct([("x", pa.float32()), ("i", pa.uint8())]))),
+              pa.array([{"a": 1}, {"a": 2}], f1), pa.array([{"a": 3}], f2),
+              pa.array([{"a": 4}], f1)]
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["o"]},
+        {"id": "b", "inputs": {"i": {"source": "a/o", "queue_size": 1000}}}]})
+    nodes = _start_nodes(d.shm, ["a", "b"])
+    a, b = nodes["a"], nodes["b"]
+    for k, arr in enumerate(arrays):
+        a.send_output("o", arr, {"k": k, "native": True})
+        a.send_output("o", Exported(arr), {"k": k, "native": False})
+    got = {}
+    for _ in range(2 * len(arrays)):
+        ev = b.next(timeout=5)
+        assert ev["type"] == "INPUT"
+        m = ev["metadata"]
+        got[(m["k"], m["native"])] = (ev["value"], ev["type_info"].to_json())
+    for k, arr in enumerate(arrays):
+        (v1, t1), (v0, t0) = got[(k, True)], got[(k, False)]
+        assert t1 == t0, k
+        assert v1.equals(v0) and v1.equals(arr), k
+    a.close()
+    b.close()
+    d.join()
+
+
 def test_descriptor_validation():
     with pytest.raises(ValueError, match="unknown output"):
         parse_descriptor({"nodes": [{"id": "a", "inputs": {"x": "b/y"}}, {"id": "b"}]})
