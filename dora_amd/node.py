@@ -262,14 +262,15 @@ class Node:
                 # an inline DataMessage::Vec sample (< 4096 B from a host source), or a host-only
                 # producer's shared memory read in place: a host pyarrow array over its bytes,
                 # as the reference's PyEvent::value; it keeps the input alive
-                r = _fast.export_array(ev.ptr)
+                # (its type from a cache keyed by the schema: no schema import per event)
+                r = _fast.export_typed(ev.ptr)
                 if r.__class__ is int:
                     _lib.check(r)
                 import pyarrow as pa
                 try:
                     out["value"] = pa.Array._import_from_c(r[0], r[1])
                 finally:
-                    _fast.free_arrow(r[0], r[1])
+                    _fast.free_arrow(r[0], 0)
         out["_event"] = ev
         return out
 

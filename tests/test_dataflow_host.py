@@ -124,7 +124,8 @@ def test_native_pyarrow_send_matches_export_path():
     schema exported once and lent to later sends): every input equals the one the generic
     _export_to_c path delivers for the same array — value and ArrowTypeInfo — for primitive,
     nullable, sliced, string, struct and list<struct> arrays, and for two struct types equal but
-    for their field metadata sent alternately."""
+    for their field metadata sent alternately (the receiver's DataType cache, keyed by schema,
+    must keep them apart too: the received types carry their own field metadata)."""
     import pyarrow as pa
 
     class Exported:  # not a pyarrow.Array: takes the generic CArray.from_pyarrow path
@@ -164,6 +165,7 @@ def test_native_pyarrow_send_matches_export_path():
         (v1, t1), (v0, t0) = got[(k, True)], got[(k, False)]
         assert t1 == t0, k
         assert v1.equals(v0) and v1.equals(arr), k
+        assert v1.type.equals(arr.type, check_metadata=True), (k, v1.type, arr.type)
     a.close()
     b.close()
     d.join()
