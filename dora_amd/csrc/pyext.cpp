@@ -349,11 +349,14 @@ PyObject* py_next_event(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     params = Py_None;
   }
   const char* err = type == DORA_EVENT_ERROR ? dora_event_error(ev) : "";
-  return Py_BuildValue("(KisNKKnis)", static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(ev)),
-                       type, dora_event_id(ev), params,
-                       static_cast<unsigned long long>(dora_event_timestamp_ns(ev)),
-                       static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(dp)),
-                       static_cast<Py_ssize_t>(dn), dev, err);
+  PyObject* out =
+      Py_BuildValue("(KisNKKnis)", static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(ev)),
+                    type, dora_event_id(ev), params,
+                    static_cast<unsigned long long>(dora_event_timestamp_ns(ev)),
+                    static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(dp)),
+                    static_cast<Py_ssize_t>(dn), dev, err);
+  if (!out) dora_event_free(ev);  // (an id or error that is not UTF-8)
+  return out;
 }
 
 // wait_input(handle, input_id, key, value, timeout_us) -> status (int) | parameters: the next
