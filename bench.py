@@ -38,7 +38,16 @@ LADDER = [4096, 16384, 40960, 65536, 409600, 1 << 20, 4096000, 4 << 20, 16 << 20
 LADDER_SMALL = [0, 8, 64, 512, 2048]
 # host-resident sources of the latency ladder (output `latency_host`): below 4096 B they travel
 # inline as the reference's DataMessage::Vec (no slot, no GPU), 4096 B is an H2D device sample
-LADDER_HOST = [8, 512, 2048, 4096]
+LADDER_HOST = [8, 512, 2048, 4096, 65536, 4 << 20, 6220800, 40960000]
+# device-resident sources delivered to a node without a GPU (`hostsink`, DORA_GPU_DEVICE -1):
+# staged to host memory on receipt, the reference's host ArrowData (event.rs:35-91)
+LADDER_D2H = [8, 4096, 65536, 1 << 20, 6220800, 40960000]
+
+
+def host_lat_n(size, lat_n):
+    """Latency-mode messages per host-source / host-receiver size: the full count up to 64 KB,
+    200 above (a 40.96 MB message crosses PCIe in ~0.75 ms)."""
+    return lat_n if size <= 65536 else min(lat_n, 200)
 
 
 def parse():
@@ -145,6 +154,34 @@ def box_copy_rate(size: int, stream, n_src: int = 8, reps: int = 24):
         e0.close(); e1.close(); dst.free()
         for b in srcs:
             b.free()
+
+
+def box_h2d_rate(size: int, stream, reps: int = 10):
+    """PCIe DMA of `size` bytes between pinned host memory and HBM on this box (hipMemcpyAsync,
+    events on one stream), both directions: the H2D / D2H roofline the host paths are measured
+    against (host sources, host-only receivers)."""
+    from ctypes import c_void_p, byref
+    from dora_amd import device
+    from dora_amd._lib import call
+    h = c_void_p()
+    call("dora_gpu_host_alloc", byref(h), size)
+    d = device.DeviceBuffer(size)
+    e0, e1 = device.Event(), device.Event()
+    out = {"bytes": size}
+    try:
+        for name, dst, src in (("h2d", d.ptr, h.value), ("d2h", h.value, d.ptr)):
+            call("dora_gpu_memcpy_async", dst, src, size, stream.handle)
+            e0.record(stream)
+            for _ in range(reps):
+                call("dora_gpu_memcpy_async", dst, src, size, stream.handle)
+            e1.record(stream)
+            e1.sync()
+            us = e0.elapsed_ms(e1) * 1e3 / reps
+            out[f"{name}_GBps"] = round(size / (us * 1e-6) / 1e9, 2)
+        return out
+    finally:
+        e0.close(); e1.close(); d.free()
+        call("dora_gpu_host_free", h.value)
 
 
 def aql_kernel_name(workload: str, region_kernels=None) -> str:
@@ -348,23 +385,34 @@ def native_sources(size, resident=False):
     return 1 if resident else max(1, min(64, (640 << 20) // max(size, 1)))
 
 
-def run_native_ladder(launcher, gpu, n=None, timeout=120.0, resident=False):
+# sizes of the sample-path ladder (allocate_data_sample -> kernel writes the slot -> send)
+NATIVE_SAMPLE_SIZES = [4096, 65536, 1 << 20, 4 << 20, 40960000]
+
+
+def run_native_ladder(launcher, gpu, n=None, timeout=120.0, resident=False, sample=False):
     """Throughput mode of the native benchmark node (dora-gpu-bench-source -> -sink, one GPU,
     zero-copy edge) per size: the data plane through its C ABI, as a Rust node would bind it,
     without the Python node's per-send cost.  Sources rotate past the caches unless `resident`
-    (the reference's one buffer per size).  Reported, never raised."""
+    (the reference's one buffer per size).  `sample`: the reference benchmark's own path,
+    allocate_data_sample + a kernel writing the slot in place + send_output_sample (no pack;
+    apis/rust/node/src/node/mod.rs:246-346), with 30 latency messages per size.  Reported,
+    never raised."""
     from dora_amd.dataflow import Dataflow
     out = {}
     n_fixed = n
-    for size in (NATIVE_RESIDENT_SIZES if resident else NATIVE_SIZES):
+    sizes = (NATIVE_SAMPLE_SIZES if sample else
+             NATIVE_RESIDENT_SIZES if resident else NATIVE_SIZES)
+    for size in sizes:
         n = n_fixed or native_ladder_msgs(size)
         tmp = tempfile.mkdtemp(prefix="dora-native-")
         try:
             desc = c4_descriptor(2, tmp, "kernel", tp_n=n, gpu=lambda g: gpu)
             desc["nodes"][0]["env"].update({
                 "DORA_BENCH_TP_SIZE": str(size), "DORA_BENCH_LAT_SIZES": str(size),
-                "DORA_BENCH_LAT_N": "5", "DORA_BENCH_LAT_GAP_US": "1000",
+                "DORA_BENCH_LAT_N": "30" if sample else "5", "DORA_BENCH_LAT_GAP_US": "1000",
                 "DORA_BENCH_TP_SOURCES": str(native_sources(size, resident))})
+            if sample:
+                desc["nodes"][0]["env"]["DORA_BENCH_SAMPLE_PATH"] = "1"
             df = Dataflow(desc, launcher=launcher).start()
             try:
                 codes = df.wait(timeout)
@@ -378,7 +426,13 @@ def run_native_ladder(launcher, gpu, n=None, timeout=120.0, resident=False):
             dropped = sk.get("dropped_inputs", 0) or 0
             if gbps and dropped:
                 gbps = round(gbps * (n - min(dropped, n - 1)) / n, 3)
+            lat = [x for x in sk.get("series", []) if x.get("input") == "latency"]
             out[str(size)] = {"GBps": gbps, "msgs": n, "sink_dropped": dropped,
+                              "lat_p50_us": lat[0]["p50_us"] if lat else None,
+                              "lat_p50_incl_write_us": lat[0]["full_p50_us"] if lat else None,
+                              "verified": sum(x.get("verified", 0) for x in sk.get("series", [])),
+                              "mismatches": sum(x.get("mismatches", 0)
+                                                for x in sk.get("series", [])),
                               "us_per_msg": round(size / (gbps * 1e3), 3) if gbps else None,
                               "hbm_frac_2S": round(2 * gbps / HBM_PEAK_GBPS, 4) if gbps else None,
                               "sources": native_sources(size, resident),
@@ -665,15 +719,24 @@ def main():
     # (DORA_BENCH_LADDER_LATE=1 keeps the old order for A/B).
     native = native_res = None
     ladder_late = os.environ.get("DORA_BENCH_LADDER_LATE") == "1"
+    native_sample = None
     if native_ladder and not ladder_late:
         native = run_native_ladder(launcher, local_rank)
         native_res = run_native_ladder(launcher, local_rank, resident=True)
+        native_sample = run_native_ladder(launcher, local_rank, sample=True)
 
     from dora_amd.dataflow import Dataflow
     result_path = os.path.join(tempfile.mkdtemp(prefix="dora-bench-"), "sink.json")
+    host_result_path = os.path.join(os.path.dirname(result_path), "hostsink.json")
     desc = {"nodes": [
-        {"id": "node", "path": "dynamic", "outputs": ["latency", "latency_host", "throughput"],
-         "inputs": {"ack": "sink/ack"}, "_unstable_deploy": {"gpu": local_rank}},
+        {"id": "node", "path": "dynamic",
+         "outputs": ["latency", "latency_host", "throughput", "to_host"],
+         "inputs": {"ack": "sink/ack", "ack_host": "hostsink/ack"},
+         "_unstable_deploy": {"gpu": local_rank}},
+        # a receiver without a GPU: device samples reach it staged in host memory
+        {"id": "hostsink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"to_host": {"source": "node/to_host", "queue_size": 10}},
+         "env": {"DORA_BENCH_RESULT": host_result_path}, "_unstable_deploy": {"gpu": -1}},
         {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
          "inputs": {"latency": {"source": "node/latency", "queue_size": 10},
                     "latency_host": {"source": "node/latency_host", "queue_size": 10},
@@ -763,6 +826,7 @@ def main():
     _gc.collect()
     _gc.disable()
     copy_cal = box_copy_rate(S, stream)
+    h2d_cal = box_h2d_rate(40960000, stream) if not args.no_ladder else None
     # the same at the mid sizes, where per-message dispatch rather than HBM binds
     copy_mid = {str(z): box_copy_rate(z, stream) for z in (4 << 20, 16 << 20)
                 if z != S and not args.no_ladder}
@@ -833,13 +897,33 @@ def main():
             node.send_output("throughput", host_src[size], {"seq": seq})  # untimed, once
             seq += 1
             time.sleep(args.lat_gap_us / 1e6)
-            for _ in range(args.lat_n):
+            for _ in range(host_lat_n(size, args.lat_n)):
                 node.send_output("latency_host", host_src[size],
                                  {"seq": seq, "t_start": time.time_ns()})
                 seq += 1
                 time.sleep(args.lat_gap_us / 1e6)
         node.send_output("throughput", b"", {"seq": seq, "ack": True})
         wait_ack(seq)
+        seq += 1
+        del host_src
+        # device sources to the receiver without a GPU (staged to host memory there); the first
+        # messages of each size carry their csum64, which the host sink checks on the host
+        for size in LADDER_D2H:
+            b = ladder_bufs.get(size)
+            if b is None:
+                b = ladder_bufs[size] = device.DeviceBuffer(size)
+                device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
+                stream.sync()
+            c = to_i64(device.csum64(b.ptr, size, stream))
+            for k in range(2 + host_lat_n(size, args.lat_n)):
+                meta = {"seq": seq, "t_start": time.time_ns()}
+                if k < 3:
+                    meta.update({"csum": c, "verify": True})
+                node.send_output_device_bytes("to_host", b.ptr, size, meta)
+                seq += 1
+                time.sleep(args.lat_gap_us / 1e6)
+        node.send_output("to_host", b"", {"seq": seq, "ack": True})
+        node.wait_input("ack_host", "seq", seq, 60.0)
         seq += 1
         phase_drops("latency_ladder")
         share_lat1 = cpu_share()
@@ -1040,6 +1124,7 @@ def main():
     stats = node.stats()
     stats["send_phase_us"] = {k: round(v, 2) for k, v in node.send_profile().items()}
     stats["fill_paths"] = node.fill_paths()
+    node_host_paths = node.host_paths()
     # the timed region's packs, each from its own stamps (first workgroup start -> fill signal)
     intervals = node.pack_intervals() if region else []
     # the default (synchronous) send at the headline size: each send returns once its pack has
@@ -1057,6 +1142,8 @@ def main():
     codes = df.wait(120)
     df.stop()
     sink = json.load(open(result_path)) if os.path.exists(result_path) else {"series": []}
+    hostsink = (json.load(open(host_result_path)) if os.path.exists(host_result_path)
+                else {"series": []})
     # the close, split at the sink (realtime clocks of one host): last send -> the sink has the
     # last message (its fill complete) -> ack sent -> the ack is back here
     for a_seq, t_rx, t_ack in sink.get("acks", []):
@@ -1077,6 +1164,7 @@ def main():
         if native_ladder and ladder_late:
             native = run_native_ladder(launcher, local_rank)
             native_res = run_native_ladder(launcher, local_rank, resident=True)
+            native_sample = run_native_ladder(launcher, local_rank, sample=True)
         launcher.close()
     barrier()
     value = total_bytes / t_max / 1e9
@@ -1101,6 +1189,22 @@ def main():
             lat[key] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
                         "p50_incl_pack_us": s["full_p50_us"],
                         "p99_incl_pack_us": s["full_p99_us"], "n": s["n"]}
+    for s in hostsink.get("series", []):
+        if s["input"] == "to_host" and s["size"]:
+            lat[f"d2h_{s['size']}"] = {"p50_us": s["p50_us"], "p99_us": s["p99_us"],
+                                       "p50_incl_pack_us": s["full_p50_us"],
+                                       "p99_incl_pack_us": s["full_p99_us"], "n": s["n"],
+                                       "verified": s["verified"], "mismatches": s["mismatches"]}
+    # host paths as rates against this box's PCIe DMA (pinned <-> HBM, box_h2d): host sources
+    # (BAR writes to 2 MiB, HIP's copy above) and device samples staged for a host-only receiver
+    host_rates = {}
+    for key, z in ([(f"host_{z}", z) for z in LADDER_HOST if z >= 4096] +
+                   [(f"d2h_{z}", z) for z in LADDER_D2H if z >= 4096]):
+        if key in lat and lat[key]["p50_incl_pack_us"]:
+            gbps = z / (lat[key]["p50_incl_pack_us"] * 1e3)
+            peak = (h2d_cal or {}).get("h2d_GBps" if key.startswith("host") else "d2h_GBps")
+            host_rates[key] = {"GBps_p50": round(gbps, 3),
+                               "frac_of_box_dma": round(gbps / peak, 4) if peak else None}
     c2_series = [s for s in sink.get("series", []) if c3 is None or s["size"] != c3["msg_bytes"]]
     verified = sum(s["verified"] for s in c2_series)
     mismatches = sum(s["mismatches"] for s in c2_series)
@@ -1133,6 +1237,8 @@ def main():
         "throughput_per_size_native": native,
         # the reference's one source buffer per size (L2-resident reads up to 16 MB)
         "throughput_per_size_native_resident_source": native_res,
+        # the reference benchmark's path: allocate_data_sample, a kernel writes the slot, send
+        "throughput_per_size_native_sample_path": native_sample,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "vs_box_copy": (round(achieved / (copy_cal["TBps_2S"] * 1e3), 3)
@@ -1162,6 +1268,10 @@ def main():
         # the same box's plain device copy of the message size, measured right before the run:
         # boxes differ (and GPUs are shared), so the pack's rate reads against this
         "box_copy": copy_cal,
+        # PCIe DMA pinned <-> HBM of this box (the host paths' roofline) and the host paths' rates
+        "box_h2d": h2d_cal,
+        "host_path_rates": host_rates,
+        "host_paths": node_host_paths,
         "box_copy_mid": copy_mid,
         "cold_start_send_us": round(cold_send_us, 1),
         "timed_region": region_setup,
@@ -1255,8 +1365,8 @@ def compact_line(line, detail_path):
                            "by_phase": {k: v for k, v in drops.items() if v}}
     lat = line.get("latency_us") or {}
     out["latency_summary"] = {z: [lat[z]["p50_us"], lat[z]["p99_us"], lat[z]["p99_incl_pack_us"]]
-                              for z in ("host_8", "host_2048", "8", "4096", "4194304",
-                                        "40960000") if z in lat}
+                              for z in ("host_8", "host_2048", "host_4096", "d2h_4096", "8",
+                                        "4096", "4194304", "40960000") if z in lat}
     out["latency_summary_keys"] = "size: [p50, p99, p99 incl. pack] us"
     ten = line.get("gpu_tenants_by_phase")
     if ten:  # the most other processes seen on this GPU at any phase's end

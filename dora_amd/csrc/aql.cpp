@@ -10,6 +10,7 @@
 #include <hsa/hsa.h>
 #include <hsa/amd_hsa_signal.h>
 #include <hsa/hsa_ext_amd.h>
+#include <immintrin.h>
 #include <sys/prctl.h>
 
 #include <algorithm>
@@ -1052,6 +1053,52 @@ int bar_write(int device, void* dst, const void* src, size_t bytes) {
 
 void bar_free(void* p) {
   if (p) hsa_amd_memory_pool_free(p);
+}
+
+int bar_map(AqlQueue* q, void* p) {
+  if (!aql_usable(q)) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue");
+  if (hsa_amd_agents_allow_access(1, &q->cpu, nullptr, p) != HSA_STATUS_SUCCESS)
+    return fail(DORA_ERR_UNSUPPORTED, "host access to device memory (no large BAR)");
+  return DORA_OK;
+}
+
+namespace {
+// 32-B non-temporal stores for the aligned body: the BAR mapping is write-combined, and
+// streaming stores leave the CPU in whole lines without a read for ownership (4 KB: 1.94 us vs
+// 3.17 for memcpy, readback included, profiles/r06_host_path_probe.jsonl)
+__attribute__((target("avx2"))) void stream_body(uint8_t* d, const uint8_t* s, size_t n) {
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i),
+                        _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i)));
+  if (i < n) std::memcpy(d + i, s + i, n - i);
+}
+}  // namespace
+
+void bar_copy(void* dst, const void* src, size_t n) {
+  auto* d = static_cast<uint8_t*>(dst);
+  auto* s = static_cast<const uint8_t*>(src);
+  const size_t head = std::min(n, size_t((32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31));
+  if (head) std::memcpy(d, s, head);
+  stream_body(d + head, s + head, n - head);
+}
+
+void bar_publish(AqlQueue* q, const void* last) {
+  __builtin_ia32_sfence();
+  *reinterpret_cast<volatile uint32_t*>(q->hdp) = 1;
+  // a read (non-posted) behind the posted writes: once it returns, they have reached the memory,
+  // whichever agent reads the sample next
+  if (last) (void)*static_cast<const volatile uint8_t*>(last);
 }
 
 size_t aql_kernel_count() { return kKernels; }

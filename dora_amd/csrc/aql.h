@@ -104,6 +104,15 @@ int bar_alloc(int device, size_t bytes, void** out);
 int bar_write(int device, void* dst, const void* src, size_t bytes);
 void bar_free(void* p);
 
+// Host-resident sources written straight into a device slot by the CPU (node.cpp
+// host_bar_fill): bar_map makes a hipMalloc'd slot host-accessible through the large BAR (once
+// per slot; its IPC export is unaffected), bar_copy writes bytes with streaming stores, and
+// bar_publish (sfence + HDP flush + one read-back of `last`) returns once every byte written so
+// far has reached HBM.
+int bar_map(AqlQueue* q, void* p);
+void bar_copy(void* dst, const void* src, size_t n);
+void bar_publish(AqlQueue* q, const void* last);
+
 // Region-end reduction of stamp areas (node.cpp): one dispatch of dora_aql_stamp_reduce over
 // `n` areas of `area_words` words each at `base` (device memory), area indices in `areas`, writing
 // (start, latest end) pairs to `out` (host memory the GPU can write); waits for it (bounded).

@@ -37,6 +37,7 @@
 #include <random>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "aql.h"
@@ -169,6 +170,9 @@ struct Slot {
   // host-only node: a POSIX shared-memory region (DataMessage::SharedMemory) instead of HBM
   bool host = false;
   std::string shm_name;
+  // device slot mapped for the CPU through the large BAR (host sources written in place,
+  // host_bar_fill): tried once per slot
+  bool bar = false, bar_tried = false;
 };
 
 // The memory of a slot no fill can still write (its events, its HBM or shared-memory region).
@@ -508,6 +512,58 @@ struct NodeCore {
     recv_pool.emplace(cap, p);
   }
 
+  // Host-only receiver (device < 0): device samples are staged into pinned host memory (one DMA
+  // per input, stage_to_host), recycled by size like the receive pool.  Pinned allocations cost
+  // milliseconds at the large sizes, so a steady edge reuses its buffers.
+  std::multimap<uint64_t, void*> host_pool;
+  std::map<int, hipStream_t> stage_streams;  // per producer GPU (under pool_mu)
+  std::atomic<uint64_t> host_staged{0}, host_staged_bytes{0};
+
+  void* host_pool_get(uint64_t len, uint64_t* cap) {
+    {
+      std::lock_guard<std::mutex> g(pool_mu);
+      auto it = host_pool.lower_bound(len);
+      if (it != host_pool.end() && it->first <= 2 * len + 4096) {
+        void* p = it->second;
+        *cap = it->first;
+        host_pool.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    const uint64_t c = (len + 4095) / 4096 * 4096;
+    if (hipHostMalloc(&p, c, hipHostMallocPortable) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    *cap = c;
+    return p;
+  }
+
+  void host_pool_put(void* p, uint64_t cap) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    if (host_pool.size() >= kMaxPooled) {
+      auto it = host_pool.begin();  // evict the smallest
+      (void)hipHostFree(it->second);
+      host_pool.erase(it);
+    }
+    host_pool.emplace(cap, p);
+  }
+
+  // A stream of the producer's GPU for the staging copies (the current device must be it)
+  hipStream_t stage_stream(int src_device) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    auto it = stage_streams.find(src_device);
+    if (it != stage_streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    stage_streams[src_device] = s;
+    return s;
+  }
+
   uint64_t* flag_dev(int idx) const {
     const uint8_t* host = reinterpret_cast<const uint8_t*>(&region->hdr()->nodes[this->idx].fill[idx]);
     return reinterpret_cast<uint64_t*>(region_dev + (host - region->base()));
@@ -644,6 +700,11 @@ struct NodeCore {
     if (sync_ev) (void)hipEventDestroy(sync_ev);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& kv : recv_pool) (void)hipFree(kv.second);
+    for (auto& kv : stage_streams) {
+      (void)hipStreamSynchronize(kv.second);
+      (void)hipStreamDestroy(kv.second);
+    }
+    for (auto& kv : host_pool) (void)hipHostFree(kv.second);
     if (fill_done) (void)hipFree(fill_done);
     if (region_dev) (void)hipHostUnregister(region->base());
     if (stream) (void)hipStreamDestroy(stream);
@@ -665,8 +726,11 @@ struct InputData {
   int remote_device = -1;     // >= 0: `ptr` is a peer GPU's slot not yet pulled (ensure_local)
   hipEvent_t bcast_ev = nullptr;  // broadcast group input: completion of its receive into `local`
   std::shared_ptr<ShmMapping> shm;  // a host-only producer's shared-memory sample, mapped here
-  bool host_mem = false;   // host receiver: `ptr` is the shared memory itself (read in place)
+  bool host_mem = false;   // host receiver: `ptr` is host memory (shared memory read in place,
+                           // or a device sample staged into `host_local`)
   bool host_pull = false;  // device receiver: `ptr` is shared memory not yet pulled into HBM
+  void* host_local = nullptr;  // host-only receiver: pinned copy of a device sample (stage_to_host)
+  uint64_t host_local_cap = 0;
   ~InputData() {
     if (!core) return;
     if (bcast_ev) {
@@ -686,6 +750,7 @@ struct InputData {
       trace(TP_RELEASED, token);
     }
     if (local) core->recv_pool_put(local, local_cap);
+    if (host_local) core->host_pool_put(host_local, host_local_cap);
   }
 };
 
@@ -742,6 +807,8 @@ struct dora_node {
   uint64_t bytes_ti_len = 0;
   std::deque<std::unique_ptr<dora_event>> queue;
   bool ended = false;
+  // samples dora_node_allocate_data_sample handed out and not yet sent or discarded
+  std::unordered_set<dora_sample*> samples_live;
   // Event-stream thread (dora_node_set_event_thread; started by every node that joins an RCCL
   // broadcast group as a receiver): the reference's event_stream_loop (event_stream/thread.rs:
   // 81-188) — it drains the daemon's ring into `queue` continuously and applies the drop-oldest
@@ -783,6 +850,7 @@ struct dora_node {
   uint32_t region_cp_next = 0;
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
+  uint64_t bar_fills = 0;  // host sources written into their slot by the CPU (host_bar_fill)
   bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
@@ -1279,7 +1347,9 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
           } else {
             hipIpcMemHandle_t h;
             std::memcpy(&h, d.ipc.handle, sizeof(h));
-            DeviceScope ds(c->device);
+            // a host-only receiver maps the slot on its producer's GPU, whose copy engine stages
+            // it to host memory (stage_to_host)
+            DeviceScope ds(c->device >= 0 ? c->device : int(d.ipc.device));
             hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
             if (e != hipSuccess) {
               ev->type = DORA_EVENT_ERROR;
@@ -1334,6 +1404,47 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
       return;  // EV_READY after init is ignored
   }
   n->queue.push_back(std::move(ev));
+}
+
+// A device sample delivered to a node without a GPU (DORA_GPU_DEVICE < 0): one DMA by the
+// producer GPU's copy engines into pinned host memory the input owns (recycled, host_pool), then
+// the producer's token goes back at once and the input is a host input like a shared-memory one
+// (the reference's receivers always get host ArrowData, event_stream/event.rs:35-91; a Python
+// receiver a pyarrow array, apis/python/operator/src/lib.rs:135-144).  4 KB: ~12.7 us, 40.96 MB:
+// 56 GB/s on an MI355X box (profiles/r06_host_path_probe.jsonl, d2h_pinned).
+int stage_to_host(InputData* in, int src_device) {
+  NodeCore* c = in->core.get();
+  if (in->ext_len) {
+    DeviceScope ds(src_device);
+    uint64_t cap = 0;
+    void* h = c->host_pool_get(in->ext_len, &cap);
+    if (!h)
+      return fail(DORA_ERR_HIP, "pinned staging buffer of %llu bytes",
+                  (unsigned long long)in->ext_len);
+    hipStream_t st = c->stage_stream(src_device);
+    hipError_t e = st ? hipMemcpyAsync(h, in->ptr, in->ext_len, hipMemcpyDeviceToHost, st)
+                      : hipErrorInvalidResourceHandle;
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      c->host_pool_put(h, cap);
+      return fail(DORA_ERR_HIP, "staging a device sample to host memory: %s",
+                  hipGetErrorString(e));
+    }
+    in->host_local = h;
+    in->host_local_cap = cap;
+    c->host_staged.fetch_add(1, std::memory_order_relaxed);
+    c->host_staged_bytes.fetch_add(in->ext_len, std::memory_order_relaxed);
+  }
+  in->ptr = in->host_local;
+  in->host_mem = true;
+  in->mapping.reset();
+  if (in->has_token) {
+    c->report_drop_token(in->token);
+    trace(TP_RELEASED, in->token);
+    in->has_token = false;
+  }
+  return DORA_OK;
 }
 
 // Complete a queued device input right before it is handed to the user: wait for the
@@ -1441,6 +1552,16 @@ void finish_input(dora_node* n, dora_event* ev) {
     }
   }
   trace(TP_FILLED, in->token);
+  if (n->core->device < 0) {
+    // a receiver without a GPU gets the reference's host ArrowData (event.rs:35-91): the sample
+    // is staged to host memory now and the producer's token goes back at once
+    if (stage_to_host(in, int(d.device)) != DORA_OK) {
+      ev->type = DORA_EVENT_ERROR;
+      ev->error = dora_gpu_last_error();
+      in->ptr = nullptr;
+    }
+    return;
+  }
   if (in->len && (d.device != n->core->device || edge_copy_forced())) {
     // Cross-GPU edge: the sample is pulled over xGMI on first access to its data
     // (ensure_local), or straight into an outgoing slot by dora_node_forward.
@@ -1836,6 +1957,13 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out, uint64_t ext_len
   return DORA_OK;
 }
 
+// An unsent sample back to the node: its slot to the cache (an inline Vec is just freed).
+void discard_sample(dora_node* n, dora_sample* s) {
+  if (!s) return;
+  if (s->slot) add_to_cache(n, s->slot);
+  delete s;
+}
+
 constexpr size_t kTimingPairs = 64;
 constexpr size_t kMaxIntervals = 1 << 16;  // stamped packs whose (start, stop) are kept
 
@@ -2033,7 +2161,7 @@ int forward_input(dora_node* n, const char* output_id, const dora_event* ev, con
   if (rc != DORA_OK) return rc;
   if (len && (!s->slot || s->slot->host)) {
     if (device_src) {
-      dora_sample_discard(n, s);
+      discard_sample(n, s);
       return fail(DORA_ERR_INVALID, "host-only node cannot forward device-resident data");
     }
     std::memcpy(s->slot ? s->slot->ptr : s->vec.data(), in->ptr, len);
@@ -2164,6 +2292,49 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
   return DORA_OK;
 }
 
+// Host-resident sources up to this size are written into their device slot by the CPU through
+// the large BAR (host_bar_fill); larger ones are DMA'd by HIP.  On an MI355X box the BAR path
+// delivers 4 KB in 1.9 us and 1 MiB in 30 us (35 GB/s), HIP's copy takes 13-14 us up to 64 KB,
+// 52 us at 1 MiB and wins from ~2 MiB (4 MiB: 89 vs 140 us; 40.96 MB: 56 GB/s)
+// (profiles/r06_host_path_probe.jsonl).
+constexpr uint64_t kBarFillMax = 2ull << 20;
+
+// The reference copies a host source into its shared-memory sample on the CPU inside
+// send_output (arrow_utils.rs:48, node/mod.rs:180-215).  A device node does the same into its
+// HBM slot: the slot is mapped for the CPU once, the segments are written with streaming stores,
+// and one HDP flush + read-back makes them visible before the descriptor leaves, so the sample
+// is complete when the call returns (FILL_DONE: no GPU dispatch, no fill flag).  False when the
+// slot cannot be mapped (no large BAR, no HSA): the caller takes the HIP copy.
+bool host_bar_fill(dora_node* n, dora_sample* s, const std::vector<Segment>& segs) {
+  Slot* slot = s->slot;
+  if (!slot || slot->host || s->ext_len > kBarFillMax) return false;
+  if (!n->core->aql_tried) {
+    n->core->aql_tried = true;
+    n->core->aql = aql_queue(n->core->device);
+  }
+  AqlQueue* q = aql_usable(n->core->aql) ? n->core->aql : nullptr;
+  if (!q) return false;
+  if (!slot->bar_tried) {
+    slot->bar_tried = true;
+    slot->bar = bar_map(q, slot->ptr) == DORA_OK;
+    if (!slot->bar) clear_error();
+  }
+  if (!slot->bar) return false;
+  for (const Segment& g : segs)
+    if (g.op != SEG_COPY) return false;
+  auto* dst = static_cast<uint8_t*>(slot->ptr);
+  const uint8_t* last = nullptr;
+  for (const Segment& g : segs) {
+    if (!g.len) continue;
+    bar_copy(dst + g.dst_off, g.src, g.len);
+    last = dst + g.dst_off + g.len - 1;
+  }
+  bar_publish(q, last);
+  s->fill = FILL_DONE;
+  ++n->bar_fills;
+  return true;
+}
+
 int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, const uint8_t* params,
                   size_t params_len, const std::vector<uint8_t>* ti_pre = nullptr,
                   uint32_t flags = 0) {
@@ -2179,11 +2350,14 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     // an inline Vec or a host-only node's shared-memory slot: the host copies the buffers
     // (copy_array_into_sample, arrow_utils.rs:48)
     if (!host_src) {
-      dora_sample_discard(n, s);
+      discard_sample(n, s);
       return fail(DORA_ERR_INVALID, "host-only node cannot send device-resident data");
     }
     uint8_t* dst = s->slot ? static_cast<uint8_t*>(s->slot->ptr) : s->vec.data();
     for (const Segment& g : plan->segs) std::memcpy(dst + g.dst_off, g.src, g.len);
+    t2 = t3 = mono_ns();
+  } else if (plan->size && host_src && plan->dev == ARROW_DEVICE_CPU &&
+             host_bar_fill(n, s, plan->segs)) {
     t2 = t3 = mono_ns();
   } else if (plan->size) {
     // Kernel stamps cost host time and a timestamp packet on each side of the dispatch, so only
@@ -2279,6 +2453,7 @@ dora_sample* vec_sample(const uint8_t* p, size_t len) {
 int proxy_send(dora_node* n, const char* output_id, const uint8_t* ti, size_t ti_len,
                const uint8_t* params, size_t params_len, dora_sample* sample, uint64_t ts) {
   DORA_GUARD_BEGIN
+  n->samples_live.erase(sample);  // consumed here (an allocate_data_sample sample or inline)
   std::vector<uint8_t> t(ti, ti + ti_len);
   return send_sample(n, output_id, t, params, params_len, sample, nullptr, ts);
   DORA_GUARD_END
@@ -2446,6 +2621,8 @@ void dora_node_free(dora_node* n) {  // Drop for DoraNode (mod.rs:384-431)
     (void)hipStreamDestroy(kv.second.stream);
   }
   n->bcast_out.clear();
+  for (dora_sample* s : n->samples_live) dora::discard_sample(n, s);  // allocated, never sent
+  n->samples_live.clear();
   for (auto& kv : n->sent_out) dora::free_slot(n, kv.second);
   for (auto* s : n->cache) dora::free_slot(n, s);
   dora::SlotReaper::reaper().drain();  // evicted slots: freed before the node's state goes
@@ -2508,7 +2685,9 @@ dora_stream_t dora_node_stream(dora_node* n) {
 int dora_node_allocate_data_sample(dora_node* n, size_t len, dora_sample** out) {
   if (!n || !out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
   DORA_GUARD_BEGIN
-  return dora::alloc_sample(n, len, out);
+  const int rc = dora::alloc_sample(n, len, out);
+  if (rc == DORA_OK) n->samples_live.insert(*out);
+  return rc;
   DORA_GUARD_END
 }
 
@@ -2520,9 +2699,14 @@ void* dora_sample_data(dora_sample* s) {
 size_t dora_sample_len(const dora_sample* s) { return s ? s->len : 0; }
 
 void dora_sample_discard(dora_node* n, dora_sample* s) {
-  if (!s) return;
-  if (s->slot && n) dora::add_to_cache(n, s->slot);
-  delete s;
+  if (!s || !n) return;
+  // only a sample this node handed out and nobody consumed yet (a second discard, or a discard
+  // after the send, would free it twice)
+  if (!n->samples_live.erase(s)) {
+    dora::fail(DORA_ERR_INVALID, "sample was already sent or discarded");
+    return;
+  }
+  dora::discard_sample(n, s);
 }
 
 int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint8_t* type_info,
@@ -2530,7 +2714,25 @@ int dora_node_send_output_sample(dora_node* n, const char* output_id, const uint
                                  dora_sample* sample) {
   if (!n || !output_id || (!type_info && type_info_len))
     return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  // the reference's DataSample is moved into send_output_sample (mod.rs:246-275): a C caller
+  // may hold on to the pointer, so a sample that was already sent or discarded is refused
+  if (sample && !n->samples_live.erase(sample))
+    return dora::fail(DORA_ERR_INVALID,
+                      "sample was already sent or discarded (or belongs to another node)");
   DORA_GUARD_BEGIN
+  if (sample && sample->slot && !sample->slot->host && sample->len &&
+      n->core->stream_used.load(std::memory_order_relaxed)) {
+    // a sample written by kernels on the node stream (dora_node_stream): receivers wait for
+    // that work through the slot's fill flag, the sender does not (no host synchronisation)
+    dora::DeviceScope ds(n->core->device);
+    const hipError_t e = dora::order_fill(n, sample, n->core->stream);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      dora::discard_sample(n, sample);
+      return dora::fail(DORA_ERR_HIP, "ordering the sample after the node stream: %s",
+                        hipGetErrorString(e));
+    }
+  }
   std::vector<uint8_t> ti(type_info, type_info + type_info_len);
   return dora::send_sample(n, output_id, ti, params, params_len, sample);
   DORA_GUARD_END
@@ -2769,7 +2971,8 @@ int dora_event_type_info(const dora_event* e, const uint8_t** ti, size_t* len) {
     if (rc != DORA_OK) return rc;
     bool changed = false;
     rc = dora::inline_type_info(e->meta.type_info.data(), e->meta.type_info.size(),
-                                e->data->ptr, e->data->ext_len, &e->ti_inline, &changed);
+                                e->data->ptr, e->data->ext_len, &e->ti_inline, &changed,
+                                e->data->host_mem);
     if (rc != DORA_OK) return rc;
     DORA_GUARD_END
   }
@@ -2801,10 +3004,12 @@ int dora_event_array(const dora_event* e, struct ArrowArray* out_array,
   if (rc != DORA_OK) return rc;
   DORA_GUARD_END
   std::shared_ptr<void> keep = e->data;
-  // an inline Vec sample, or shared memory read in place: a host array over its bytes
+  // an inline Vec sample, shared memory read in place or a device sample staged to host memory:
+  // a host array over its bytes (a staged sample keeps its validity tail)
   if (e->data->host_mem || (!e->data->has_token && !e->data->local))
     return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
-                               e->meta.type_info.size(), keep, out_array, out_schema, 0, true);
+                               e->meta.type_info.size(), keep, out_array, out_schema,
+                               e->data->ext_len, true);
   return dora::import_sample(e->data->ptr, e->data->len, e->meta.type_info.data(),
                              e->meta.type_info.size(), keep, out_array, out_schema,
                              e->data->ext_len);
@@ -2867,6 +3072,15 @@ int dora_node_fill_paths(dora_node* n, uint64_t* aql_packs, uint64_t* hip_packs)
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (aql_packs) *aql_packs = n->aql_packs;
   if (hip_packs) *hip_packs = n->hip_packs;
+  return DORA_OK;
+}
+
+int dora_node_host_paths(dora_node* n, uint64_t* bar_fills, uint64_t* staged,
+                         uint64_t* staged_bytes) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  if (bar_fills) *bar_fills = n->bar_fills;
+  if (staged) *staged = n->core->host_staged.load();
+  if (staged_bytes) *staged_bytes = n->core->host_staged_bytes.load();
   return DORA_OK;
 }
 

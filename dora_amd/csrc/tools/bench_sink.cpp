@@ -13,6 +13,7 @@
 #include <array>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -55,6 +56,25 @@ uint64_t mono() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+// csum64 of host bytes (the csum_kernel's sum, include/dora_gpu.h dora_gpu_csum64), for inputs a
+// receiver without a GPU got staged in host memory
+uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t csum64_host(const uint8_t* p, size_t n) {
+  constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull, kSeed = 0xD0A5D0A5D0A5D0A5ull;
+  uint64_t s = 0;
+  for (size_t i = 0; 8 * i < n; ++i) {
+    uint64_t w = 0;
+    std::memcpy(&w, p + 8 * i, std::min<size_t>(8, n - 8 * i));
+    s += fmix64(w ^ (i * kGolden + kSeed));
+  }
+  return fmix64(s + n);
 }
 
 uint64_t now_ns() {
@@ -190,6 +210,12 @@ int main() {
       const bool dev = dora_event_is_device(ev);
       if (params.count("csum") && params.count("verify") && dev)
         verify(p, len, static_cast<uint64_t>(params["csum"].i), s);
+      if (params.count("csum") && params.count("verify") && !dev && p) {
+        ++s.verified;  // a host input (inline, shared memory, or a device sample staged here)
+        if (csum64_host(static_cast<const uint8_t*>(p), len) !=
+            static_cast<uint64_t>(params["csum"].i))
+          ++s.mismatches;
+      }
       const bool ack = params.count("ack") != 0;
       if (params.count("csum") && params.count("verify_late") && dev) {
         held.push_back({ev, p, len, static_cast<uint64_t>(params["csum"].i), &s});

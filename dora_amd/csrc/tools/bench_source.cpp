@@ -9,6 +9,10 @@
 //               DORA_BENCH_LAT_GAP_US apart (33333 = 30 Hz, C5);
 //   throughput: DORA_BENCH_TP_N messages of DORA_BENCH_TP_SIZE bytes back-to-back, closed by an
 //               ack request that every one of the DORA_BENCH_ACKS receivers acknowledges.
+// DORA_BENCH_SAMPLE_PATH=1: every message takes the reference benchmark's own path
+// (examples/benchmark/node/src/main.rs via allocate_data_sample + send_output_sample,
+// apis/rust/node/src/node/mod.rs:246-346): a slot is allocated, a kernel on the node stream
+// writes the payload into it in place, and the sample is sent — no pack, no source buffer.
 // Outputs `latency` and `throughput` (warmup and ack requests go on `throughput`, like the
 // reference node's two outputs); every input is an ack channel from a receiver.
 //   env: DORA_GPU_DATAFLOW, DORA_NODE_ID, DORA_GPU_DEVICE, DORA_BENCH_RESULT (path)
@@ -122,6 +126,38 @@ int main() {
   }
   dora_gpu_stream_sync(st);
 
+  // sample path: the node stream the payload kernels run on, and byte_array type infos by size
+  const bool sample_path = env_long("DORA_BENCH_SAMPLE_PATH", 0) != 0;
+  dora_stream_t nst = sample_path ? dora_node_stream(node) : nullptr;
+  std::map<uint64_t, std::vector<uint8_t>> tis;
+  auto type_info = [&](const void* data, uint64_t size) -> const std::vector<uint8_t>& {
+    auto it = tis.find(size);
+    if (it != tis.end()) return it->second;
+    std::vector<uint8_t>& ti = tis[size];
+    dora_plan* plan = nullptr;
+    size_t n = 0;
+    if (dora_gpu_plan_bytes(data, size, ARROW_DEVICE_ROCM, &plan) == 0) {
+      ti.resize(4096);
+      if (dora_gpu_plan_type_info(plan, ti.data(), ti.size(), &n) != 0) n = 0;
+      dora_gpu_plan_free(plan);
+    }
+    ti.resize(n);
+    return ti;
+  };
+  // one message of `size` bytes written in place by a kernel (sample path)
+  auto send_in_place = [&](const char* output, uint64_t size, const uint8_t* params,
+                           size_t params_len) -> int {
+    dora_sample* smp = nullptr;
+    if (dora_node_allocate_data_sample(node, size, &smp) != 0) return -1;
+    if (size && dora_gpu_fill_splitmix(dora_sample_data(smp), size, 0xD05A + size, nst) != 0) {
+      dora_sample_discard(node, smp);
+      return -1;
+    }
+    const std::vector<uint8_t>& ti = type_info(dora_sample_data(smp), size);
+    return dora_node_send_output_sample(node, output, ti.data(), ti.size(), params, params_len,
+                                        smp);
+  };
+
   int64_t seq = 0;
   // throughput-mode messages carry default parameters, like the reference node's
   // send_output_raw(.., Default::default(), ..): latency comes from the metadata timestamp
@@ -129,7 +165,9 @@ int main() {
     const Source& x = src[size];
     const size_t k = static_cast<size_t>(seq++ % tp_sources);
     const void* p = k == 0 ? x.ptr : x.extra[k - 1];
-    if (dora_node_send_output_bytes(node, output, p, size, ARROW_DEVICE_ROCM, nullptr, 0) != 0) {
+    if ((sample_path ? send_in_place(output, size, nullptr, 0)
+                     : dora_node_send_output_bytes(node, output, p, size, ARROW_DEVICE_ROCM,
+                                                   nullptr, 0)) != 0) {
       std::fprintf(stderr, "source: send failed: %s\n", dora_gpu_last_error());
       ++errors;
     }
@@ -144,8 +182,9 @@ int main() {
       p["verify"].i = 1;
     }
     auto enc = encode_params(p);
-    if (dora_node_send_output_bytes(node, output, src[size].ptr, size, ARROW_DEVICE_ROCM,
-                                    enc.data(), enc.size()) != 0) {
+    if ((sample_path ? send_in_place(output, size, enc.data(), enc.size())
+                     : dora_node_send_output_bytes(node, output, src[size].ptr, size,
+                                                   ARROW_DEVICE_ROCM, enc.data(), enc.size())) != 0) {
       std::fprintf(stderr, "source: send failed: %s\n", dora_gpu_last_error());
       ++errors;
     }

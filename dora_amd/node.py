@@ -334,6 +334,13 @@ class Node:
         call("dora_node_fill_paths", self.handle, byref(a), byref(h))
         return {"aql": a.value, "hip": h.value}
 
+    def host_paths(self) -> dict:
+        """Host sources written into their slot by the CPU through the BAR, and device samples
+        this node (without a GPU) staged to host memory (dora_node_host_paths)."""
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        call("dora_node_host_paths", self.handle, byref(a), byref(b), byref(c))
+        return {"bar_fills": a.value, "staged": b.value, "staged_bytes": c.value}
+
     def set_timing_period(self, period: int):
         """Stamp every `period`-th pack launch (0: the default, every 8th)."""
         call("dora_node_set_timing_period", self.handle, int(period))

@@ -260,9 +260,14 @@ dora_stream_t dora_node_stream(dora_node* node);
 int dora_node_allocate_data_sample(dora_node* node, size_t len, dora_sample** out);
 void* dora_sample_data(dora_sample* sample); /* device pointer (slot) */
 size_t dora_sample_len(const dora_sample* sample);
-void dora_sample_discard(dora_node* node, dora_sample* sample); /* unsent sample -> cache */
-/* send_output_sample (mod.rs:246-275): consumes `sample` (may be NULL = no data). The sample
- * must be fully written (its stream synchronized) before the call. `params` is the encoded
+/* An unsent sample back to the node's cache.  A sample that was already sent or discarded is
+ * left alone (dora_gpu_last_error says so). */
+void dora_sample_discard(dora_node* node, dora_sample* sample);
+/* send_output_sample (mod.rs:246-275): consumes `sample` (may be NULL = no data); a sample that
+ * was already sent or discarded is refused with DORA_ERR_INVALID (the reference moves its
+ * DataSample into the call).  The sample must be written before the call: on the host, or by
+ * work queued on dora_node_stream() — receivers then wait for that work through the slot's fill
+ * signal, the call does not — or on another stream the caller synchronized.  `params` is the encoded
  * MetadataParameters (u32 n, then per entry: u64 klen, key, u8 tag 0=bool 1=int 2=string,
  * value: u8 | i64 | u64 len + bytes). */
 int dora_node_send_output_sample(dora_node* node, const char* output_id, const uint8_t* type_info,
@@ -365,6 +370,13 @@ int dora_node_dataflow_counters(dora_node* node, const char* node_id, uint64_t* 
  * sources of <= 8 segments) or hipLaunchKernel on
  * the node's fill streams (larger, host sources, compacting transforms, relays). */
 int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_packs);
+/* The host side of the data plane (new; diagnostics): host-resident sources of 4096 B..2 MiB a
+ * device node wrote into its slot with the CPU through the large BAR (the reference's memcpy
+ * into its shared-memory sample, arrow_utils.rs:48: no GPU dispatch), and device samples a node
+ * without a GPU (DORA_GPU_DEVICE < 0) staged into host memory on receipt (count, bytes): such a
+ * receiver gets the reference's host ArrowData (event.rs:35-91). */
+int dora_node_host_paths(dora_node* node, uint64_t* bar_fills, uint64_t* staged,
+                         uint64_t* staged_bytes);
 /* dora_node_send_output of device arrays keeps the plans of recent sends that read no array
  * bytes (fixed-width and nested arrays with known null counts), keyed by everything such a plan
  * depends on (schema strings and flags, lengths, offsets, null counts, buffer addresses): a

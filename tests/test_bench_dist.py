@@ -158,7 +158,7 @@ def test_compact_line_fits_the_driver_tail():
     full["sink_dropped_by_phase"] = {"warmup": 0, "latency_ladder": 2, "timed_region": 0}
     full["config"]["workload"] = ("C2: examples/benchmark node->sink edge, device-resident UInt8 "
                                   "samples, 1 node + 1 sink per GPU")
-    for z in ("host_8", "host_512", "host_2048", "host_4096"):
+    for z in ("host_8", "host_512", "host_2048", "host_4096", "d2h_4096"):
         full["latency_us"][z] = dict(full["latency_us"]["8"])
     full["sync_send_headline"].update({"hbm_frac_2S": 0.19, "pack_own_us": 17.9,
                                        "pack_own_frac": 0.57, "gap_us_median": 6.3})
@@ -170,8 +170,8 @@ def test_compact_line_fits_the_driver_tail():
               "roofline", "cpu_baseline"):
         assert k in c, k
     assert list(c)[-1] == "cpu_baseline"
-    assert set(c["latency_summary"]) == {"host_8", "host_2048", "8", "4096", "4194304",
-                                         "40960000"}
+    assert set(c["latency_summary"]) == {"host_8", "host_2048", "host_4096", "d2h_4096", "8",
+                                         "4096", "4194304", "40960000"}
     assert c["config"]["workload"] == full["config"]["workload"]  # whole, not cut
     assert c["roofline"]["frac"] == full["roofline"]["frac"]
     assert c["sink_dropped"]["by_phase"] == {"latency_ladder": 2}

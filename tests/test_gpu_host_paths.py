@@ -3,7 +3,8 @@
 * A device node's host-source payloads below the zero-copy threshold travel inline as
   `DataMessage::Vec` — the reference's allocate_data_sample (apis/rust/node/src/node/mod.rs:40,
   303-319): no slot, no H2D copy, no fill signal.  Every size 1..4095 class arrives byte-identical
-  to the oracle's copy_array_into_sample (oracle/pack_ref.py), and 4096 B takes the device slot.
+  to the oracle's copy_array_into_sample (oracle/pack_ref.py), and 4096 B takes the device slot
+  (written by the CPU through the BAR).
 * A host-only node's samples >= 4096 B are `DataMessage::SharedMemory` regions (mod.rs:321-346);
   a device receiver pulls them into HBM by DMA and returns the token at once.
 """
@@ -61,6 +62,7 @@ def test_host_small_payloads_go_inline_bit_exact(launcher):
         n = _nodes(df, {"src": 0, "dst": 0})
         tx, rx = n["src"], n["dst"]
         paths0 = tx.fill_paths()
+        bar0 = tx.host_paths()["bar_fills"]
         for z in sizes:
             payload = rng.integers(0, 256, z, dtype=np.uint8).tobytes()
             want, info = pack(pa.array(np.frombuffer(payload, np.uint8), pa.uint8()))
@@ -77,8 +79,10 @@ def test_host_small_payloads_go_inline_bit_exact(launcher):
                 assert _device_bytes(ev, s) == want, z
             del ev
         paths1 = tx.fill_paths()
-        # only the 4096-B message was packed (an H2D pack on the fill streams)
-        assert (paths1["aql"] + paths1["hip"]) - (paths0["aql"] + paths0["hip"]) == 1, paths1
+        # nothing was packed: the 4096-B message went into its slot by CPU stores through the
+        # BAR (node.cpp host_bar_fill), the rest inline
+        assert paths1 == paths0, paths1
+        assert tx.host_paths()["bar_fills"] - bar0 == 1, tx.host_paths()
         # host pyarrow arrays whose sample is < 4096 B (the reference's own KATs and fixtures)
         names = [m for m in recipes.KATS + recipes.CASES if len(pack(recipes.build(m))[0]) < 4096]
         assert len(names) >= 10, names
