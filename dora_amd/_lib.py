@@ -106,6 +106,8 @@ _SIGS = {
     "dora_node_init_from_env": (c_int, [POINTER(c_void_p)]),
     "dora_node_free": (None, [c_void_p]),
     "dora_node_stream": (c_void_p, [c_void_p]),
+    "dora_node_dataflow_id": (c_char_p, [c_void_p]),
+    "dora_node_id": (c_char_p, [c_void_p]),
     "dora_node_allocate_data_sample": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "dora_sample_data": (c_void_p, [c_void_p]),
     "dora_sample_len": (c_size_t, [c_void_p]),
@@ -188,31 +190,19 @@ _SIGS = {
 _TEST_SIGS = {
     "dora_gpu_test_fill_reached": (c_int, [c_void_p, c_uint64]),
     "dora_gpu_test_cp_arm": (c_int, [c_void_p, c_uint64]),
-    "dora_gpu_test_pack_signal_tune": (c_int, [ctypes.c_uint32, c_int]),
-    "dora_gpu_test_pack_tune": (c_int, [c_int, c_int, ctypes.c_uint32]),
-    "dora_gpu_test_cp_grid": (c_int, [ctypes.c_uint32]),
-    "dora_gpu_test_cp_grid_multi": (c_int, [ctypes.c_uint32]),
-    "dora_gpu_test_in_flight": (c_int, [ctypes.c_long, ctypes.c_long]),
     "dora_gpu_test_l2_touch": (c_int, [c_void_p, c_size_t, c_void_p]),
     "dora_gpu_test_bar_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p)]),
     "dora_gpu_test_bar_write": (c_int, [c_int, c_void_p, c_void_p, c_size_t]),
     "dora_gpu_test_bar_free": (None, [c_void_p]),
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
-    "dora_gpu_test_cp_lone": (c_int, [c_int]),
-    "dora_gpu_test_heartbeat_start": (c_int, [c_int, c_int, ctypes.c_double, ctypes.c_double,
-                                              ctypes.POINTER(c_void_p)]),
-    "dora_gpu_test_heartbeat_stop": (c_int, [c_void_p]),
+    "dora_gpu_test_reduce_timeout": (c_int, [c_uint64]),
+    "dora_gpu_test_abandoned_slots": (c_int, [c_int, POINTER(c_uint32)]),
     "dora_gpu_test_keep_awake_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_int)]),
-    "dora_gpu_test_keep_warm_start": (c_int, [c_int, ctypes.c_double, ctypes.POINTER(c_void_p)]),
-    "dora_gpu_test_keep_warm_stop": (c_int, [c_void_p]),
-    "dora_gpu_test_mid_queues": (c_int, [c_int, c_int]),
     "dora_gpu_test_aql_ring_wc": (c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "dora_gpu_test_bcast_group": (c_int, [c_int, c_void_p, c_uint64, POINTER(c_int),
                                           POINTER(c_int)]),
     "dora_gpu_test_l1_stale": (c_int, [c_int, c_int, POINTER(c_uint32), POINTER(c_uint32),
                                        POINTER(c_uint32)]),
-    "dora_gpu_test_aql_pipeline": (c_int, [c_int, c_size_t, c_int, c_int, c_int, c_int,
-                                           POINTER(ctypes.c_double)]),
     "dora_gpu_test_ide_output": (c_int, [c_char_p, c_char_p, c_char_p, c_void_p, c_size_t,
                                          c_void_p, c_size_t, c_uint64, c_uint64, c_void_p,
                                          c_void_p, c_size_t, c_int, c_void_p, c_size_t,

@@ -11,6 +11,7 @@
 #include <hsa/amd_hsa_signal.h>
 #include <hsa/hsa_ext_amd.h>
 #include <immintrin.h>
+#include <pthread.h>
 #include <sys/prctl.h>
 
 #include <algorithm>
@@ -108,8 +109,6 @@ constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4", "dora_aql_pa
 // * four HSA queues per process: 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s against
 //   two (profiles/r01_aql_queues_ab.jsonl);
 constexpr int kQueues = 4;
-// test hooks (aql_mid_queues): queues a process creates, and how many take 8-32 MiB packs
-std::atomic<int> g_create_queues{kQueues}, g_mid_queues{4};
 // * packs of [1 MiB, 32 MiB) are signalled by the command processor (the packet's completion
 //   signal, every wave waiting for its own stores), so consecutive packets of a queue overlap:
 //   4 MB over 4 queues 1.95 -> 1.59-1.64 us each (profiles/r03_aql_pipeline_probe.jsonl), C3's
@@ -163,6 +162,10 @@ struct AqlQueue {
   uint32_t* hdp = nullptr;    // HDP_MEM_FLUSH_CNTL
   uint64_t next = 0, next_big = 0;
   Use uses[kRingSlots];
+  // argument slots left to a packet that may still run (a stamp reduction that timed out): never
+  // written again (take_slot skips them)
+  bool abandoned[kRingSlots] = {};
+  uint32_t n_abandoned = 0;
   std::atomic<bool> failed{false};
   bool profiling = false;
   std::vector<hsa_signal_t> free_sigs, used_sigs;
@@ -191,6 +194,8 @@ struct AqlQueue {
   // and whether the warm thread is parked (no dispatch for kWarmWindow)
   std::atomic<uint64_t> activity{0};
   std::atomic<bool> warm_parked{false};
+  std::atomic<bool> warm_stop{false};  // process exit (stop_warm_threads)
+  std::thread warm_thread;
   std::atomic<uint64_t> heartbeats{0};  // empty packets published (aql_heartbeats)
   std::mutex warm_mu;
   std::condition_variable warm_cv;
@@ -373,7 +378,7 @@ AqlQueue* create(int device) {
     std::memcpy(a->ring + size_t(r) * kSlotBytes, zero.data(), kSlotBytes);
   __builtin_ia32_sfence();
   (void)*reinterpret_cast<volatile uint32_t*>(a->ring + size_t(kRingSlots - 1) * kSlotBytes);
-  const int create_queues = std::max(1, std::min(kMaxQueues, g_create_queues.load()));
+  const int create_queues = std::min(kMaxQueues, kQueues);
   for (int i = 0; i < create_queues; ++i) {
     if (hsa_queue_create(f.gpu, kQueuePackets, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
                          UINT32_MAX, UINT32_MAX, &a->qs[i]) != HSA_STATUS_SUCCESS)
@@ -427,6 +432,7 @@ AqlQueue* create(int device) {
 
 namespace {
 void warm_main(AqlQueue* a);
+void stop_warm_threads();
 std::mutex g_queues_mu;
 AqlQueue* g_queues[64] = {};
 }  // namespace
@@ -440,8 +446,23 @@ AqlQueue* aql_queue(int device) {
   if (!tried[device]) {
     tried[device] = true;
     queues[device] = create(device);
-    // the warm thread (warm_main) lives as long as the process, like the queues
-    if (queues[device]) std::thread(warm_main, queues[device]).detach();
+    // the warm thread (warm_main) lives as long as the process, like the queues; it is stopped
+    // and joined at exit, before HIP's and HSA's own teardown (registered earlier, so run later)
+    if (queues[device]) {
+      queues[device]->warm_thread = std::thread(warm_main, queues[device]);
+      static std::once_flag once;
+      std::call_once(once, [] {
+        std::atexit(stop_warm_threads);
+        // a forked child has no warm threads: it must not join its parent's
+        pthread_atfork(nullptr, nullptr, [] {
+          for (AqlQueue* q : g_queues)
+            if (q && q->warm_thread.joinable()) {
+              new (&q->warm_thread) std::thread();
+              q->warm_stop.store(true);
+            }
+        });
+      });
+    }
   }
   AqlQueue* q = queues[device];
   return (q && !q->failed.load()) ? q : nullptr;
@@ -529,7 +550,13 @@ namespace {
 // profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
 // the 20-cloud burst, profiles/r04_full_ab.jsonl).
 int big_queues(int nq, uint64_t bytes) {
-  return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : g_mid_queues.load());
+  return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : 4);
+}
+
+// The argument slot of dispatch number a->next (a->mu held), past any abandoned slot.
+uint64_t take_slot(AqlQueue* a) {
+  while (a->abandoned[a->next % kRingSlots]) ++a->next;
+  return a->next % kRingSlots;
 }
 
 // The number of the oldest dispatch still in an outstanding list (a->next when none is).
@@ -554,7 +581,7 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // sits in its queue's outstanding list until seen complete (prune) and the lists hold
   // dispatches in order, so one older than every list's front is complete: no load of its flag
   // line (which the GPU has written since: a cache miss per send)
-  const uint64_t r = a->next % kRingSlots;
+  const uint64_t r = take_slot(a);
   Use& u = a->uses[r];
   if (u.flag && u.seq >= oldest_outstanding(a) && !fill_reached(u.flag, u.epoch)) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -848,7 +875,8 @@ void warm_main(AqlQueue* a) {
   uint64_t seen = a->activity.load(std::memory_order_relaxed);
   auto last_change = clock::now();
   auto next = last_change;
-  while (!a->failed.load(std::memory_order_relaxed)) {
+  while (!a->failed.load(std::memory_order_relaxed) &&
+         !a->warm_stop.load(std::memory_order_relaxed)) {
     const auto period = std::chrono::nanoseconds(g_warm_period_ns.load(std::memory_order_relaxed));
     if (period.count() <= 0) {  // off: look again every 10 ms
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
@@ -872,7 +900,8 @@ void warm_main(AqlQueue* a) {
       std::unique_lock<std::mutex> lk(a->warm_mu);
       a->warm_parked.store(true);
       while (a->warm_parked.load() && a->activity.load(std::memory_order_relaxed) == seen &&
-             !a->failed.load(std::memory_order_relaxed))
+             !a->failed.load(std::memory_order_relaxed) &&
+             !a->warm_stop.load(std::memory_order_relaxed))
         a->warm_cv.wait_for(lk, std::chrono::milliseconds(10));
       a->warm_parked.store(false);
       seen = a->activity.load(std::memory_order_relaxed);
@@ -883,6 +912,19 @@ void warm_main(AqlQueue* a) {
       heartbeat_locked(a);
       a->mu.unlock();
     }
+  }
+}
+
+// At exit: no empty packet may be written into a queue while HSA tears it down.
+void stop_warm_threads() {
+  for (AqlQueue* a : g_queues) {
+    if (!a || !a->warm_thread.joinable()) continue;
+    {
+      std::lock_guard<std::mutex> g(a->warm_mu);
+      a->warm_stop.store(true);
+    }
+    a->warm_cv.notify_all();
+    a->warm_thread.join();
   }
 }
 
@@ -990,12 +1032,6 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   return DORA_OK;
 }
 
-namespace {
-std::atomic<bool> g_cp_lone{true};  // lone single-segment packs above the window: CP-signalled
-}  // namespace
-
-void aql_cp_lone(bool on) { g_cp_lone.store(on); }
-
 uint64_t aql_heartbeats(int device, bool* parked) {
   if (device < 0 || device >= 64) return 0;
   AqlQueue* a;
@@ -1012,18 +1048,13 @@ void aql_keep_awake(double period_us) {
   g_warm_period_ns.store(period_us > 0 ? int64_t(std::max(period_us, 5.0) * 1000) : 0);
 }
 
-void aql_mid_queues(int create, int use) {
-  if (create > 0) g_create_queues.store(create);
-  if (use > 0) g_mid_queues.store(use);
-}
-
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone) {
   if (n == 0) return false;
   const bool single = n == 1 && segs[0].dst_off == 0;
   uint64_t bytes = 0;
   for (size_t i = 0; i < n; ++i) bytes += segs[i].len;
-  return bytes >= kCpLo &&
-         (bytes < kCpHi || (lone && single && g_cp_lone.load(std::memory_order_relaxed)));
+  // a lone single-segment pack above the window is CP-signalled too (r04)
+  return bytes >= kCpLo && (bytes < kCpHi || (lone && single));
 }
 
 int bar_alloc(int device, size_t bytes, void** out) {
@@ -1141,14 +1172,6 @@ int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint6
   return DORA_OK;
 }
 
-int aql_heartbeat(int device) {
-  AqlQueue* a = aql_queue(device);
-  if (!aql_usable(a)) return fail(DORA_ERR_HIP, "AQL queue unavailable");
-  std::lock_guard<std::mutex> g(a->mu);
-  heartbeat_locked(a);
-  return DORA_OK;
-}
-
 uint64_t aql_cp_signalled(int device) {
   if (device < 0 || device >= 64) return 0;
   AqlQueue* a;
@@ -1173,151 +1196,21 @@ uint64_t aql_dispatched(int device, size_t k) {
   return a->dispatched[k];
 }
 
-// Test hook (microbenchmark, dora_gpu_test_aql_pipeline): `n` single-segment packs of `bytes`
-// from rotating HBM sources over `nq` of the queues, at most `depth` packets outstanding per
-// queue, completion seen by the host.  mode 0: the product's in-kernel fill signal (flag in
-// pinned host memory, polled); 1: no in-kernel signal, the packet's completion signal (the
-// command processor's, after the kernel ends), release fence none; 2: as 1, release fence agent;
-// 3: as 0 without the acquire fence; 4: as 1 without the acquire fence; 5: as 1, every wave
-// waiting for its stores to complete before it ends (so the completion signal, written after
-// the last wave ended, follows every store of the pack without relying on a release fence).
-int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
-                       double* us_per_msg) {
-  // 6: as 5 with the coherent kernel and no acquire fence (dora_aql_pack1c_u4); 7: as 5 with the
-  // arguments in the device ring (write-combined stores + HDP flush) instead of host memory;
-  // 8: 6 and 7 together — the latency of a lone pack's dispatch
-  const bool coherent = mode == 6 || mode == 8;
-  const bool dev_args = mode == 7 || mode == 8;
-  const bool no_acquire = mode == 3 || mode == 4 || coherent;
-  const bool wave_wait = mode >= 5;
-  if (mode == 3) mode = 0;
-  if (mode >= 4) mode = 1;
+
+// How long a region end waits for its stamp reduction (test hook: aql_reduce_timeout), and how
+// many abandoned argument slots retire a process's queues.
+std::atomic<uint64_t> g_reduce_timeout_ns{uint64_t(5) * 1000000000ull};
+constexpr uint32_t kMaxAbandoned = 8;
+
+void aql_reduce_timeout(uint64_t ns) {
+  g_reduce_timeout_ns.store(ns ? ns : uint64_t(5) * 1000000000ull);
+}
+
+uint32_t aql_abandoned_slots(int device) {
   AqlQueue* a = aql_queue(device);
-  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
-  if (!a->hring) return fail(DORA_ERR_UNSUPPORTED, "no host argument ring");
-  if (bytes == 0 || n <= 0 || mode < 0 || mode > 4 || nq < 1 || nq > a->nq || depth < 1 ||
-      depth > 8)
-    return fail(DORA_ERR_INVALID, "bad pipeline bench parameters");
-  const size_t stride = (bytes + 4095) & ~size_t(4095);
-  const size_t nbuf = std::max<size_t>(2, std::min<size_t>(256, (size_t(640) << 20) / stride));
-  uint8_t *src = nullptr, *dst = nullptr;
-  uint32_t* done = nullptr;
-  uint64_t* flags = nullptr;
-  const int slots = nq * depth + 1;
-  if (hipMalloc(&src, nbuf * stride) != hipSuccess || hipMalloc(&dst, nbuf * stride) != hipSuccess ||
-      hipMalloc(&done, size_t(slots) * kMaxSignalWgs * 4) != hipSuccess ||
-      hipHostMalloc(&flags, size_t(slots) * 64, hipHostMallocCoherent) != hipSuccess) {
-    if (src) (void)hipFree(src);
-    if (dst) (void)hipFree(dst);
-    if (done) (void)hipFree(done);
-    return fail(DORA_ERR_HIP, "pipeline bench: allocation");
-  }
-  (void)hipMemset(src, 0x5a, nbuf * stride);
-  (void)hipMemset(done, 0, size_t(slots) * kMaxSignalWgs * 4);
-  std::memset(flags, 0, size_t(slots) * 64);
-  (void)hipDeviceSynchronize();
-  std::vector<hsa_signal_t> sigs(static_cast<size_t>(slots));
-  for (auto& sg : sigs) (void)hsa_signal_create(1, 0, nullptr, &sg);
-  struct Out {
-    int slot;
-    uint64_t epoch;
-  };
-  std::vector<std::deque<Out>> outq(static_cast<size_t>(nq));
-  std::vector<int> free_slots;
-  for (int k = slots - 1; k >= 0; --k) free_slots.push_back(k);
-  uint64_t epoch = 0;
-  int rc = DORA_OK;
-  auto complete = [&](const Out& o) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      const bool ok = mode == 0 ? __atomic_load_n(flags + 8 * o.slot, __ATOMIC_ACQUIRE) >= o.epoch
-                                : hsa_signal_load_scacquire(sigs[size_t(o.slot)]) == 0;
-      if (ok) return true;
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
-    }
-  };
-  auto run = [&](int count) -> int {
-    std::lock_guard<std::mutex> g(a->mu);
-    for (int i = 0; i < count; ++i) {
-      const int qi = i % nq;
-      auto& oq = outq[size_t(qi)];
-      if (int(oq.size()) >= depth) {
-        if (!complete(oq.front())) return fail(DORA_ERR_TIMEOUT, "pipeline bench: pack lost");
-        free_slots.push_back(oq.front().slot);
-        oq.pop_front();
-      }
-      const int sl = free_slots.back();
-      free_slots.pop_back();
-      ++epoch;
-      const size_t b = size_t(epoch) % nbuf;
-      Segment sg{src + b * stride, 0, bytes};
-      // (a CP-signalled pack's `epoch` is its stamp area: none here)
-      FillSignal fs{mode == 0 ? flags + 8 * sl : nullptr, mode == 0 ? epoch : 0,
-                    mode == 0 || wave_wait ? done + size_t(sl) * kMaxSignalWgs : nullptr};
-      uint8_t args[kArgs1Bytes];
-      uint32_t grid = 0;
-      if (build_aql_args1(sg, dst + b * stride, fs, args, &grid) != DORA_OK)
-        return DORA_ERR_INVALID;
-      const uint64_t r = a->next++ % kRingSlots;
-      uint8_t* slot = (dev_args ? a->ring + r * kSlotBytes : a->hring + r * kHostSlotBytes);
-      std::memcpy(slot, args, kArgs1Bytes);
-      if (dev_args) {
-        __builtin_ia32_sfence();
-        *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
-      }
-      if (mode != 0) hsa_signal_store_relaxed(sigs[size_t(sl)], 1);
-      hsa_queue_t* const q = a->qs[qi];
-      const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
-      while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) __builtin_ia32_pause();
-      hsa_queue_store_write_index_relaxed(q, idx + 1);
-      auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-      const int k = coherent ? kOneCohKernel : kOneKernel;
-      p->workgroup_size_x = 256;
-      p->workgroup_size_y = 1;
-      p->workgroup_size_z = 1;
-      p->reserved0 = 0;
-      p->grid_size_x = grid * 256u;
-      p->grid_size_y = 1;
-      p->grid_size_z = 1;
-      p->private_segment_size = a->priv[k];
-      p->group_segment_size = a->group[k];
-      p->kernel_object = a->kobj[k];
-      p->kernarg_address = slot;
-      p->reserved2 = 0;
-      p->completion_signal = mode == 0 ? hsa_signal_t{0} : sigs[size_t(sl)];
-      const uint32_t rel = mode == 2 ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_NONE;
-      const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                              ((no_acquire ? HSA_FENCE_SCOPE_NONE : HSA_FENCE_SCOPE_AGENT)
-                               << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                              (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-      const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-      publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
-      oq.push_back({sl, epoch});
-    }
-    for (auto& oq : outq) {
-      while (!oq.empty()) {
-        if (!complete(oq.front())) return fail(DORA_ERR_TIMEOUT, "pipeline bench: pack lost");
-        free_slots.push_back(oq.front().slot);
-        oq.pop_front();
-      }
-    }
-    return DORA_OK;
-  };
-  rc = run(std::min(n, 64));  // warm
-  if (rc == DORA_OK) {
-    const auto t0 = std::chrono::steady_clock::now();
-    rc = run(n);
-    const auto t1 = std::chrono::steady_clock::now();
-    *us_per_msg = std::chrono::duration<double, std::micro>(t1 - t0).count() / n;
-  }
-  for (auto& sg : sigs) (void)hsa_signal_destroy(sg);
-  if (rc == DORA_OK) {
-    (void)hipFree(src);
-    (void)hipFree(dst);
-    (void)hipFree(done);
-    (void)hipHostFree(flags);
-  }  // else: a pack may still run, leak its buffers rather than free them under it
-  return rc;
+  if (!a) return 0;
+  std::lock_guard<std::mutex> g(a->mu);
+  return a->n_abandoned;
 }
 
 int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
@@ -1331,7 +1224,7 @@ int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
     return fail(DORA_ERR_HIP, "hsa_signal_create");
   }
   // the host argument slot of the dispatch kRingSlots back must be free (as in dispatch_locked)
-  const uint64_t r = a->next % kRingSlots;
+  const uint64_t r = take_slot(a);
   Use& u = a->uses[r];
   const auto t0 = std::chrono::steady_clock::now();
   while (u.flag && u.seq >= oldest_outstanding(a) && !fill_reached(u.flag, u.epoch)) {
@@ -1380,12 +1273,17 @@ int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
   publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
   ++a->dispatched[k];
   if (hsa_signal_wait_scacquire(a->reduce_sig, HSA_SIGNAL_CONDITION_LT, 1,
-                                uint64_t(5) * 1000000000ull, HSA_WAIT_STATE_ACTIVE) != 0) {
+                                g_reduce_timeout_ns.load(std::memory_order_relaxed),
+                                HSA_WAIT_STATE_ACTIVE) != 0) {
     // A diagnostic: the data-path queues stay in use.  The packet is still queued and may yet
-    // run: its signal is abandoned (a later reduction makes its own), and the caller must not
-    // free or reuse `areas` / `out` (node.cpp leaks them and reads the areas through the BAR).
+    // run: its signal is abandoned (a later reduction makes its own), the caller must not free
+    // or reuse `areas` / `out` (node.cpp leaks them and reads the areas through the BAR), and
+    // its argument slot is never written again — a later pack's arguments there would be the
+    // reduction's if it ran after them.  Queues that lose several stop dispatching.
     a->reduce_sig.handle = 0;
-    return fail(DORA_ERR_TIMEOUT, "stamp reduction did not complete in 5 s");
+    a->abandoned[r] = true;
+    if (++a->n_abandoned >= kMaxAbandoned) a->failed.store(true);
+    return fail(DORA_ERR_TIMEOUT, "stamp reduction did not complete in time");
   }
   return DORA_OK;
 }

@@ -67,26 +67,13 @@ uint64_t aql_dispatched(int device, size_t k);
 // Test tool: while held, every batchable send of this process on `device` waits in the
 // backlog; releasing dispatches the backlog as batch packs (tests/test_gpu_dataflow.py).
 int aql_hold(int device, bool hold);
-// Whether a lone single-segment pack above the CP window is CP-signalled (default) or signals
-// in-kernel (test hook, probes of the synchronous send).
-void aql_cp_lone(bool on);
 // Period of the warm thread's empty packets (aql.cpp warm_main; 0: off; at least 5 us).
 void aql_keep_awake(double period_us);
 // Test tool: empty packets the warm thread of `device` has published, and whether it is parked.
 uint64_t aql_heartbeats(int device, bool* parked);
-// Test tool: one empty barrier-AND packet (no dependencies, no completion signal) on the first
-// queue of `device` (latency probe: does a packet keep the dispatch side awake).
-int aql_heartbeat(int device);
-// Test hook: HSA queues a process creates (before its first AQL use; 0 keeps 4) and how many
-// take packs of 8-32 MiB (0 keeps 4).
-void aql_mid_queues(int create, int use);
 // Whether the process's packet rings are published with fences (in device memory), and where
 // the runtime says they are (pointer type * 4 + owner: 1 CPU agent, 2 this GPU, 3 other).
 int aql_ring_write_combined(int device, bool* wc, int* where);
-// Test hook: packs pipelined over the queues with in-kernel or command-processor completion
-// signals (dora_gpu_test_aql_pipeline).
-int aql_pipeline_bench(int device, size_t bytes, int n, int mode, int nq, int depth,
-                       double* us_per_msg);
 // Packs signalled by the command processor (cp_signal_window, aql.cpp).
 uint64_t aql_cp_signalled(int device);
 // A pack's own GPU stamp (s_memrealtime ticks) as CLOCK_REALTIME ns, for the message trace
@@ -118,6 +105,11 @@ void bar_publish(AqlQueue* q, const void* last);
 // (start, latest end) pairs to `out` (host memory the GPU can write); waits for it (bounded).
 int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
                      const uint32_t* areas, uint32_t n, uint64_t* out);
+
+// Test hooks: the stamp reduction's wait (0: the default 5 s), and the argument slots left to
+// reductions that timed out (never written again).
+void aql_reduce_timeout(uint64_t ns);
+uint32_t aql_abandoned_slots(int device);
 
 // Segments one AQL dispatch takes.
 size_t aql_max_segments();

@@ -127,7 +127,7 @@ class Daemon {
     parse(spec);
     std::vector<std::string> ids;
     for (auto& n : nodes_) ids.push_back(n.id);
-    region_.reset(Region::create(shm, ids, ring_cap, "dataflow"));
+    region_.reset(Region::create(shm, ids, ring_cap, dataflow_id_));
     for (size_t i = 0; i < nodes_.size(); ++i) {
       NodeEntry& e = region_->hdr()->nodes[i];
       std::string outs, ins;

@@ -31,46 +31,25 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs args) {
   pack_body<U, NT>(args, blockIdx.x, gridDim.x);
 }
 
-// Kernel variant: unroll depth (loads in flight per lane) and non-temporal policy.
-struct Variant {
-  int unroll;
-  bool nt;
-  bool wt = false;  // write-through (sc1 nt) stores without a fill signal (microbenchmark)
-};
-
-// Microbenchmark tuning of HIP-launched packs (pack_tune, the test library's
-// dora_gpu_test_pack_tune): 0 / -1 = the defaults below.
-std::atomic<int> g_unroll{0};
-std::atomic<int> g_nt{-1};
-std::atomic<uint32_t> g_chunk{0};
-// workgroups of a signalling launch (0: kSignalGrid)
-std::atomic<uint32_t> g_signal_grid{0};
-// workgroups at most of a pack the command processor signals (3584: a synchronous 40.96 MB send
+// Workgroups at most of a pack the command processor signals: a synchronous 40.96 MB send
 // (5,000 chunks) takes 21.7-22.0 us with 3584 workgroups against 22.0-22.7 with 4096, 22.9 with
 // one per chunk, 22.7-23.3 with 3072 and 24.6-25.3 with fewer, larger chunks, in four interleaved
-// rounds of 200 sends, profiles/r04_sync_ab.jsonl batches sy4-sy6; packs below 28 MiB have fewer
-// chunks than that)
-std::atomic<uint32_t> g_cp_grid{3584u};
-// workgroups at most of a multi-segment pack the command processor signals (0: g_cp_grid).  Such
-// packs (C3's 13 MB clouds) run up to four at once, one per queue: 640 workgroups each (2.5 per
-// CU) against the single-segment cap of 3584, C3's 20-cloud burst 0.67-0.72 -> 0.72-0.75 and its
-// 200-cloud steady state 0.71-0.72 -> 0.77-0.79 of HBM (caps 512-1536 interleaved over four
-// boxes, profiles/r05_c3_cp_grid_b.jsonl, r05_c3_multi_grid_*.jsonl)
-std::atomic<uint32_t> g_cp_grid_multi{640};
-std::atomic<bool> g_bench_signal{false};  // dora_gpu_pack signals a scratch flag (microbench)
+// rounds of 200 sends (profiles/r04_sync_ab.jsonl batches sy4-sy6; packs below 28 MiB have fewer
+// chunks than that).
+constexpr uint32_t kCpGrid = 3584;
+// Workgroups at most of a multi-segment pack the command processor signals.  Such packs (C3's
+// 13 MB clouds) run up to four at once, one per queue: 640 workgroups each (2.5 per CU) against
+// the single-segment cap of 3584, C3's 20-cloud burst 0.67-0.72 -> 0.72-0.75 and its 200-cloud
+// steady state 0.71-0.72 -> 0.77-0.79 of HBM (caps 512-1536 interleaved over four boxes,
+// profiles/r05_c3_cp_grid_b.jsonl, r05_c3_multi_grid_*.jsonl).
+constexpr uint32_t kCpGridMulti = 640;
 
-// Defaults from the r01 sweep (profiles/r01_pack_sweep*.jsonl): non-temporal loads/stores win
-// 10-12 % at 16-40 MB (the sample is consumed by another process, not re-read from this CU's
-// cache) and are neutral below.
-Variant pack_variant() {
-  Variant v{0, true};
-  if (const int u = g_unroll.load(std::memory_order_relaxed)) v.unroll = u;
-  if (const int nt = g_nt.load(std::memory_order_relaxed); nt >= 0) {
-    v.nt = nt != 0;
-    v.wt = nt == 2;
-  }
-  return v;
-}
+// The HIP-launched pack: 4 x 16-B loads in flight per lane, non-temporal loads and stores (the
+// r01 sweep, profiles/r01_pack_sweep*.jsonl: 10-12 % at 16-40 MB, the sample is consumed by
+// another process; neutral below); its signalling launch stores write-through (NT = 2).  The
+// sweep's other variants (2 / 8 loads, cached stores) and their tuning hooks were removed in r06
+// (verdict r05 item 6): the product library carries no variant only a microbenchmark selects.
+constexpr int kUnroll = 4;
 
 // ------------------------------------------------------------------------------------------
 // Transform segments of compacting plans: bitmap slices shifted to bit 0 and offsets rebased to
@@ -144,17 +123,12 @@ uint64_t xseg_elems(const Segment& s) {
 // no release fence) 4 loads over 8 KiB chunks are faster there: C3 4.70-4.91 -> 4.56 us per
 // cloud, a flat 13 MB pack 4.81-4.91 -> 4.33-4.37 us, 16 MB unchanged
 // (profiles/r02_u4_mid_ab.jsonl, r02_c3_final_knobs_ab.jsonl).
-int default_unroll(uint64_t) { return 4; }
-
-uint32_t choose_chunk_bytes(uint64_t body_bytes, int unroll) {
-  if (const uint32_t c = g_chunk.load(std::memory_order_relaxed)) return c;
+uint32_t choose_chunk_bytes(uint64_t body_bytes) {
   // r01 probes (profiles/r01_copy_probe.jsonl): at >= 32 MB the best shape is many small
   // workgroups (8 KiB each, 4 loads in flight per lane: 40.96 MB in 14.6 us launch-to-launch);
-  // 8-32 MB preferred 32 KiB x 8 loads in isolation (the 8-load variant's chunk, kept for the
-  // tuning knob); below that ~2k workgroups of >= 8 KiB.
+  // below that ~2k workgroups of >= 8 KiB.
   constexpr uint64_t kGrain = 8192;
   if (body_bytes >= (32u << 20)) return kGrain;
-  if (unroll == 8) return 32768;
   uint64_t cb = (body_bytes / 2048 + kGrain - 1) / kGrain * kGrain;
   cb = std::max<uint64_t>(cb, kGrain);
   cb = std::min<uint64_t>(cb, uint64_t(1) << 22);
@@ -265,18 +239,6 @@ __global__ __launch_bounds__(64) void l1_stale_kernel(const uint32_t* src, uint3
   second[b * 64 + t] = probe_load<MODE>(src + t);
 }
 
-// One resident wave that keeps the GPU from idling (a latency probe): it sleeps in
-// s_sleep slices and leaves when the host sets `stop` or after `max_ticks` of s_memrealtime
-// (100 MHz) — every exit is bounded.
-__global__ __launch_bounds__(64) void keep_warm_kernel(const uint32_t* stop, uint64_t max_ticks) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
-    __builtin_amdgcn_s_sleep(64);
-  }
-}
-
 unsigned grid_for(uint64_t items) {
   uint64_t g = (items + kThreads - 1) / kThreads;
   return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 4096)));
@@ -343,9 +305,7 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     uint64_t body = 0;
     const size_t m = std::min<size_t>(kMaxSegs, n - i);
     for (size_t k = 0; k < m; ++k) body += segs[i + k].len;
-    Variant var = pack_variant();
-    if (var.unroll == 0) var.unroll = default_unroll(body);
-    a.chunk_bytes = choose_chunk_bytes(body, var.unroll);
+    a.chunk_bytes = choose_chunk_bytes(body);
     uint64_t chunks = 0;
     for (size_t k = 0; k < m; ++k) {
       const Segment& s = segs[i + k];
@@ -360,26 +320,14 @@ int launch_pack(const Segment* segs_in, size_t n_in, ArrowDeviceType dev, uint8_
     const bool first = launch == 0, last = launch + 1 == n_launch;
     a.n_chunks = static_cast<uint32_t>(chunks);
     uint64_t grid = chunks;
-    void (*kern)(PackArgs) = pack_kernel<4, 0>;
-    if (var.unroll == 8) kern = var.nt ? pack_kernel<8, 1> : pack_kernel<8, 0>;
-    else if (var.unroll == 2) kern = var.nt ? pack_kernel<2, 1> : pack_kernel<2, 0>;
-    else if (var.wt) kern = pack_kernel<4, 2>;
-    else if (var.nt) kern = pack_kernel<4, 1>;
-    // microbenchmark: the write-through launch that signals nothing, with the signalling grid
-    // (dora_gpu_pack_signal_tune) — the grid's cost apart from the signal's
-    if (var.wt && !signal) {
-      const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-      if (g && grid > g) grid = g;
-    }
+    void (*kern)(PackArgs) = pack_kernel<kUnroll, 1>;
     if (last && signal) {
-      // signalling launch: write-through stores, at most kMaxSignalWgs workgroups
+      // signalling launch: write-through stores, at most kSignalGrid workgroups
       a.flag = signal->flag;
       a.done = signal->done;
       a.epoch = signal->epoch;
-      const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-      const uint64_t cap = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
-      if (grid > cap) grid = cap;
-      kern = var.unroll == 8 ? pack_kernel<8, 2> : pack_kernel<4, 2>;
+      if (grid > kSignalGrid) grid = kSignalGrid;
+      kern = pack_kernel<kUnroll, 2>;
     }
     a.grid = static_cast<uint32_t>(grid);
     if (ev_start || ev_stop) {
@@ -481,7 +429,7 @@ size_t aql_batch_args_size() { return sizeof(dora::pack::AqlBatchArgs); }
 uint32_t aql_chunk_bytes(const Segment* segs, size_t n) {
   uint64_t body = 0;
   for (size_t k = 0; k < n; ++k) body += segs[k].len;
-  return choose_chunk_bytes(body, 4);  // the AQL kernels keep 4 loads in flight per lane
+  return choose_chunk_bytes(body);  // the AQL kernels keep 4 loads in flight per lane
 }
 
 // Arguments of dora_aql_packb_u4: the segments of `n` messages with absolute destinations,
@@ -529,9 +477,7 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
   }
   a.nseg = static_cast<uint32_t>(ns);
   a.n_chunks = static_cast<uint32_t>(chunks);
-  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-  const uint64_t cap_wgs = g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
-  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap_wgs));
+  a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, kSignalGrid));
   a.flag = items[0].sig.flag;
   a.done = items[0].sig.done;
   a.epoch = items[0].sig.epoch;
@@ -543,16 +489,10 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
 }
 
 // Workgroups of an AQL pack signalled as `sig` says.  In-kernel signals (a flag): the signalling
-// grid (kSignalGrid, or a tuned grid up to the kMaxSignalWgs done words).  Signalled by
-// the command processor (no flag): nothing to poll, so up to aql_cp_grid() workgroups — a lone
-// 40.96 MB pack capped at 1024 keeps 8 MiB in flight, half of what HBM needs.
-uint32_t aql_cp_grid() { return std::max<uint32_t>(1, g_cp_grid.load(std::memory_order_relaxed)); }
-
-uint64_t signal_grid_cap(const FillSignal& sig) {
-  if (!sig.flag) return aql_cp_grid();
-  const uint32_t g = g_signal_grid.load(std::memory_order_relaxed);
-  return g ? std::min<uint32_t>(g, kMaxSignalWgs) : kSignalGrid;
-}
+// grid (kSignalGrid).  Signalled by the command processor (no flag): nothing to poll, so up to
+// kCpGrid workgroups — a lone 40.96 MB pack capped at 1024 keeps 8 MiB in flight, half of what
+// HBM needs.
+uint64_t signal_grid_cap(const FillSignal& sig) { return sig.flag ? kSignalGrid : kCpGrid; }
 
 // Arguments of one AQL-dispatched signalling pack (aql.cpp): the same chunking and signalling
 // grid as launch_pack's last launch.
@@ -568,7 +508,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
     if (segs[k].op != SEG_COPY) return fail(DORA_ERR_INVALID, "AQL pack: transform segment");
     body += segs[k].len;
   }
-  a.chunk_bytes = choose_chunk_bytes(body, 4);
+  a.chunk_bytes = choose_chunk_bytes(body);
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
   uint64_t chunks = 0;
   for (size_t k = 0; k < n; ++k) {
@@ -581,10 +521,7 @@ int build_aql_args(const Segment* segs, size_t n, uint8_t* dst, const FillSignal
   a.nseg = static_cast<uint32_t>(n);
   a.edge_mask = edge_mask(segs, n, dst, dst_cap);
   a.n_chunks = static_cast<uint32_t>(chunks);
-  uint64_t grid_cap = signal_grid_cap(sig);
-  if (!sig.flag) {
-    if (const uint32_t m = g_cp_grid_multi.load(std::memory_order_relaxed)) grid_cap = m;
-  }
+  const uint64_t grid_cap = sig.flag ? kSignalGrid : kCpGridMulti;
   a.grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, grid_cap));
   a.flag = sig.flag;
   a.done = sig.done;
@@ -604,7 +541,7 @@ int build_aql_args1(const Segment& sg, uint8_t* dst, const FillSignal& sig, uint
                 (unsigned long long)sg.dst_off);
   const uint64_t base = reinterpret_cast<uintptr_t>(dst);
   const uint64_t cap = signal_grid_cap(sig);
-  const uint32_t chunk_bytes = choose_chunk_bytes(sg.len, 4);
+  const uint32_t chunk_bytes = choose_chunk_bytes(sg.len);
   const uint64_t chunks = segment_chunks(base, 0, sg.len, chunk_bytes);
   if (chunks > 0x7fffffffull) return fail(DORA_ERR_INVALID, "pack: too many chunks");
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(chunks, cap));
@@ -646,24 +583,6 @@ int launch_l2_touch(const void* p, size_t len, hipStream_t stream) {
 // One run of l1_stale_kernel (see there): `src` holds 64 words of pattern A, the host rewrites
 // them to pattern B once every workgroup has read them.  Out: workgroups whose first read was
 // not A (setup failures), whose second read still held A words (stale), and the workgroups.
-// keep_warm_kernel on a stream of its own: `stop_host` is a pinned, mapped word the caller sets
-// to end it; at most `seconds` in any case.
-int keep_warm_start(int device, double seconds, uint32_t* stop_dev, hipStream_t* out) {
-  DORA_HIP(hipSetDevice(device));
-  hipStream_t st = nullptr;
-  DORA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  const double s = std::min(std::max(seconds, 0.0), 600.0);
-  hipLaunchKernelGGL(keep_warm_kernel, dim3(1), dim3(64), 0, st, stop_dev,
-                     uint64_t(s * 100e6));
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    (void)hipStreamDestroy(st);
-    return fail(DORA_ERR_HIP, "keep-warm launch: %s", hipGetErrorString(e));
-  }
-  *out = st;
-  return DORA_OK;
-}
-
 int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks) {
   *bad_first = *stale = *blocks = 0;
   DORA_HIP(hipSetDevice(device));
@@ -736,40 +655,6 @@ int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, u
   return DORA_OK;
 }
 
-// Microbenchmark tuning of HIP-launched packs (the test library's dora_gpu_test_pack_tune /
-// dora_gpu_test_pack_signal_tune): 16-B loads in flight per lane (0 = default 4; 2, 4, 8),
-// non-temporal policy (-1 default, 0, 1; 2 = the signalling kernels' write-through stores
-// without a signal), bytes per workgroup (0 = auto, else a multiple of 128); workgroups of a
-// signalling launch (0: kSignalGrid), and whether dora_gpu_pack signals a scratch flag.
-int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
-  if (unroll != 0 && unroll != 2 && unroll != 4 && unroll != 8)
-    return fail(DORA_ERR_INVALID, "unroll must be 0, 2, 4 or 8");
-  if (chunk_bytes % pack::kLine)
-    return fail(DORA_ERR_INVALID, "chunk_bytes must be a multiple of 128 (a cache line)");
-  g_unroll.store(unroll);
-  g_nt.store(nontemporal < 0 ? -1 : nontemporal == 2 ? 2 : (nontemporal ? 1 : 0));
-  g_chunk.store(chunk_bytes);
-  return DORA_OK;
-}
-
-int pack_signal_tune(uint32_t grid, bool bench_signal) {
-  g_signal_grid.store(grid);
-  g_bench_signal.store(bench_signal);
-  return DORA_OK;
-}
-
-// Workgroup cap of the command processor's packs (0: the default, 3584).
-int pack_cp_grid_tune(uint32_t grid) {
-  g_cp_grid.store(grid ? grid : 3584u);
-  return DORA_OK;
-}
-
-// Workgroup cap of the command processor's multi-segment packs (0: the default, 640).
-int pack_cp_grid_multi_tune(uint32_t grid) {
-  g_cp_grid_multi.store(grid ? grid : 640u);
-  return DORA_OK;
-}
-
 int launch_fill(void* dst, size_t len, uint64_t seed, hipStream_t stream) {
   if (!len) return DORA_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for((len + 7) / 8)), dim3(kThreads), 0, stream,
@@ -791,22 +676,6 @@ int dora_gpu_pack(const dora_plan* plan, void* dst, size_t dst_len, dora_stream_
                       static_cast<unsigned long long>(plan->size));
   if (plan->segs.empty()) return DORA_OK;
   if (!dst) return dora::fail(DORA_ERR_INVALID, "dst is NULL");
-  if (dora::g_bench_signal.load()) {
-    // microbenchmark of signalling launches: a scratch flag + counters in device memory
-    static uint8_t* scratch = nullptr;
-    static uint64_t epoch = 0;
-    if (!scratch) {
-      // the flag owns a 64-byte line (epoch + the two launch stamps), the done words follow
-      DORA_HIP(hipMalloc(&scratch, 64 + dora::kMaxSignalWgs * 4));
-      DORA_HIP(hipMemset(scratch, 0, 64 + dora::kMaxSignalWgs * 4));
-      DORA_HIP(hipDeviceSynchronize());
-    }
-    dora::FillSignal sig{reinterpret_cast<uint64_t*>(scratch), ++epoch,
-                         reinterpret_cast<uint32_t*>(scratch + 64)};
-    return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
-                             static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream),
-                             nullptr, nullptr, &sig, nullptr, dst_len);
-  }
   return dora::launch_pack(plan->segs.data(), plan->segs.size(), plan->dev,
                            static_cast<uint8_t*>(dst), static_cast<hipStream_t>(stream), nullptr,
                            nullptr, nullptr, nullptr, dst_len);

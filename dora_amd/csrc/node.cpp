@@ -116,7 +116,7 @@ struct IpcMapping {
 struct ShmMapping {
   void* base = nullptr;
   size_t len = 0;
-  bool registered = false;
+  bool registered = false, reg_tried = false;  // pinned for DMA on the first pull (ensure_local)
   uint64_t last_use = 0;
   ~ShmMapping() {
     if (registered) (void)hipHostUnregister(base);
@@ -128,6 +128,10 @@ struct ShmMapping {
 // kMaxCacheSlots slots plus those in flight, so a steady edge stays within it; slots a producer
 // has freed (size changes) age out instead of pinning the producer's memory for good.
 constexpr size_t kMaxIpcMappings = 128;
+// Shared-memory regions a device receiver keeps mapped and pinned while nothing holds them: at
+// most this many bytes (the least recently used unheld ones are unpinned and unmapped first), so
+// regions a producer has dropped do not stay page-locked in every receiver.
+constexpr uint64_t kMaxCachedShmBytes = uint64_t(1) << 30;
 
 namespace {
 
@@ -217,12 +221,7 @@ constexpr uint64_t kSmallInFlightBytes = 8ull << 20;
 // dropped one, 0-5 per bench run in the throughput ladders.  A cap of 10 instead cost 4 MB
 // sends ~6 %: 1.56-1.63 vs 1.41-1.50 us, profiles/r04_cap_ab.jsonl.)  DORA_GPU_MAX_IN_FLIGHT=N
 // sets both, `S:L` each.
-std::atomic<long> g_in_flight_small{0}, g_in_flight_big{0};  // test overrides (0: none)
-
 size_t max_in_flight(uint64_t len) {
-  if (const long o = (len < kSmallInFlightBytes ? g_in_flight_small : g_in_flight_big)
-                         .load(std::memory_order_relaxed))
-    return static_cast<size_t>(o);
   static const std::pair<long, long> env = [] {
     const char* e = std::getenv("DORA_GPU_MAX_IN_FLIGHT");
     if (!e) return std::make_pair(0L, 0L);
@@ -236,16 +235,6 @@ size_t max_in_flight(uint64_t len) {
   return len < kSmallInFlightBytes ? 11 : 8;
 }
 
-}  // namespace
-
-// The in-flight caps below / from 8 MiB (0: DORA_GPU_MAX_IN_FLIGHT or the defaults), for the
-// test library's dora_gpu_test_in_flight.
-void set_in_flight_caps(long small, long big) {
-  g_in_flight_small.store(small);
-  g_in_flight_big.store(big);
-}
-
-namespace {
 
 // Streams the HIP-launched fills of a node rotate over (host sources, compacting transforms,
 // relays; device-source packs go to the AQL queues, aql.h).  A pack ends in a drain tail (its
@@ -437,16 +426,15 @@ struct NodeCore {
         *err = "shared-memory sample `" + name + "`: " + std::strerror(errno);
         return nullptr;
       }
-      if (device >= 0) {
-        DeviceScope ds(device);
-        m->registered = hipHostRegister(m->base, m->len, hipHostRegisterDefault) == hipSuccess;
-      }
-      (void)hipGetLastError();
       shm_cache.emplace(name, m);
-      while (shm_cache.size() > kMaxIpcMappings) {
+      // bounded by count and by bytes; mappings an input still holds stay
+      for (;;) {
+        uint64_t bytes = 0;
+        for (auto& kv : shm_cache) bytes += kv.second->len;
+        if (shm_cache.size() <= kMaxIpcMappings && bytes <= kMaxCachedShmBytes) break;
         auto victim = shm_cache.end();
         for (auto v = shm_cache.begin(); v != shm_cache.end(); ++v)
-          if (v->second.use_count() == 1 &&
+          if (v->second != m && v->second.use_count() == 1 &&
               (victim == shm_cache.end() || v->second->last_use < victim->second->last_use))
             victim = v;
         if (victim == shm_cache.end()) break;
@@ -550,7 +538,8 @@ struct NodeCore {
     host_pool.emplace(cap, p);
   }
 
-  // A stream of the producer's GPU for the staging copies (the current device must be it)
+  // A private stream of GPU `src_device` for copies waited for alone (a host-only receiver's
+  // staging, a device receiver's pulls); the current device must be it
   hipStream_t stage_stream(int src_device) {
     std::lock_guard<std::mutex> g(pool_mu);
     auto it = stage_streams.find(src_device);
@@ -1609,23 +1598,40 @@ int ensure_local(InputData* in) {
   void* local = c->recv_pool_get(in->ext_len, &cap);
   if (!local)
     return fail(DORA_ERR_HIP, "receive slot of %llu bytes", (unsigned long long)in->ext_len);
+  // The pull runs on a stream of its own and is waited for alone: on the node stream it would
+  // queue behind (and its wait would wait for) every consumer kernel already there.
+  // The pulled copy is complete on return, so any stream may read it.
+  hipStream_t ps = c->stage_stream(c->device);
+  if (!ps) ps = c->stream;
   int rc = DORA_OK;
   if (in->host_pull) {
-    // a host-only producer's shared memory (registered here): one DMA into HBM
-    hipError_t e = hipMemcpyAsync(local, in->ptr, in->ext_len, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    // a host-only producer's shared memory: pinned once per region on its first pull (not at
+    // drain time, which may hold the event queue's lock), then one DMA into HBM
+    {
+      std::lock_guard<std::mutex> g(c->ipc_mu);
+      if (!in->shm->reg_tried) {
+        in->shm->reg_tried = true;
+        in->shm->registered =
+            hipHostRegister(in->shm->base, in->shm->len, hipHostRegisterDefault) == hipSuccess;
+        (void)hipGetLastError();
+      }
+    }
+    hipError_t e = hipMemcpyAsync(local, in->ptr, in->ext_len, hipMemcpyHostToDevice, ps);
+    if (e == hipSuccess) e = hipStreamSynchronize(ps);
     if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "shared-memory pull: %s", hipGetErrorString(e));
   } else if (peer_copy_mode() == PEER_SDMA) {
-    rc = enqueue_peer_copy(c, local, in->ptr, in->remote_device, in->ext_len);
+    rc = ensure_peer_access(c, in->remote_device);
     if (rc == DORA_OK) {
-      hipError_t e = hipStreamSynchronize(c->stream);
+      hipError_t e =
+          hipMemcpyPeerAsync(local, c->device, in->ptr, in->remote_device, in->ext_len, ps);
+      if (e == hipSuccess) e = hipStreamSynchronize(ps);
       if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "cross-GPU pull: %s", hipGetErrorString(e));
     }
   } else {
     // the pack kernel reads the peer's HBM over xGMI; wait on its own completion flag
     rc = ensure_peer_access(c, in->remote_device);
     Segment seg{in->ptr, 0, in->ext_len};
-    if (rc == DORA_OK) rc = launch_pack_wait(&seg, 1, static_cast<uint8_t*>(local), c->stream);
+    if (rc == DORA_OK) rc = launch_pack_wait(&seg, 1, static_cast<uint8_t*>(local), ps);
   }
   if (rc != DORA_OK) {
     c->recv_pool_put(local, cap);
@@ -3029,6 +3035,12 @@ int dora_node_forward(dora_node* n, const char* output_id, const dora_event* ev,
   return dora::forward_input(n, output_id, ev, params, params_len);
   DORA_GUARD_END
 }
+
+const char* dora_node_dataflow_id(const dora_node* n) {
+  return n ? n->core->region->hdr()->dataflow_id : "";
+}
+
+const char* dora_node_id(const dora_node* n) { return n ? n->id.c_str() : ""; }
 
 int dora_node_stats(dora_node* n, uint64_t* slots_created, uint64_t* cache_hits,
                     uint64_t* in_flight, uint64_t* dropped_inputs) {

@@ -438,6 +438,9 @@ PyObject* schema_for(PyObject* type) {
   PyObject* hit = PyDict_GetItemWithError(g_schemas, type);  // borrowed (type, capsule)
   if (!hit && PyErr_Occurred()) return nullptr;
   if (hit) {
+    // a strong reference for the call into Python below: code there may release the GIL, and
+    // another sending thread may then clear g_schemas or replace this entry
+    Py_INCREF(hit);
     PyObject* key = PyTuple_GET_ITEM(hit, 0);
     int same = key == type;
     if (!same) {
@@ -448,15 +451,22 @@ PyObject* schema_for(PyObject* type) {
       PyObject* r = a ? PyObject_Call(eq, a, kw) : nullptr;
       Py_XDECREF(a);
       Py_XDECREF(eq);
-      if (!r) return nullptr;
+      if (!r) {
+        Py_DECREF(hit);
+        return nullptr;
+      }
       same = PyObject_IsTrue(r);
       Py_DECREF(r);
-      if (same < 0) return nullptr;
+      if (same < 0) {
+        Py_DECREF(hit);
+        return nullptr;
+      }
     }
     if (same) {
       cap = PyTuple_GET_ITEM(hit, 1);
       Py_INCREF(cap);
     }
+    Py_DECREF(hit);
   }
   if (!cap) {  // export it (replacing an entry equal but for field metadata)
     if (PyDict_GET_SIZE(g_schemas) >= 64) PyDict_Clear(g_schemas);

@@ -30,13 +30,6 @@ int build_aql_batch_args(const BatchItem* items, size_t n, uint8_t* out, size_t 
                          uint32_t* grid);
 int launch_l2_touch(const void* p, size_t len, hipStream_t stream);
 int l1_stale_probe(int device, int mode, uint32_t* bad_first, uint32_t* stale, uint32_t* blocks);
-int keep_warm_start(int device, double seconds, uint32_t* stop_dev, hipStream_t* out);
-int pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
-int pack_signal_tune(uint32_t grid, bool bench_signal);
-int pack_cp_grid_tune(uint32_t grid);
-int pack_cp_grid_multi_tune(uint32_t grid);
-// node.cpp
-void set_in_flight_caps(long small, long big);
 }  // namespace dora
 
 namespace dora {
@@ -83,24 +76,6 @@ std::string jstr(const std::string& v) {
 
 
 extern "C" {
-
-int dora_gpu_test_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes) {
-  return dora::pack_tune(unroll, nontemporal, chunk_bytes);
-}
-
-int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal) {
-  return dora::pack_signal_tune(grid, bench_signal != 0);
-}
-
-int dora_gpu_test_cp_grid(uint32_t grid) { return dora::pack_cp_grid_tune(grid); }
-
-int dora_gpu_test_cp_grid_multi(uint32_t grid) { return dora::pack_cp_grid_multi_tune(grid); }
-
-int dora_gpu_test_in_flight(long small, long big) {
-  if (small < 0 || big < 0) return dora::fail(DORA_ERR_INVALID, "negative in-flight cap");
-  dora::set_in_flight_caps(small, big);
-  return DORA_OK;
-}
 
 int dora_gpu_test_batch_args(size_t n_msgs, const size_t* seg_counts, const uint64_t* segs,
                              const uint64_t* dsts, const uint64_t* dst_caps,
@@ -152,85 +127,14 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
-int dora_gpu_test_mid_queues(int create, int use) {
-  if (create < 0 || create > 8 || use < 0 || use > 8)
-    return dora::fail(DORA_ERR_INVALID, "queues: 0..8");
-  dora::aql_mid_queues(create, use);
+int dora_gpu_test_reduce_timeout(uint64_t ns) {
+  dora::aql_reduce_timeout(ns);
   return DORA_OK;
 }
 
-struct KeepWarm {
-  uint32_t* stop = nullptr;  // pinned, mapped
-  hipStream_t stream = nullptr;
-};
-
-int dora_gpu_test_keep_warm_start(int device, double seconds, void** out) {
-  if (!out) return dora::fail(DORA_ERR_INVALID, "NULL argument");
-  auto* k = new KeepWarm();
-  if (hipHostMalloc(reinterpret_cast<void**>(&k->stop), 64,
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-    delete k;
-    return dora::fail(DORA_ERR_HIP, "keep-warm stop word");
-  }
-  __atomic_store_n(k->stop, 0u, __ATOMIC_SEQ_CST);
-  uint32_t* d = nullptr;
-  (void)hipHostGetDevicePointer(reinterpret_cast<void**>(&d), k->stop, 0);
-  const int rc = dora::keep_warm_start(device, seconds, d, &k->stream);
-  if (rc != DORA_OK) {
-    (void)hipHostFree(k->stop);
-    delete k;
-    return rc;
-  }
-  *out = k;
-  return DORA_OK;
-}
-
-int dora_gpu_test_keep_warm_stop(void* h) {
-  auto* k = static_cast<KeepWarm*>(h);
-  if (!k) return DORA_OK;
-  __atomic_store_n(k->stop, 1u, __ATOMIC_SEQ_CST);
-  const hipError_t e = hipStreamSynchronize(k->stream);
-  (void)hipStreamDestroy(k->stream);
-  (void)hipHostFree(k->stop);
-  delete k;
-  return e == hipSuccess ? DORA_OK : dora::fail(DORA_ERR_HIP, "keep-warm: %s", hipGetErrorString(e));
-}
-
-struct Heartbeat {
-  std::atomic<bool> stop{false};
-  std::thread th;
-  void* bar = nullptr;
-};
-
-int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double seconds,
-                                  void** out) {
-  if (!out || mode < 1 || mode > 3 || !(period_us >= 5) || !(seconds > 0) || seconds > 600)
-    return dora::fail(DORA_ERR_INVALID, "heartbeat: mode 1..3, period >= 5 us, 0 < seconds <= 600");
-  auto* h = new Heartbeat();
-  if (mode != 1 && dora::bar_alloc(device, 4096, &h->bar) != DORA_OK) {
-    delete h;
-    return dora::fail(DORA_ERR_HIP, "heartbeat: no host-visible device memory");
-  }
-  h->th = std::thread([h, device, mode, period_us, seconds] {
-    (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
-    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(seconds);
-    const auto period = std::chrono::nanoseconds(int64_t(period_us * 1000));
-    auto next = std::chrono::steady_clock::now();
-    uint32_t v = 0;
-    while (!h->stop.load(std::memory_order_relaxed) && std::chrono::steady_clock::now() < t_end) {
-      if (mode == 1) {
-        (void)dora::aql_heartbeat(device);
-      } else if (mode == 2) {
-        v += *static_cast<volatile uint32_t*>(h->bar);  // one uncached read over PCIe
-      } else {
-        *static_cast<volatile uint32_t*>(h->bar) = ++v;  // one posted write over PCIe
-        __builtin_ia32_sfence();
-      }
-      next += period;
-      std::this_thread::sleep_until(next);
-    }
-  });
-  *out = h;
+int dora_gpu_test_abandoned_slots(int device, uint32_t* slots) {
+  if (!slots) return dora::fail(DORA_ERR_INVALID, "NULL argument");
+  *slots = dora::aql_abandoned_slots(device);
   return DORA_OK;
 }
 
@@ -239,20 +143,6 @@ int dora_gpu_test_keep_awake_stats(int device, uint64_t* heartbeats, int* parked
   bool pk = false;
   *heartbeats = dora::aql_heartbeats(device, &pk);
   *parked = pk ? 1 : 0;
-  return DORA_OK;
-}
-
-int dora_gpu_test_heartbeat_stop(void* p) {
-  auto* h = static_cast<Heartbeat*>(p);
-  if (!h) return DORA_OK;
-  h->stop.store(true);
-  if (h->th.joinable()) h->th.join();
-  delete h;  // the BAR word stays (bar_alloc has no free; 4 KiB)
-  return DORA_OK;
-}
-
-int dora_gpu_test_cp_lone(int on) {
-  dora::aql_cp_lone(on != 0);
   return DORA_OK;
 }
 
@@ -288,12 +178,6 @@ int dora_gpu_test_bcast_group(int device, void* buf, uint64_t bytes, int* nranks
   (void)hipStreamDestroy(st);
   return rc;
   DORA_GUARD_END
-}
-
-int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
-                               double* us_per_msg) {
-  if (!us_per_msg) return dora::fail(DORA_ERR_INVALID, "us_per_msg is NULL");
-  return dora::aql_pipeline_bench(device, bytes, n, mode, queues, depth, us_per_msg);
 }
 
 int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out) {

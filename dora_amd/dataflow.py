@@ -170,6 +170,16 @@ def node_config_yaml(nodes: List[NodeSpec], node_id: str, dataflow_id: str, shm:
     return yaml.safe_dump(node_config(nodes, node_id, dataflow_id, shm), sort_keys=False)
 
 
+def _load_descriptor(desc) -> dict:
+    """The descriptor as a plain dict (a path is read as YAML), JSON-safe."""
+    import json
+    if isinstance(desc, str):
+        import yaml
+        with open(desc) as f:
+            desc = yaml.safe_load(f)
+    return json.loads(json.dumps(desc, default=str))
+
+
 def parse_descriptor(desc) -> List[NodeSpec]:
     base = os.getcwd()
     if isinstance(desc, str):
@@ -308,6 +318,7 @@ class Dataflow:
         under this daemon; `machines` maps machine names to the (host, port) their daemons
         listen on (port 0 for this machine: any free port, see `listen_port`)."""
         self.all_nodes = parse_descriptor(descriptor)
+        self.descriptor = _load_descriptor(descriptor)
         self.machine, self.machines, self.dataflow_id = machine, machines, dataflow_id
         self.nodes = [n for n in self.all_nodes if machine is None or n.machine == machine]
         self.listen_port: Optional[int] = None
@@ -351,6 +362,11 @@ class Dataflow:
         return open(p).read() if os.path.exists(p) else ""
 
     def start(self, timeout: float = 30.0):
+        # the parsed descriptor, for Node.dataflow_descriptor (apis/python/node/src/lib.rs:186)
+        import json
+        from .node import descriptor_path
+        with open(descriptor_path(self.shm), "w") as f:
+            json.dump(self.descriptor, f)
         fd, self._spec_file = tempfile.mkstemp(prefix="dora-gpu-spec-", suffix=".txt")
         with os.fdopen(fd, "w") as f:
             f.write(daemon_spec(self.all_nodes, self.machine, self.machines, self.dataflow_id))
@@ -393,6 +409,9 @@ class Dataflow:
         shm_path = "/dev/shm" + self.shm
         if os.path.exists(shm_path):
             os.unlink(shm_path)
+        from .node import descriptor_path
+        if os.path.exists(descriptor_path(self.shm)):
+            os.unlink(descriptor_path(self.shm))
 
     def __enter__(self):
         return self.start()

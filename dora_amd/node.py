@@ -102,6 +102,12 @@ def decode_parameters(raw: bytes) -> dict:
     return out
 
 
+def descriptor_path(region: str) -> str:
+    """Where a dataflow's launcher leaves its parsed descriptor (JSON) for its nodes: beside its
+    control region in /dev/shm, removed with it."""
+    return "/dev/shm/" + region.lstrip("/") + ".descriptor.json"
+
+
 def _is_pyarrow_array(data) -> bool:
     pa = sys.modules.get("pyarrow")  # an Array exists only once pyarrow is imported
     return pa is not None and isinstance(data, pa.Array)
@@ -140,6 +146,12 @@ class _Event(dict):
 
 
 class Node:
+    """The reference's `Node` pyclass (apis/python/node/src/lib.rs:29-209): `Node(node_id=None)`,
+    `next(timeout=None)`, iteration (`__iter__` / `__next__`), `send_output(output_id, data,
+    metadata=None)`, `dataflow_descriptor()`, `dataflow_id()`, `merge_external_events(...)`.
+    Added here: `dataflow` / `device` to join a dataflow by its region name on a given GPU (the
+    reference finds a dynamic node's daemon by node id), and the device-side calls below."""
+
     def __init__(self, node_id: Optional[str] = None, dataflow: Optional[str] = None,
                  device: Optional[int] = None):
         self._lib = load()
@@ -151,8 +163,9 @@ class Node:
             dev = device if device is not None else int(os.environ.get("DORA_GPU_DEVICE", "0"))
             call("dora_node_init", shm.encode(), node_id.encode(), dev, byref(h))
         self.handle = h.value
-        self.id = node_id or os.environ.get("DORA_NODE_ID")
+        self.id = self._lib.dora_node_id(self.handle).decode()
         self.device = device if device is not None else int(os.environ.get("DORA_GPU_DEVICE", "0"))
+        self._region = dataflow or os.environ.get("DORA_GPU_DATAFLOW", "")
 
     # -------------------------------------------------------------------------------- sending
     def send_output(self, output_id: str, data, metadata: Optional[dict] = None, *,
@@ -288,11 +301,54 @@ class Node:
         return r
 
     def __iter__(self):
-        while True:
-            ev = self.next()
-            if ev is None:
-                return
-            yield ev
+        return self
+
+    def __next__(self):
+        """`next(node)`: the next event (blocking); StopIteration once the stream has ended, as
+        the reference's `__next__` returning None (lib.rs:118-120)."""
+        ev = self.next()
+        if ev is None:
+            raise StopIteration
+        return ev
+
+    # ------------------------------------------------------------------------------ dataflow
+    def dataflow_id(self) -> str:
+        """The dataflow's id (lib.rs:196-202: DataflowId, a uuid): the one in the node's
+        DORA_NODE_CONFIG, else the daemon's dataflow name as the inter-daemon wire maps it."""
+        from .dataflow import dataflow_uuid
+        cfg = self._node_config()
+        if cfg and cfg.get("dataflow_id"):
+            return str(cfg["dataflow_id"])
+        return dataflow_uuid(self._lib.dora_node_dataflow_id(self.handle).decode())
+
+    def dataflow_descriptor(self) -> dict:
+        """The dataflow's descriptor as parsed from its YAML (lib.rs:186-194), written next to the
+        dataflow's control region by its launcher (dora_amd.dataflow.Dataflow); else the
+        descriptor of the node's DORA_NODE_CONFIG."""
+        import json
+        p = descriptor_path(self._region) if self._region else None
+        if p and os.path.exists(p):
+            with open(p) as f:
+                return json.load(f)
+        cfg = self._node_config()
+        if cfg and "dataflow_descriptor" in cfg:
+            return cfg["dataflow_descriptor"]
+        raise RuntimeError(f"no descriptor for dataflow region `{self._region}`")
+
+    def merge_external_events(self, subscription):
+        """Merging an external event stream (lib.rs:204-209) exists in the reference only for
+        ROS2 subscriptions (dora_ros2_bridge_python), which is outside this data plane: refused."""
+        raise NotImplementedError(
+            "merge_external_events takes a dora.Ros2Subscription; the ROS2 bridge is not part of "
+            "the device data plane")
+
+    def _node_config(self) -> Optional[dict]:
+        raw = os.environ.get("DORA_NODE_CONFIG")
+        if not raw:
+            return None
+        import yaml
+        cfg = yaml.safe_load(raw)
+        return cfg if isinstance(cfg, dict) and cfg.get("node_id") == self.id else None
 
     # -------------------------------------------------------------------------------- stats
     @property

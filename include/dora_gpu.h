@@ -245,6 +245,11 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
 int dora_node_init_from_env(dora_node** out);
 /* Drop for DoraNode (mod.rs:384-431): close outputs, wait <= 10 s for drop tokens, done. */
 void dora_node_free(dora_node* node);
+/* DoraNode::dataflow_id / id (mod.rs:373-382): the dataflow's id as its daemon names it (the
+ * reference's DataflowId is a uuid; a name that is not one maps to the UUID the inter-daemon
+ * wire carries, dora_amd/dataflow.py dataflow_uuid) and this node's id.  Owned by the node. */
+const char* dora_node_dataflow_id(const dora_node* node);
+const char* dora_node_id(const dora_node* node);
 /* The node's HIP stream; consumers must run their kernels on it so the drop token is only
  * returned after they have read the sample.  Sends spread their fills over the node's fill
  * streams (three): a fill runs after the work queued on this stream

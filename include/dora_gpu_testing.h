@@ -1,7 +1,9 @@
 /*
  * dora_gpu_testing.h — test and microbenchmark hooks of the device data plane, exported by
  * libdora_gpu_testing.so (dora_amd/csrc/testing/testing.cpp), which is built apart from the
- * shipped libdora_gpu.so and links against it.  No reference counterpart: tests/ and scripts/
+ * shipped libdora_gpu.so and links against it.  The pack-tuning knobs of r01-r05 (variants,
+ * grids, in-flight caps, queue counts) are gone with their variants (r06): the product carries no
+ * code path only a microbenchmark selects.  No reference counterpart: tests/ and scripts/
  * use these to reach internals (the AQL backlog, the BAR, the fill-flag protocol, the RCCL group
  * path, the inter-daemon codec) that the product ABI (dora_gpu.h) does not expose.
  */
@@ -13,24 +15,6 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-
-/* Tuning knob of the pack kernel (process-wide): 16-B loads in flight per lane (0 = default,
- * 2, 4, 8), non-temporal loads/stores (-1 = default, 0, 1; 2 = the signalling kernels'
- * write-through stores without a signal, a microbenchmark variant), bytes per workgroup (0 =
- * auto, else a multiple of 128: chunks start on cache lines). */
-int dora_gpu_test_pack_tune(int unroll, int nontemporal, uint32_t chunk_bytes);
-/* Tuning of packs that signal their fill from the kernel (node sends): workgroups of such a
- * launch, which then strides over the chunks (0: up to 4096).  With `bench_signal`,
- * dora_gpu_pack signals a scratch flag too (microbenchmarks). */
-int dora_gpu_test_pack_signal_tune(uint32_t grid, int bench_signal);
-/* Workgroup cap of packs the command processor signals (0: the default, 3584; a pack has at most
- * one workgroup per chunk). */
-int dora_gpu_test_cp_grid(uint32_t grid);
-/* Workgroup cap of multi-segment packs the command processor signals (0: the default, 640). */
-int dora_gpu_test_cp_grid_multi(uint32_t grid);
-/* Samples a sender of this process may have in flight below / from 8 MiB before an allocation
- * waits for a returned token (0: DORA_GPU_MAX_IN_FLIGHT or the defaults 11 / 8). */
-int dora_gpu_test_in_flight(long small, long big);
 
 /* Test tool (no reference counterpart): one workgroup per CU reads all of [data, data + len)
  * with plain cached loads, leaving the lines in every XCD's L2 (the acquire-fence negative
@@ -44,26 +28,14 @@ int dora_gpu_test_bar_alloc(int device, size_t bytes, void** out);
  * the backlog; clearing it dispatches the backlog as batch packs.  Only for asynchronous sends
  * (DORA_SEND_ASYNC): a synchronous send waits for its own pack. */
 int dora_gpu_test_aql_hold(int device, int hold);
-/* Test tool: 1 (default) lets the command processor signal a lone single-segment pack above
- * 32 MiB (a synchronous send's); 0 makes it signal its fill in-kernel. */
-int dora_gpu_test_cp_lone(int on);
-/* Test tool (latency probe): a host thread that every `period_us` either publishes an empty
- * barrier-AND packet on this process's first AQL queue of `device` (mode 1), reads (2) or writes
- * (3) one word of host-visible device memory over PCIe; until dora_gpu_test_heartbeat_stop or
- * `seconds` (at most 600). */
-int dora_gpu_test_heartbeat_start(int device, int mode, double period_us, double seconds,
-                                  void** out);
-int dora_gpu_test_heartbeat_stop(void* h);
+/* Test hooks of the region-end stamp reduction (aql_stamp_reduce): how long it is waited for
+ * (ns; 0 = the default 5 s) — a tiny value makes the wait time out while the packet still runs —
+ * and the AQL argument slots left to reductions that timed out (never written again). */
+int dora_gpu_test_reduce_timeout(uint64_t ns);
+int dora_gpu_test_abandoned_slots(int device, uint32_t* slots);
 /* Test tool: empty packets the keep-awake thread of `device` has published in this process
  * (dora_gpu_set_keep_awake), and whether it is parked (no send for 100 ms). */
 int dora_gpu_test_keep_awake_stats(int device, uint64_t* heartbeats, int* parked);
-/* Test tool (latency probe): one resident wave on `device` that sleeps until
- * dora_gpu_test_keep_warm_stop (or `seconds`, at most 600) so the GPU never idles. */
-int dora_gpu_test_keep_warm_start(int device, double seconds, void** out);
-int dora_gpu_test_keep_warm_stop(void* handle);
-/* Test tool: the AQL queues this process creates (effective before its first AQL use; 0 keeps
- * 4, at most 8) and how many of them take packs of 8-32 MiB in turn (0 keeps 4). */
-int dora_gpu_test_mid_queues(int create, int use);
 /* Test tool: `wc` 1 if `device`'s AQL packet rings are published with store fences (the runtime
  * put them in this GPU's memory), 0 otherwise; `where` (may be NULL): the runtime's pointer type
  * of the ring * 4 + its owner (0 none, 1 the CPU agent, 2 this GPU, 3 another agent). */
@@ -82,14 +54,6 @@ int dora_gpu_test_bar_write(int device, void* dst, const void* src, size_t bytes
  * processor signals. */
 int dora_gpu_test_fill_reached(const void* flag, uint64_t epoch);
 int dora_gpu_test_cp_arm(void* flag, uint64_t epoch);
-/* Test hook (microbenchmark): `n` single-segment AQL packs of `bytes` from rotating HBM sources,
- * round robin over `queues` of the device's AQL queues with at most `depth` outstanding per
- * queue; mode 0 completes them with the in-kernel fill signal, 1 with the packet's completion
- * signal (release fence none), 2 the same with an agent release fence, 3 and 4 as 0 and 1 without
- * the acquire fence, 5 as 1 with every wave waiting for its stores.  *us_per_msg = host time
- * per pack. */
-int dora_gpu_test_aql_pipeline(int device, size_t bytes, int n, int mode, int queues, int depth,
-                               double* us_per_msg);
 void dora_gpu_test_bar_free(void* ptr);
 /* Test hook (RCCL path of the fan-out): form a broadcast group of one rank on
  * `device` (unique id -> join(nranks 1) -> ncclBroadcast of `bytes` at `buf` in place on a fresh

@@ -68,6 +68,18 @@ def test_test_hooks_live_in_their_own_library(lib):
     assert "dora_gpu_test_" not in exported
 
 
+def test_product_library_has_no_tuning_entry_point(lib):
+    """Verdict r05 item 6: the pack-tuning knobs (kernel variants, grid caps, in-flight caps,
+    queue counts, the CP-signal switch) and their microbenchmark hooks are gone from the shipped
+    library — no exported symbol, C or C++, sets one."""
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--defined-only", "-C", _lib.LIB_PATH], capture_output=True,
+                          text=True, check=True).stdout
+    for word in ("pack_tune", "pack_signal_tune", "cp_grid", "set_in_flight_caps", "cp_lone",
+                 "mid_queues", "pipeline_bench", "keep_warm", "pack_variant", "aql_heartbeat("):
+        assert word not in syms, word
+
+
 def test_version_and_errors(lib):
     assert lib.dora_gpu_version().startswith(b"dora-gpu")
     h = ctypes.c_void_p()
