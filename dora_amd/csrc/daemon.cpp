@@ -163,11 +163,17 @@ class Daemon {
   // Returns 0 when every node is done, DORA_ERR_TIMEOUT after timeout_ms (<0: no timeout).
   int run(int64_t timeout_ms) {
     const uint64_t t0 = mono_ns();
-    uint64_t idle_since = mono_ns();
-    uint64_t idle_from = 0;
-    uint64_t last_liveness = 0;
-    AdaptiveSpin spin;  // spins through short idle gaps instead of sleeping (shm.h)
-    std::vector<uint8_t> payload;
+    // The idle bookkeeping and the spin estimate persist across calls: the daemon binary calls
+    // run() in 200 ms slices, and a fresh estimate (mean 0: the 200 us base budget) each slice
+    // put the daemon to sleep before the next message of a 1 ms stream every 200 ms — ~1 % of
+    // them then paid a futex wake, 11-13 us (the host 8 B p99, profiles/r06_inline_tail_*.json)
+    uint64_t& idle_since = idle_since_;
+    uint64_t& idle_from = idle_from_;
+    uint64_t& last_liveness = last_liveness_;
+    AdaptiveSpin& spin = spin_;  // spins through short idle gaps instead of sleeping (shm.h)
+    uint64_t& last_spin = last_spin_;  // the previous spinning pass (0: not spinning)
+    if (!idle_since) idle_since = t0;
+    std::vector<uint8_t>& payload = payload_;
     RegionHdr* h = region_->hdr();
     bool placed = false;
     for (;;) {
@@ -183,6 +189,7 @@ class Daemon {
         uint32_t kind;
         int budget = 64;
         while (budget-- > 0 && req_[i].try_pop(&kind, &payload)) {
+          if (kind == REQ_SEND_MESSAGE) msg_spin_.arrived(mono_ns());
           handle(static_cast<int>(i), kind, payload);
           work = true;
         }
@@ -198,8 +205,13 @@ class Daemon {
         work |= !released_.empty();
       }
       const uint64_t now = mono_ns();
+      // idle time is accounted up to a slice's end once (idle_counted_), while the gap the spin
+      // estimate observes runs on from idle_from across slices
       auto leave = [&](int rc) {
-        if (idle_from && !work) add_idle_ns(now - idle_from);
+        if (idle_from && !work) {
+          add_idle_ns(now - std::max(idle_from, idle_counted_));
+          idle_counted_ = now;
+        }
         return rc;
       };
       if (all_done()) return leave(DORA_OK);
@@ -210,9 +222,11 @@ class Daemon {
         check_liveness();
         last_liveness = now;
       }
+      woke_ = false;  // only the pass right after a sleep routes "woken"
       if (work) {
+        last_spin = 0;
         if (idle_from) {  // the spin/sleep that preceded this work
-          add_idle_ns(now - idle_from);
+          add_idle_ns(now - std::max(idle_from, idle_counted_));
           spin.observe(now - idle_from);
         }
         idle_from = 0;
@@ -220,16 +234,24 @@ class Daemon {
         continue;
       }
       if (!idle_from) idle_from = now;
-      if (int64_t(now - idle_since) / 1000 < spin.budget_us()) {
+      // Time this thread spent off the CPU (descheduled) is not spinning: the window moves by
+      // it, so being preempted does not put the daemon to sleep before the next message
+      if (last_spin && now - last_spin > kOffCpuNs) idle_since += now - last_spin;
+      last_spin = now;
+      if (int64_t(now - idle_since) / 1000 < std::max(spin.budget_us(), msg_spin_.budget_us())) {
         __builtin_ia32_pause();
         continue;
       }
+      last_spin = 0;
       h->daemon_sleeping.store(1, std::memory_order_seq_cst);
       std::atomic_thread_fence(std::memory_order_seq_cst);  // pairs with ring_doorbell's fence
       const uint32_t bell = h->doorbell.load(std::memory_order_seq_cst);
       bool empty = true;
       for (auto& r : req_) empty &= r.empty();
-      if (empty) futex_wait(&h->doorbell, bell, 20000);
+      if (empty) {
+        futex_wait(&h->doorbell, bell, 20000);
+        woke_ = true;
+      }
       h->daemon_sleeping.store(0, std::memory_order_seq_cst);
       idle_since = mono_ns();
     }
@@ -489,8 +511,12 @@ class Daemon {
         ev_buf_.raw(tail, tail_len);
         push_event_raw(rc.node, EV_INPUT, ev_buf_.data(), ev_buf_.size());
         if (ti) {
-          trace(TP_ROUTED, data.token());
+          trace(woke_ ? TP_ROUTED_WOKE : TP_ROUTED, data.token());
           ti->add(rc.node);
+        } else if (trace_enabled() && tail_len >= 18) {
+          uint64_t ts;  // an inline sample: keyed by its metadata timestamp (u64 len, u16, u64)
+          std::memcpy(&ts, tail + 10, 8);
+          trace(woke_ ? TP_ROUTED_WOKE : TP_ROUTED, ts_key(ts));
         }
       }
     }
@@ -634,6 +660,12 @@ class Daemon {
   std::map<std::string, PeerAddr> peers_;
   std::vector<ProxySpec> proxies_;
   std::string dataflow_id_ = "local", listen_host_ = "127.0.0.1";
+  bool woke_ = false;  // this loop pass follows a futex sleep (message trace)
+  // run()'s loop state, kept between calls
+  uint64_t idle_since_ = 0, idle_from_ = 0, last_liveness_ = 0, last_spin_ = 0, idle_counted_ = 0;
+  AdaptiveSpin spin_;
+  MessageSpin msg_spin_;  // data messages' spacing alone (shm.h)
+  std::vector<uint8_t> payload_;
   int listen_port_ = -1;
   std::unique_ptr<Forwarder> fwd_;
   std::unique_ptr<Gateway> gw_;

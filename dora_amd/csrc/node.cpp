@@ -558,7 +558,8 @@ struct NodeCore {
     return reinterpret_cast<uint64_t*>(region_dev + (host - region->base()));
   }
 
-  void ring_doorbell() {
+  // True when the daemon was asleep and had to be woken (the message trace notes it).
+  bool ring_doorbell() {
     // the daemon sets `daemon_sleeping` before it reads the doorbell and re-checks the rings;
     // the fence orders the request's head store before our load of the flag (shm.cpp's ring
     // wake-up argument), so the doorbell is only bumped for a sleeping daemon
@@ -567,8 +568,11 @@ struct NodeCore {
     if (h->daemon_sleeping.load(std::memory_order_relaxed)) {
       h->doorbell.fetch_add(1, std::memory_order_seq_cst);
       futex_wake(&h->doorbell);
+      return true;
     }
+    return false;
   }
+  bool last_rang = false;  // the last request woke the daemon (trace only)
 
   int request(uint32_t kind, const std::vector<uint8_t>& payload) {
     return request(kind, payload.data(), payload.size());
@@ -581,7 +585,7 @@ struct NodeCore {
       if (!req.push(kind, payload, len, 30000000))
         return fail(DORA_ERR_TIMEOUT, "daemon did not drain the request ring for 30 s");
     }
-    ring_doorbell();
+    last_rang = ring_doorbell();
     return DORA_OK;
   }
 
@@ -1285,6 +1289,9 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
       DataMsg d = r.data();
       auto in = std::make_shared<InputData>();
       in->core = n->core;
+      const bool woke = ring_take_woke();
+      if (d.kind != DATA_DEVICE_IPC && trace_enabled())
+        trace(woke ? TP_POPPED_WOKE : TP_POPPED, ts_key(ev->meta.timestamp_ns));
       if (d.kind == DATA_VEC) {
         in->vec = std::move(d.vec);
         in->ptr = in->vec.data();
@@ -1308,7 +1315,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
       } else if (d.kind == DATA_DEVICE_IPC) {
         in->has_token = true;  // set first: a mapping failure still returns the token
         in->token = d.ipc.token;
-        trace(TP_POPPED, in->token);
+        trace(woke ? TP_POPPED_WOKE : TP_POPPED, in->token);
         in->len = d.ipc.len;
         in->ext_len = std::max(d.ipc.ext_len, d.ipc.len);
         void* base = nullptr;
@@ -1856,7 +1863,9 @@ int send_sample(dora_node* n, const char* output_id, const std::vector<uint8_t>&
   } else if (slot) {
     n->sent_out[d.ipc.token] = slot;
     if (token_out) *token_out = d.ipc.token;
-    trace(TP_SENT, d.ipc.token);
+    trace(n->core->last_rang ? TP_SENT_RANG : TP_SENT, d.ipc.token);
+  } else if (trace_enabled()) {
+    trace(n->core->last_rang ? TP_SENT_RANG : TP_SENT, ts_key(ts));  // an inline sample
   }
   return DORA_OK;
 }

@@ -1,6 +1,7 @@
 // Shared-memory region + SPSC rings + futex waits (see shm.h).
 #include "common.h"
 #include "shm.h"
+#include "trace.h"
 
 #include <cstddef>
 
@@ -13,6 +14,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -200,6 +202,22 @@ void AdaptiveSpin::observe(uint64_t idle_ns) {
   const uint64_t lim = uint64_t(std::max<int64_t>(spin_max_us(), 0)) * 4000;
   if (idle_ns > lim) idle_ns = lim;
   mean_ns_ = idle_ns <= mean_ns_ || !mean_ns_ ? idle_ns : mean_ns_ + (idle_ns - mean_ns_) / 4;
+}
+
+void MessageSpin::arrived(uint64_t now_ns) {
+  if (last_ns_) {
+    // gaps beyond 4 x the cap count as the cap's 4 x (a pause ends a stream's estimate quickly
+    // without one outlier dominating it); 1/8 weight per message
+    const uint64_t lim = uint64_t(spin_max_us()) * 4000;
+    const uint64_t g = std::min<uint64_t>(now_ns - last_ns_, lim);
+    mean_ns_ = mean_ns_ ? mean_ns_ - mean_ns_ / 8 + g / 8 : g;
+  }
+  last_ns_ = now_ns;
+}
+
+int64_t MessageSpin::budget_us() const {
+  const int64_t want = int64_t(2 * mean_ns_ / 1000);
+  return mean_ns_ && want <= spin_max_us() ? want : 0;
 }
 
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us) {
@@ -453,8 +471,19 @@ bool RingReader::try_pop(uint32_t* kind, std::vector<uint8_t>* payload) {
   }
 }
 
+namespace {
+thread_local bool tl_wait_slept = false;  // the thread's last wait slept in the futex
+}  // namespace
+
+bool ring_take_woke() {
+  const bool v = tl_wait_slept;
+  tl_wait_slept = false;
+  return v;
+}
+
 bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_flag) {
   const uint64_t t0 = mono_ns();
+  tl_wait_slept = false;
   // One idle gap may span several calls that time out (a sender polling for drop tokens every
   // 1 ms): the gap — for the spin budget and the adaptive mean — runs from the first of them,
   // unless the caller did other work for a while in between.
@@ -484,21 +513,32 @@ bool RingReader::wait(int64_t timeout_us, const std::atomic<uint32_t>* abort_fla
       }
     }
   } idle{this, t0, was_empty};
+  uint64_t spin_from = gap0, prev = t0;
+  bool sleeping = false;  // past the spin: futex slices until a record comes
   while (empty()) {
     const uint64_t now = mono_ns();
     const int64_t el = int64_t(now - t0) / 1000;
     if (timeout_us >= 0 && el >= timeout_us) return false;
     if (abort_flag && abort_flag->load(std::memory_order_relaxed)) return false;
-    if (int64_t(now - gap0) / 1000 < spin) {
-      __builtin_ia32_pause();
-      continue;
+    if (!sleeping) {
+      // time off the CPU is not spinning: the window moves by it (as the daemon's, daemon.cpp)
+      if (now - prev > kOffCpuNs) spin_from += now - prev;
+      prev = now;
+      if (int64_t(now - spin_from) / 1000 < spin) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      sleeping = true;
     }
     h_->waiters.fetch_add(1, std::memory_order_seq_cst);
     const uint32_t s = h_->seq.load(std::memory_order_seq_cst);
     if (empty()) {
       int64_t slice = 20000;  // re-check abort flags periodically
       if (timeout_us >= 0) slice = std::min<int64_t>(slice, timeout_us - el);
-      if (slice > 0) futex_wait(&h_->seq, s, slice);
+      if (slice > 0) {
+        tl_wait_slept = true;
+        futex_wait(&h_->seq, s, slice);
+      }
     }
     h_->waiters.fetch_sub(1, std::memory_order_seq_cst);
   }

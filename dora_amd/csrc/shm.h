@@ -192,6 +192,20 @@ class AdaptiveSpin {
   uint64_t mean_ns_ = 0;
 };
 
+// The daemon's estimate of the spacing of data messages alone (REQ_SEND_MESSAGE arrivals): a
+// plain moving average, so the drop-token report that follows each device message a few
+// microseconds later — a short gap of the daemon's other traffic, which AdaptiveSpin follows
+// down at once — does not put the daemon to sleep before the next message of a 1 ms stream
+// (each such message paid a ~2 us futex wake, 11-13 us from an idle core).
+class MessageSpin {
+ public:
+  void arrived(uint64_t now_ns);
+  int64_t budget_us() const;  // 0 when messages are too far apart to spin through
+
+ private:
+  uint64_t last_ns_ = 0, mean_ns_ = 0;
+};
+
 class RingReader {
  public:
   RingReader() = default;
@@ -220,6 +234,10 @@ void shmem_unmap(void* p, size_t len);
 void shmem_unlink(const std::string& name);
 // The first `len` bytes of region `name` (the inter-daemon forwarder's copy).
 bool read_shmem(const std::string& name, uint64_t len, std::vector<uint8_t>* out);
+
+// A spinning thread that saw the clock jump by more than this between two passes was off the
+// CPU meanwhile: that time does not count against its spin budget (shm.cpp, daemon.cpp).
+constexpr uint64_t kOffCpuNs = 50000;
 
 // futex helpers on shared (non-private) words
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected, int64_t timeout_us);

@@ -261,7 +261,8 @@ int main() {
                "\"free_us\": %.3f, \"busy_us_per_input\": %.3f, "
                "\"fill_wait_us_per_input\": %.3f, \"pulls\": %llu, \"pull_bytes\": %llu, "
                "\"bcast_groups\": %llu, "
-               "\"bcast_received\": %llu, \"bcast_error\": \"%s\", \"series\": [",
+               "\"bcast_received\": %llu, \"bcast_error\": \"%s\", \"sched\": %s, "
+               "\"series\": [",
                errors, (unsigned long long)dropped,
                n_inputs ? double(t_next) / n_inputs / 1000.0 : 0.0,
                n_inputs ? double(t_free) / n_inputs / 1000.0 : 0.0,
@@ -270,7 +271,8 @@ int main() {
                             : 0.0,
                n_inputs > 1 ? double(fill_last - fill_first) / 1e3 / double(n_inputs - 1) : 0.0,
                (unsigned long long)pulls, (unsigned long long)pull_bytes,
-               (unsigned long long)bgroups, (unsigned long long)brecv, json_safe(berr).c_str());
+               (unsigned long long)bgroups, (unsigned long long)brecv, json_safe(berr).c_str(),
+               sched_json().c_str());
   bool first = true;
   for (auto& kv : stats) kv.second.close_burst();
   for (auto& kv : stats) {

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "dora_gpu.h"
+#include "params.h"
 
 static volatile sig_atomic_t g_stop = 0;
 static uint64_t mono_ns_main() {
@@ -75,10 +76,10 @@ int main(int argc, char** argv) {
   dora_daemon_remote_stats(d, &fwd, &staged, &received);
   std::printf("{\"daemon\": \"done\", \"rc\": %d, \"routed\": %llu, \"pending_tokens\": %llu, "
               "\"busy_us\": %.1f, \"busy_us_per_routed\": %.3f, \"forwarded\": %llu, "
-              "\"staged_bytes\": %llu, \"remote_received\": %llu}\n",
+              "\"staged_bytes\": %llu, \"remote_received\": %llu, \"sched\": %s}\n",
               rc, (unsigned long long)routed, (unsigned long long)pending, busy_us,
               routed ? busy_us / double(routed) : 0.0, (unsigned long long)fwd,
-              (unsigned long long)staged, (unsigned long long)received);
+              (unsigned long long)staged, (unsigned long long)received, sched_json().c_str());
   dora_daemon_free(d);
   return rc == 0 ? 0 : 1;
 }

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -85,3 +87,31 @@ inline std::string json_safe(const char* s) {
   for (; s && *s; ++s) o += (*s == '"' || *s == '\\' || static_cast<unsigned char>(*s) < 0x20) ? ' ' : *s;
   return o;
 }
+
+// The calling process's main thread as the scheduler saw it (/proc/self/schedstat: time on the
+// CPU, time runnable but waiting for one; /proc/self/status: context switches), as a JSON object.
+// A spinning receiver that waited on the run queue or was switched out involuntarily lost the CPU
+// to other load: the tail of its latencies is that, not its own work.
+inline std::string sched_json() {
+  unsigned long long run = 0, wait = 0, slices = 0, vol = 0, invol = 0;
+  if (FILE* f = std::fopen("/proc/self/schedstat", "r")) {
+    if (std::fscanf(f, "%llu %llu %llu", &run, &wait, &slices) != 3) run = wait = slices = 0;
+    std::fclose(f);
+  }
+  if (FILE* f = std::fopen("/proc/self/status", "r")) {
+    char line[256];
+    while (std::fgets(line, sizeof(line), f)) {
+      if (std::strncmp(line, "voluntary_ctxt_switches:", 24) == 0) vol = std::strtoull(line + 24, nullptr, 10);
+      if (std::strncmp(line, "nonvoluntary_ctxt_switches:", 27) == 0)
+        invol = std::strtoull(line + 27, nullptr, 10);
+    }
+    std::fclose(f);
+  }
+  char b[256];
+  std::snprintf(b, sizeof(b),
+                "{\"run_ms\": %.3f, \"runq_wait_ms\": %.3f, \"timeslices\": %llu, "
+                "\"voluntary_switches\": %llu, \"involuntary_switches\": %llu}",
+                run / 1e6, wait / 1e6, slices, vol, invol);
+  return b;
+}
+

@@ -1,5 +1,6 @@
 #include "trace.h"
 
+#include <sched.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -20,6 +21,7 @@ struct Rec {
   uint64_t t;
   DropToken tok;
   uint8_t p;
+  int16_t cpu;  // the CPU the stamp was taken on (whose interrupts / sibling load it saw)
 };
 
 // DORA_GPU_TRACE=<dir>: per-message trace files in <dir> (and the sub-phase profile below);
@@ -49,12 +51,12 @@ struct Tracer {
                              ".trace.csv";
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) return;
-    std::fprintf(f, "who,point,token,t_ns\n");
+    std::fprintf(f, "who,point,token,t_ns,cpu\n");
     const size_t m = std::min(n.load(), buf.size());
     for (size_t i = 0; i < m; ++i) {
       std::fprintf(f, "%s,%u,", who.c_str(), unsigned(buf[i].p));
       for (int k = 0; k < 16; ++k) std::fprintf(f, "%02x", buf[i].tok.b[k]);
-      std::fprintf(f, ",%llu\n", (unsigned long long)buf[i].t);
+      std::fprintf(f, ",%llu,%d\n", (unsigned long long)buf[i].t, int(buf[i].cpu));
     }
     std::fclose(f);
   }
@@ -73,17 +75,24 @@ void trace(TracePoint p, const DropToken& t) {
   Tracer& tr = tracer();
   if (!tr.dir) return;
   const size_t i = tr.n.fetch_add(1, std::memory_order_relaxed);
-  if (i < tr.buf.size()) tr.buf[i] = {now_ns(), t, p};
+  if (i < tr.buf.size()) tr.buf[i] = {now_ns(), t, p, int16_t(sched_getcpu())};
 }
 
 void trace_at(TracePoint p, const DropToken& t, uint64_t t_ns) {
   Tracer& tr = tracer();
   if (!tr.dir) return;
   const size_t i = tr.n.fetch_add(1, std::memory_order_relaxed);
-  if (i < tr.buf.size()) tr.buf[i] = {t_ns, t, p};
+  if (i < tr.buf.size()) tr.buf[i] = {t_ns, t, p, int16_t(sched_getcpu())};
 }
 
 void trace_set_name(const std::string& who) { tracer().who = who; }
+
+DropToken ts_key(uint64_t ts) {
+  DropToken k;
+  std::memcpy(k.b, &ts, 8);
+  std::memset(k.b + 8, 0xff, 8);
+  return k;
+}
 
 void trace_flush() { tracer().flush(); }
 

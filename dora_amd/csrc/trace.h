@@ -25,7 +25,17 @@ enum TracePoint : uint8_t {
   TP_RELEASED,         // receiver: drop token reported
   TP_GPU_START,        // receiver: the pack's first workgroup started (host clock via HSA)
   TP_GPU_SIGNAL,       // receiver: the pack signalled its fill (host clock via HSA)
+  // r06: the control plane's wake-ups, per message (inline samples too, keyed by ts_key)
+  TP_SENT_RANG,        // sender: as TP_SENT, after waking a sleeping daemon (futex)
+  TP_ROUTED_WOKE,      // daemon: as TP_ROUTED, in the loop pass that followed a futex sleep
+  TP_POPPED_WOKE,      // receiver: as TP_POPPED, its wait for the event slept in the futex
 };
+
+// The trace key of a message without a drop token (an inline Vec sample): its metadata
+// timestamp, which the sender, the daemon and the receiver all see.
+DropToken ts_key(uint64_t ts);
+// Whether the calling thread's last RingReader::wait slept in the futex (cleared by the call).
+bool ring_take_woke();
 
 bool trace_enabled();
 void trace(TracePoint p, const DropToken& t);
