@@ -730,12 +730,13 @@ def main():
     host_result_path = os.path.join(os.path.dirname(result_path), "hostsink.json")
     desc = {"nodes": [
         {"id": "node", "path": "dynamic",
-         "outputs": ["latency", "latency_host", "throughput", "to_host"],
+         "outputs": ["latency", "latency_host", "throughput", "to_host", "to_host_warm"],
          "inputs": {"ack": "sink/ack", "ack_host": "hostsink/ack"},
          "_unstable_deploy": {"gpu": local_rank}},
         # a receiver without a GPU: device samples reach it staged in host memory
         {"id": "hostsink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
-         "inputs": {"to_host": {"source": "node/to_host", "queue_size": 10}},
+         "inputs": {"to_host": {"source": "node/to_host", "queue_size": 10},
+                    "to_host_warm": {"source": "node/to_host_warm", "queue_size": 10}},
          "env": {"DORA_BENCH_RESULT": host_result_path}, "_unstable_deploy": {"gpu": -1}},
         {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
          "inputs": {"latency": {"source": "node/latency", "queue_size": 10},
@@ -915,7 +916,11 @@ def main():
                 device.fill_splitmix(b.ptr, size, payload_seed(size), stream)
                 stream.sync()
             c = to_i64(device.csum64(b.ptr, size, stream))
-            for k in range(2 + host_lat_n(size, args.lat_n)):
+            for k in range(2):  # untimed: the receiver's first staging buffer of this size
+                node.send_output_device_bytes("to_host_warm", b.ptr, size, {"seq": seq})
+                seq += 1
+                time.sleep(args.lat_gap_us / 1e6)
+            for k in range(host_lat_n(size, args.lat_n)):
                 meta = {"seq": seq, "t_start": time.time_ns()}
                 if k < 3:
                     meta.update({"csum": c, "verify": True})

@@ -139,6 +139,44 @@ def test_device_producer_to_host_only_python_receiver(launcher):
     s.close()
 
 
+def test_host_only_receiver_staging_stress(launcher):
+    """600 device messages of 8 B .. 1 MiB, each with new bytes (the source is rewritten after
+    every synchronous send), reach a receiver without a GPU byte for byte: below 1 MiB staged by
+    one AQL pack writing pinned host memory and signalling a host flag, 1 MiB by the copy
+    engines.  Checks the write-to-host ordering of the in-kernel signal under load."""
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.device import DeviceBuffer
+    from oracle.checksum_ref import splitmix_bytes
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["x"]},
+        {"id": "dst", "path": "dynamic", "inputs": {"x": {"source": "src/x", "queue_size": 10}},
+         "_unstable_deploy": {"gpu": -1}},
+    ]}
+    sizes = [8, 100, 4096, 4097, 65539, (1 << 20) - 1, 1 << 20]
+    s = device.Stream()
+    buf = DeviceBuffer(1 << 20)
+    with Dataflow(desc, launcher=launcher) as df:
+        n = _nodes(df, {"src": 0, "dst": -1})
+        tx, rx = n["src"], n["dst"]
+        for k in range(600):
+            z = sizes[k % len(sizes)]
+            device.fill_splitmix(buf.ptr, z, 0xABC000 + k, s)
+            s.sync()
+            tx.send_output_device_bytes("x", buf.ptr, z, {"k": k})
+            ev = rx.next(timeout=60)
+            assert ev["metadata"] == {"k": k} and not ev["on_device"]
+            assert ctypes.string_at(ev["data_ptr"], z) == splitmix_bytes(z, 0xABC000 + k), (k, z)
+            del ev
+        hp = rx.host_paths()
+        assert hp["staged"] >= 600, hp
+        tx.close()
+        rx.close()
+        df.wait(30)
+    buf.free()
+    s.close()
+
+
 def test_host_sources_bar_and_dma_paths_bit_exact(launcher):
     """Host bytes of 4096, 4097, 1 MiB + 3, 2 MiB, 2 MiB + 1 and 40.96 MB, and multi-buffer host
     pyarrow arrays (a 20k-point cloud on the BAR path, the 1M-point C3 cloud on the DMA path),
