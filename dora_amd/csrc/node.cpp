@@ -538,46 +538,6 @@ struct NodeCore {
     host_pool.emplace(cap, p);
   }
 
-  // A host-only receiver's small-sample staging by raw AQL dispatch on the producer's GPU
-  // (stage_to_host): the fill flag the pack signals (pinned host memory), its done words, the
-  // process's AQL queue of that GPU.  One per producer GPU, made on first use (under pool_mu).
-  struct StageCtx {
-    int device = -1;
-    AqlQueue* q = nullptr;
-    FillFlag* flag = nullptr;
-    uint64_t* flag_dev = nullptr;
-    uint32_t* done = nullptr;
-    uint64_t epoch = 0;
-  };
-  std::vector<StageCtx> stage_ctx;
-
-  StageCtx* stage_ctx_for(int src_device) {
-    std::lock_guard<std::mutex> g(pool_mu);
-    for (auto& x : stage_ctx)
-      if (x.device == src_device) return x.q ? &x : nullptr;
-    StageCtx x;
-    x.device = src_device;
-    x.q = aql_queue(src_device);
-    void* f = nullptr;
-    void* fd = nullptr;
-    const size_t done_bytes = size_t(kMaxSignalWgs) * sizeof(uint32_t);
-    if (x.q && hipHostMalloc(&f, sizeof(FillFlag), hipHostMallocMapped | hipHostMallocCoherent) ==
-                   hipSuccess &&
-        hipHostGetDevicePointer(&fd, f, 0) == hipSuccess &&
-        hipMalloc(reinterpret_cast<void**>(&x.done), done_bytes) == hipSuccess &&
-        hipMemset(x.done, 0, done_bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
-      x.flag = new (f) FillFlag();
-      x.flag_dev = static_cast<uint64_t*>(fd);
-    } else {
-      (void)hipGetLastError();
-      if (f) (void)hipHostFree(f);
-      if (x.done) (void)hipFree(x.done);
-      x = StageCtx{src_device};  // no AQL staging on this GPU: the HIP copy
-    }
-    stage_ctx.push_back(x);
-    return stage_ctx.back().q ? &stage_ctx.back() : nullptr;
-  }
-
   // A private stream of GPU `src_device` for copies waited for alone (a host-only receiver's
   // staging, a device receiver's pulls); the current device must be it
   hipStream_t stage_stream(int src_device) {
@@ -736,12 +696,6 @@ struct NodeCore {
     for (auto& kv : stage_streams) {
       (void)hipStreamSynchronize(kv.second);
       (void)hipStreamDestroy(kv.second);
-    }
-    for (auto& x : stage_ctx) {
-      if (!x.flag) continue;
-      aql_forget_flags(x.device, x.flag, sizeof(FillFlag));  // (every stage pack was waited for)
-      (void)hipHostFree(x.flag);
-      (void)hipFree(x.done);
     }
     for (auto& kv : host_pool) (void)hipHostFree(kv.second);
     if (fill_done) (void)hipFree(fill_done);
@@ -1449,15 +1403,14 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
   n->queue.push_back(std::move(ev));
 }
 
-// A device sample delivered to a node without a GPU (DORA_GPU_DEVICE < 0) is staged into pinned
-// host memory the input owns (recycled, host_pool), then the producer's token goes back at once
-// and the input is a host input like a shared-memory one (the reference's receivers always get
-// host ArrowData, event_stream/event.rs:35-91; a Python receiver a pyarrow array,
-// apis/python/operator/src/lib.rs:135-144).  Below 1 MiB the pack kernel on the producer's GPU
-// writes it, dispatched as one raw AQL packet and signalling a host flag; from 1 MiB the copy
-// engines DMA it (hipMemcpyAsync + a stream synchronise: ~12.7 us at 4 KB, 56 GB/s at 40.96 MB
-// on an MI355X box, profiles/r06_host_path_probe.jsonl d2h_pinned).
-constexpr uint64_t kAqlStageMax = 1ull << 20;
+// A device sample delivered to a node without a GPU (DORA_GPU_DEVICE < 0): one DMA by the
+// producer GPU's copy engines into pinned host memory the input owns (recycled, host_pool), then
+// the producer's token goes back at once and the input is a host input like a shared-memory one
+// (the reference's receivers always get host ArrowData, event_stream/event.rs:35-91; a Python
+// receiver a pyarrow array, apis/python/operator/src/lib.rs:135-144).  4 KB: ~12.7 us, 40.96 MB:
+// 56 GB/s on an MI355X box (profiles/r06_host_path_probe.jsonl, d2h_pinned).  The pack kernel
+// writing pinned host memory from one raw AQL packet instead was slower at every size tried,
+// 23 / 27 / 30 us against 18 / 16 / 20 at 4 KB / 64 KB / 256 KB (profiles/r06_d2h_stage_ab.jsonl).
 int stage_to_host(InputData* in, int src_device) {
   NodeCore* c = in->core.get();
   if (in->ext_len) {
@@ -1467,40 +1420,15 @@ int stage_to_host(InputData* in, int src_device) {
     if (!h)
       return fail(DORA_ERR_HIP, "pinned staging buffer of %llu bytes",
                   (unsigned long long)in->ext_len);
-    bool done = false;
-    if (in->ext_len < kAqlStageMax) {
-      // one raw AQL packet: the pack kernel on the producer's GPU writes the sample into the
-      // pinned buffer and signals the host flag (in-kernel below 1 MiB), polled here
-      if (NodeCore::StageCtx* sc = c->stage_ctx_for(src_device); sc && aql_usable(sc->q)) {
-        const FillSignal sig{sc->flag_dev, ++sc->epoch, sc->done};
-        const Segment seg{in->ptr, 0, in->ext_len};
-        if (aql_pack(sc->q, &seg, 1, static_cast<uint8_t*>(h), sig, &sc->flag->epoch, false, cap) ==
-            DORA_OK) {
-          const uint64_t t0 = mono_ns();
-          while (!fill_reached(&sc->flag->epoch, sig.epoch)) {
-            if (mono_ns() - t0 > 10000000000ull) {
-              // the pack may still write the buffer: leave it to the pack, not to the pool
-              return fail(DORA_ERR_TIMEOUT, "staging pack did not complete within 10 s");
-            }
-            __builtin_ia32_pause();
-          }
-          done = true;
-        } else {
-          clear_error();  // the HIP copy below
-        }
-      }
-    }
-    if (!done) {
-      hipStream_t st = c->stage_stream(src_device);
-      hipError_t e = st ? hipMemcpyAsync(h, in->ptr, in->ext_len, hipMemcpyDeviceToHost, st)
-                        : hipErrorInvalidResourceHandle;
-      if (e == hipSuccess) e = hipStreamSynchronize(st);
-      if (e != hipSuccess) {
-        (void)hipGetLastError();
-        c->host_pool_put(h, cap);
-        return fail(DORA_ERR_HIP, "staging a device sample to host memory: %s",
-                    hipGetErrorString(e));
-      }
+    hipStream_t st = c->stage_stream(src_device);
+    hipError_t e = st ? hipMemcpyAsync(h, in->ptr, in->ext_len, hipMemcpyDeviceToHost, st)
+                      : hipErrorInvalidResourceHandle;
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      c->host_pool_put(h, cap);
+      return fail(DORA_ERR_HIP, "staging a device sample to host memory: %s",
+                  hipGetErrorString(e));
     }
     in->host_local = h;
     in->host_local_cap = cap;

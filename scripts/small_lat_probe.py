@@ -48,14 +48,6 @@ def spin(us):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=400)
-    ap.add_argument("--warm", action="store_true",
-                    help="one resident sleeping wave keeps the GPU from idling during the cases "
-                         "(dora_gpu_test_keep_warm_start)")
-    ap.add_argument("--heartbeat", type=int, default=0,
-                    help="a host thread keeps touching the GPU during the cases "
-                         "(dora_gpu_test_heartbeat_start): 1 empty AQL packet, 2 PCIe read, "
-                         "3 PCIe write; 0 none")
-    ap.add_argument("--period", type=float, default=40.0, help="heartbeat period, us")
     ap.add_argument("--keep-awake-us", type=float, default=None,
                     help="dora_gpu_set_keep_awake period (0: off; default: the library's)")
     a = ap.parse_args()
@@ -90,20 +82,6 @@ def main():
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
     seq += 1
-    warm = None
-    if a.warm:
-        import ctypes
-
-        from dora_amd._lib import call
-        warm = ctypes.c_void_p()
-        call("dora_gpu_test_keep_warm_start", 0, 120.0, ctypes.byref(warm))
-    beat = None
-    if a.heartbeat:
-        import ctypes
-
-        from dora_amd._lib import call
-        beat = ctypes.c_void_p()
-        call("dora_gpu_test_heartbeat_start", 0, a.heartbeat, a.period, 120.0, ctypes.byref(beat))
     t_case = {}
     for label, z, gap, spun in CASES:
         t0 = time.time_ns()
@@ -118,10 +96,6 @@ def main():
         t_case[label] = (t0, time.time_ns())
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
-    if beat is not None:
-        call("dora_gpu_test_heartbeat_stop", beat)
-    if warm is not None:
-        call("dora_gpu_test_keep_warm_stop", warm)
     buf.free()
     stream.close()
     node.close()
@@ -135,7 +109,7 @@ def main():
             ev.setdefault(r["token"], {}).setdefault(int(r["point"]), int(r["t_ns"]))
     for label, z, gap, _ in CASES:
         s = series.get(z, {})
-        row = {"case": label, "warm": a.warm, "heartbeat": a.heartbeat, "period_us": a.period,
+        row = {"case": label,
                "keep_awake_us": a.keep_awake_us, "bytes": z, "gap_us": gap, "n": s.get("n"),
                "latency_p50_us": s.get("p50_us"), "latency_p99_us": s.get("p99_us"),
                "incl_send_p50_us": s.get("full_p50_us")}

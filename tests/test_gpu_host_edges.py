@@ -141,9 +141,8 @@ def test_device_producer_to_host_only_python_receiver(launcher):
 
 def test_host_only_receiver_staging_stress(launcher):
     """600 device messages of 8 B .. 1 MiB, each with new bytes (the source is rewritten after
-    every synchronous send), reach a receiver without a GPU byte for byte: below 1 MiB staged by
-    one AQL pack writing pinned host memory and signalling a host flag, 1 MiB by the copy
-    engines.  Checks the write-to-host ordering of the in-kernel signal under load."""
+    every synchronous send), reach a receiver without a GPU byte for byte, each staged by the
+    copy engines into a recycled pinned buffer (a stale or reused buffer would show)."""
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.device import DeviceBuffer
