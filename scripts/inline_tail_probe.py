@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where the inline small-message tail comes from (verdict r05 item 4; DESIGN §10.3).
+"""Where the inline small-message tail comes from (verdict r05 item 4; DESIGN §10.2).
 
 The bench's `latency_host` series, alone and traced: a Python node sends host bytes at a fixed
 spacing to the native bench sink (dora-gpu-bench-sink), with DORA_GPU_TRACE on, so every message
