@@ -196,28 +196,6 @@ struct AqlQueue {
   std::atomic<bool> warm_parked{false};
   std::atomic<bool> warm_stop{false};  // process exit (stop_warm_threads)
   std::thread warm_thread;
-  // experiment (aql_cp_hold): a queue of its own holding one barrier-AND packet whose dependency
-  // the host releases — does a pending packet keep the command processor from idling?
-  hsa_queue_t* hold_q = nullptr;
-  hsa_signal_t hold_sig{0};
-  bool holding = false;
-  // Armed lone dispatch (arm_locked): a queue of its own holding a barrier-AND
-  // packet that waits on a host signal, with a single-segment pack's dispatch packet behind it;
-  // the next lone pack of that grid writes its arguments into the pair's argument slot and
-  // releases the signal — no doorbell, no packet fetch, and a command processor kept awake by the
-  // pending barrier.
-  hsa_queue_t* arm_q = nullptr;
-  bool arm_broken = false;  // the queue or a signal could not be created: never armed
-  uint64_t arm_rd = 0;
-  hsa_signal_t arm_sig[4] = {};
-  uint64_t arm_sig_pkt[4] = {};  // packet index of the barrier that last waited on each signal
-  uint64_t arm_sig_next = 0;
-  bool armed = false;
-  uint32_t arm_grid = 0;
-  uint64_t arm_slot = 0;  // device ring slot of the pair's arguments (take_slot skips it)
-  uint32_t arm_cur = 0;   // arm_sig index of the pending barrier
-  std::deque<Use> arm_out;  // released armed packs not yet seen complete
-  uint64_t arm_hits = 0, arm_misses = 0, arm_count = 0;
   std::atomic<uint64_t> heartbeats{0};  // empty packets published (aql_heartbeats)
   std::mutex warm_mu;
   std::condition_variable warm_cv;
@@ -575,14 +553,9 @@ int big_queues(int nq, uint64_t bytes) {
   return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : 4);
 }
 
-void wake_warm(AqlQueue* a);
-
-// The argument slot of dispatch number a->next (a->mu held), past any abandoned slot and the
-// armed pair's.
+// The argument slot of dispatch number a->next (a->mu held), past any abandoned slot.
 uint64_t take_slot(AqlQueue* a) {
-  while (a->abandoned[a->next % kRingSlots] ||
-         (a->armed && a->next % kRingSlots == a->arm_slot))
-    ++a->next;
+  while (a->abandoned[a->next % kRingSlots]) ++a->next;
   return a->next % kRingSlots;
 }
 
@@ -591,144 +564,12 @@ uint64_t oldest_outstanding(const AqlQueue* a) {
   uint64_t m = a->next;
   for (int i = 0; i < a->nq; ++i)
     if (!a->outq[i].empty()) m = std::min(m, a->outq[i].front().seq);
-  if (!a->arm_out.empty()) m = std::min(m, a->arm_out.front().seq);
   return m;
-}
-
-// Armed lone dispatch.  Measured (scripts/arm_probe.py, profiles/r06_arm_probe.jsonl): a no-op
-// dispatch written ahead behind a barrier-AND and released by a signal store completes 6.9 us
-// after the release whatever the gap before it (p99 7.2-7.5), against 7.5 us through the doorbell
-// 20 us after the previous dispatch and 12.8-13.1 us >= 200 us after it (the command processor
-// asleep); arguments written after the packets were published were never stale (0 of 2400).
-std::atomic<bool> g_arm{[] {
-  const char* e = std::getenv("DORA_GPU_ARMED");  // A/B only (r06), removed once decided
-  return !(e && e[0] == '0');
-}()};
-const bool g_arm_low = [] {
-  const char* e = std::getenv("DORA_GPU_ARMED");
-  return e && e[0] == '2';
-}();
-
-// Release the pending barrier (a->mu held): its dispatch runs on whatever the pair's argument
-// slot holds — the no-op arguments written at arming, or a pack's.
-void arm_release_locked(AqlQueue* a) {
-  hsa_signal_store_screlease(a->arm_sig[a->arm_cur], 0);
-  a->armed = false;
-}
-
-// Write a pair for the next lone single-segment pack of `grid` workgroups (a->mu held).  Nothing
-// when it cannot be written without waiting (a signal or argument slot still in use).
-void arm_locked(AqlQueue* a, uint32_t grid) {
-  if (a->armed || a->arm_broken || !g_arm.load(std::memory_order_relaxed)) return;
-  while (!a->arm_out.empty() && fill_reached(a->arm_out.front().flag, a->arm_out.front().epoch))
-    a->arm_out.pop_front();
-  if (!a->arm_q && hsa_queue_create(a->gpu, 256, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
-                                    UINT32_MAX, UINT32_MAX, &a->arm_q) != HSA_STATUS_SUCCESS) {
-    a->arm_q = nullptr;
-    a->arm_broken = true;
-    return;
-  } else if (g_arm_low && a->arm_count == 0) {
-    hsa_amd_queue_set_priority(a->arm_q, HSA_AMD_QUEUE_PRIORITY_LOW);
-  }
-  hsa_queue_t* const q = a->arm_q;
-  const uint32_t si = uint32_t(a->arm_sig_next % 4);
-  if (!a->arm_sig[si].handle) {
-    if (hsa_signal_create(1, 0, nullptr, &a->arm_sig[si]) != HSA_STATUS_SUCCESS) {
-      a->arm_sig[si].handle = 0;
-      a->arm_broken = true;
-      return;
-    }
-  } else if (a->arm_sig_next >= 4 &&
-             hsa_queue_load_read_index_scacquire(q) <= a->arm_sig_pkt[si]) {
-    return;  // the barrier that last waited on this signal is not consumed yet
-  }
-  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
-  if (idx + 2 - a->arm_rd > q->size &&
-      idx + 2 - (a->arm_rd = hsa_queue_load_read_index_scacquire(q)) > q->size)
-    return;
-  const uint64_t r = take_slot(a);
-  Use& u = a->uses[r];
-  if (u.flag && u.seq >= oldest_outstanding(a) && !fill_reached(u.flag, u.epoch)) return;
-  u = Use{nullptr, 0, a->next};
-  ++a->next;
-  // no-op arguments (aql_kernels.hip pack1: zero length, no flag, no done words)
-  uint8_t args[kArgs1Bytes] = {};
-  std::memcpy(args + 52, &grid, 4);
-  std::memcpy(a->ring + r * kSlotBytes, args, kArgs1Bytes);
-  __builtin_ia32_sfence();
-  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;
-  hsa_signal_store_relaxed(a->arm_sig[si], 1);
-  hsa_queue_store_write_index_relaxed(q, idx + 2);
-  auto* b = static_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  std::memset(reinterpret_cast<uint8_t*>(b) + 4, 0, sizeof(*b) - 4);
-  b->dep_signal[0] = a->arm_sig[si];
-  auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + ((idx + 1) & (q->size - 1));
-  const int k = kOneCohKernel;  // a lone pack's kernel and packet (dispatch_locked)
-  p->workgroup_size_x = 256;
-  p->workgroup_size_y = 1;
-  p->workgroup_size_z = 1;
-  p->reserved0 = 0;
-  p->grid_size_x = grid * 256u;
-  p->grid_size_y = 1;
-  p->grid_size_z = 1;
-  p->private_segment_size = a->priv[k];
-  p->group_segment_size = a->group[k];
-  p->kernel_object = a->kobj[k];
-  p->kernarg_address = a->ring + r * kSlotBytes;
-  p->reserved2 = 0;
-  p->completion_signal = hsa_signal_t{0};
-  const uint16_t hk = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-  const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  // the dispatch's header first: the command processor stops at the barrier's until it is written
-  if (a->wc_ring) __builtin_ia32_sfence();
-  __atomic_store_n(reinterpret_cast<uint32_t*>(p), hk | (uint32_t(setup) << 16), __ATOMIC_RELEASE);
-  const uint16_t hb = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                      (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-  publish_packet(q, b, hb, idx + 1, a->wc_ring);
-  a->armed = true;
-  a->arm_grid = grid;
-  a->arm_slot = r;
-  a->arm_cur = si;
-  a->arm_sig_pkt[si] = idx;
-  ++a->arm_sig_next;
-  ++a->arm_count;
-}
-
-// A lone single-segment pack through the armed pair (a->mu held): if the pair's grid is the
-// pack's, its arguments go into the pair's slot and the barrier is released (*used); otherwise a
-// pending pair is released as a no-op.  *grid: the pack's grid.
-int armed_dispatch_locked(AqlQueue* a, const Pending& it, bool* used, uint32_t* grid) {
-  *used = false;
-  uint8_t args[kSlotBytes];
-  const int rc = build_aql_args1(it.segs[0], it.dst, it.sig, args, grid);
-  if (rc != DORA_OK || !a->armed) return rc;
-  if (*grid != a->arm_grid) {
-    arm_release_locked(a);
-    ++a->arm_misses;
-    return DORA_OK;
-  }
-  SubSpan sp_disp(SP_AQL_DISPATCH);
-  std::memcpy(a->ring + a->arm_slot * kSlotBytes, args, kArgs1Bytes);
-  __builtin_ia32_sfence();
-  *reinterpret_cast<volatile uint32_t*>(a->hdp) = 1;  // posted before the signal store below
-  Use& u = a->uses[a->arm_slot];
-  u.flag = it.flag_host;
-  u.epoch = it.sig.epoch;
-  a->arm_out.push_back(u);
-  arm_release_locked(a);
-  a->activity.store(a->next + 1, std::memory_order_relaxed);
-  if (a->warm_parked.load(std::memory_order_relaxed)) wake_warm(a);
-  ++a->dispatched[kOneCohKernel];
-  ++a->arm_hits;
-  *used = true;
-  return DORA_OK;
 }
 
 // Write and ring one packet on queue `qi` (a->mu held): one message with the single- or
 // multi-segment kernels, or a batch of `n` > 1 messages with dora_aql_packb_u4.
+void wake_warm(AqlQueue* a);
 
 int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool big) {
   const Pending& it0 = items[0];
@@ -807,10 +648,6 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // (aql_pipeline_bench modes 5 vs 7, profiles/r04_lone_dispatch_ab.jsonl).  Pipelined packs keep
   // the host ring: no HDP flush per send.
   const bool dev_args1 = one && it0.lone;
-  // a pack through the queues (pipelined, big or multi-segment): the armed pair goes (as a
-  // no-op) — a barrier pending on another queue delays these packs' dispatch (aql_cp_hold:
-  // +0.5 us p50, p99 12.5-14.8 us), the keep-awake thread covers them instead
-  if (a->armed) arm_release_locked(a);
   if (one && !dev_args1) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
     slot = a->hring + r * kHostSlotBytes;
@@ -1007,7 +844,6 @@ void pump_locked(AqlQueue* a) {
 // One empty barrier-AND packet (no dependencies, no completion signal) on the first queue
 // (a->mu held); nothing if that queue's ring is full.
 void heartbeat_locked(AqlQueue* a) {
-  if (a->armed) return;  // the pending barrier keeps the command processor awake
   hsa_queue_t* const q = a->qs[0];
   const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
   if (idx - a->rd[0] >= q->size && idx - (a->rd[0] = hsa_queue_load_read_index_scacquire(q)) >= q->size)
@@ -1059,10 +895,6 @@ void warm_main(AqlQueue* a) {
       continue;
     }
     if (now - last_change > kWarmWindow) {
-      {  // an idle process leaves the command processor to sleep
-        std::lock_guard<std::mutex> g(a->mu);
-        if (a->armed) arm_release_locked(a);
-      }
       // park; a dispatch wakes it (wake_warm).  The 10 ms bound covers a dispatch that raced
       // the parking.
       std::unique_lock<std::mutex> lk(a->warm_mu);
@@ -1086,14 +918,6 @@ void warm_main(AqlQueue* a) {
 // At exit: no empty packet may be written into a queue while HSA tears it down.
 void stop_warm_threads() {
   for (AqlQueue* a : g_queues) {
-    if (a && a->holding) {  // a held barrier (aql_cp_hold) is released first
-      hsa_signal_store_screlease(a->hold_sig, 0);
-      a->holding = false;
-    }
-    if (a) {  // and an armed pair, as a no-op
-      std::lock_guard<std::mutex> g(a->mu);
-      if (a->armed) arm_release_locked(a);
-    }
     if (!a || !a->warm_thread.joinable()) continue;
     {
       std::lock_guard<std::mutex> g(a->warm_mu);
@@ -1177,20 +1001,6 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // (four below 32 MiB) queues, big_queues: more concurrent 40 MB copies only contend (14.1-14.5
   // us per pack without the barrier, 12.9-13.0 with it; profiles/r02_aql_big_ab.jsonl).
   const bool big = p.bytes >= kBarrierBytes;
-  // a lone in-kernel-signalled single-segment pack: through the armed pair when its grid matches,
-  // and a pair is armed for the next one either way
-  const bool armable = p.lone && !p.cp && !p.profile && n == 1 && segs[0].dst_off == 0 &&
-                       a->hring && !big && g_arm.load(std::memory_order_relaxed);
-  uint32_t arm_grid = 0;
-  if (armable) {
-    bool used = false;
-    const int rc = armed_dispatch_locked(a, p, &used, &arm_grid);
-    if (rc != DORA_OK) return rc;
-    if (used) {
-      arm_locked(a, arm_grid);
-      return DORA_OK;
-    }
-  }
   if (big) {
     const size_t qi = size_t(a->next_big++ % uint64_t(big_queues(a->nq, p.bytes)));
     const int rc = dispatch_locked(a, qi, &p, 1, true);
@@ -1207,11 +1017,7 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   p.chunk = aql_chunk_bytes(segs, n);
   if (a->backlog.empty()) {
     const int qi = pick_queue(a, 0, p.cp ? kCpDepth : 0);
-    if (qi >= 0) {
-      const int rc = dispatch_locked(a, size_t(qi), &p, 1, false);
-      if (rc == DORA_OK && armable) arm_locked(a, arm_grid);
-      return rc;
-    }
+    if (qi >= 0) return dispatch_locked(a, size_t(qi), &p, 1, false);
   }
   a->backlog.push_back(p);
   ++a->backlogged;
@@ -1363,181 +1169,6 @@ int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint6
   *batches = a->batches;
   *batched_msgs = a->batched_msgs;
   *backlogged = a->backlogged;
-  return DORA_OK;
-}
-
-int aql_cp_hold(int device, bool on) {
-  AqlQueue* a = aql_queue(device);
-  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
-  std::lock_guard<std::mutex> g(a->mu);
-  if (!on) {
-    if (a->holding) hsa_signal_store_screlease(a->hold_sig, 0);
-    a->holding = false;
-    return DORA_OK;
-  }
-  if (a->holding) return DORA_OK;
-  if (!a->hold_q && hsa_queue_create(a->gpu, 64, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a,
-                                     UINT32_MAX, UINT32_MAX, &a->hold_q) != HSA_STATUS_SUCCESS) {
-    a->hold_q = nullptr;
-    return fail(DORA_ERR_HIP, "hold queue");
-  }
-  if (!a->hold_sig.handle && hsa_signal_create(1, 0, nullptr, &a->hold_sig) != HSA_STATUS_SUCCESS) {
-    a->hold_sig.handle = 0;
-    return fail(DORA_ERR_HIP, "hold signal");
-  }
-  hsa_signal_store_relaxed(a->hold_sig, 1);
-  hsa_queue_t* const q = a->hold_q;
-  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
-  if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size)
-    return fail(DORA_ERR_HIP, "hold queue full");
-  hsa_queue_store_write_index_relaxed(q, idx + 1);
-  auto* p = static_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  std::memset(reinterpret_cast<uint8_t*>(p) + 4, 0, sizeof(*p) - 4);
-  p->dep_signal[0] = a->hold_sig;
-  const uint16_t header = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                          (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                          (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-  publish_packet(q, p, header, idx, false);
-  a->holding = true;
-  return DORA_OK;
-}
-
-int aql_arm_probe(int device, int mode, uint32_t n, uint64_t gap_ns, uint64_t* out_ns) {
-  AqlQueue* a = aql_queue(device);
-  if (!a || !a->hring) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
-  if (n == 0 || !out_ns) return fail(DORA_ERR_INVALID, "arm probe: n");
-  std::lock_guard<std::mutex> g(a->mu);
-  hsa_queue_t* q = nullptr;
-  if (hsa_queue_create(a->gpu, 256, HSA_QUEUE_TYPE_SINGLE, on_queue_error, a, UINT32_MAX,
-                       UINT32_MAX, &q) != HSA_STATUS_SUCCESS)
-    return fail(DORA_ERR_HIP, "probe queue");
-  hsa_signal_t done{0}, go{0};
-  if (hsa_signal_create(1, 0, nullptr, &done) != HSA_STATUS_SUCCESS ||
-      hsa_signal_create(1, 0, nullptr, &go) != HSA_STATUS_SUCCESS) {
-    hsa_queue_destroy(q);
-    return fail(DORA_ERR_HIP, "probe signals");
-  }
-  // the reduction kernel with n = 0: one workgroup that returns at once.  Mode 2 (armed, its
-  // arguments written only after the gap): n = 1 over a two-word area in pinned host memory, so
-  // a dispatch that ran on arguments read before they were written shows in out[]
-  uint64_t* hbuf = nullptr;
-  if (mode == 2 && (hipHostMalloc(reinterpret_cast<void**>(&hbuf), 4096, 0) != hipSuccess || !hbuf)) {
-    hsa_queue_destroy(q);
-    return fail(DORA_ERR_HIP, "probe buffer");
-  }
-  const uint64_t r = take_slot(a);
-  a->uses[r] = Use{nullptr, 0, a->next};
-  ++a->next;
-  uint8_t* slot = a->hring + r * kHostSlotBytes;
-  std::memset(slot, 0, kHostSlotBytes);
-  auto put_kernel = [&](uint64_t idx) {
-    auto* p = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-    const int k = kReduceKernel;
-    p->workgroup_size_x = 256;
-    p->workgroup_size_y = 1;
-    p->workgroup_size_z = 1;
-    p->reserved0 = 0;
-    p->grid_size_x = 256;
-    p->grid_size_y = 1;
-    p->grid_size_z = 1;
-    p->private_segment_size = a->priv[k];
-    p->group_segment_size = a->group[k];
-    p->kernel_object = a->kobj[k];
-    p->kernarg_address = slot;
-    p->reserved2 = 0;
-    p->completion_signal = done;
-    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                            (1 << HSA_PACKET_HEADER_BARRIER) |
-                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-    publish_packet(q, p, header | (uint32_t(setup) << 16), idx, a->wc_ring);
-  };
-  auto put_barrier = [&](uint64_t idx) {
-    auto* p = static_cast<hsa_barrier_and_packet_t*>(q->base_address) + (idx & (q->size - 1));
-    std::memset(reinterpret_cast<uint8_t*>(p) + 4, 0, sizeof(*p) - 4);
-    p->dep_signal[0] = go;
-    const uint16_t header = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-    publish_packet(q, p, header, idx, a->wc_ring);
-  };
-  using clock = std::chrono::steady_clock;
-  int rc = DORA_OK;
-  for (uint32_t i = 0; i < n && rc == DORA_OK; ++i) {
-    hsa_signal_store_relaxed(done, 1);
-    const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
-    if (mode == 2) {
-      std::memset(slot, 0, kHostSlotBytes);
-      std::memset(hbuf, 0, 256);
-    }
-    if (mode >= 1) {  // armed: barrier + kernel written now, released after the gap
-      hsa_signal_store_relaxed(go, 1);
-      hsa_queue_store_write_index_relaxed(q, idx + 2);
-      put_barrier(idx);
-      put_kernel(idx + 1);
-    }
-    const auto until = clock::now() + std::chrono::nanoseconds(gap_ns);
-    while (clock::now() < until) __builtin_ia32_pause();
-    const auto t0 = clock::now();
-    if (mode == 2) {
-      hbuf[0] = i + 1;
-      hbuf[1] = 7;
-      reinterpret_cast<uint32_t*>(hbuf + 8)[0] = 0;  // areas[0]
-      const uint64_t w[3] = {reinterpret_cast<uintptr_t>(hbuf), reinterpret_cast<uintptr_t>(hbuf + 8),
-                             reinterpret_cast<uintptr_t>(hbuf + 16)};
-      const uint32_t nw[2] = {1, 2};  // n, area_words
-      std::memcpy(slot, w, sizeof(w));
-      std::memcpy(slot + 24, nw, sizeof(nw));
-    }
-    if (mode >= 1) {
-      hsa_signal_store_screlease(go, 0);
-    } else {
-      hsa_queue_store_write_index_relaxed(q, idx + 1);
-      put_kernel(idx);
-    }
-    while (hsa_signal_load_scacquire(done) > 0) {
-      __builtin_ia32_pause();
-      if (clock::now() - t0 > std::chrono::seconds(2)) {
-        rc = fail(DORA_ERR_TIMEOUT, "arm probe: no completion");
-        break;
-      }
-    }
-    out_ns[i] = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(clock::now() - t0).count());
-    if (mode == 2 && rc == DORA_OK &&
-        (__atomic_load_n(hbuf + 16, __ATOMIC_ACQUIRE) != i + 1 ||
-         __atomic_load_n(hbuf + 17, __ATOMIC_ACQUIRE) != 7))
-      out_ns[i] |= uint64_t(1) << 63;  // ran on stale arguments
-  }
-  if (hbuf && rc == DORA_OK) (void)hipHostFree(hbuf);
-  if (rc != DORA_OK) {
-    hsa_signal_store_screlease(go, 0);  // let a held packet run before the queue goes
-    a->failed.store(true);
-    return rc;  // the queue and signals are left to the process's teardown
-  }
-  hsa_queue_destroy(q);
-  hsa_signal_destroy(done);
-  hsa_signal_destroy(go);
-  return DORA_OK;
-}
-
-void aql_arm(bool on) {
-  g_arm.store(on);
-  if (on) return;
-  for (AqlQueue* a : g_queues) {
-    if (!a) continue;
-    std::lock_guard<std::mutex> g(a->mu);
-    if (a->armed) arm_release_locked(a);
-  }
-}
-
-int aql_arm_stats(int device, uint64_t* hits, uint64_t* misses, uint64_t* arms) {
-  AqlQueue* a = aql_queue(device);
-  if (!a) return fail(DORA_ERR_UNSUPPORTED, "no AQL queue on device %d", device);
-  std::lock_guard<std::mutex> g(a->mu);
-  *hits = a->arm_hits;
-  *misses = a->arm_misses;
-  *arms = a->arm_count;
   return DORA_OK;
 }
 

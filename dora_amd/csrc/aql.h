@@ -106,19 +106,6 @@ void bar_publish(AqlQueue* q, const void* last);
 int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
                      const uint32_t* areas, uint32_t n, uint64_t* out);
 
-// Experiment (dora_gpu_test_cp_hold): while `on`, a queue of the process holds one barrier-AND
-// packet waiting on a host signal; `off` releases it.
-int aql_cp_hold(int device, bool on);
-// Armed lone dispatch (aql.cpp arm_locked): on/off for the process, and per device the lone packs
-// that went through a pair, the pairs released unused (another grid), and the pairs written.
-void aql_arm(bool on);
-int aql_arm_stats(int device, uint64_t* hits, uint64_t* misses, uint64_t* arms);
-// Experiment (dora_gpu_test_arm_probe): `n` no-op dispatches on a queue of their own, `gap_ns`
-// apart; mode 0 rings the doorbell after the gap, mode 1 writes a barrier-AND + the dispatch
-// before it and releases the barrier's signal after; mode 2 as 1 with the dispatch's arguments
-// written after the gap (bit 63 of out_ns[i]: it ran on the old ones).  out_ns[i]: release ->
-// completion seen.
-int aql_arm_probe(int device, int mode, uint32_t n, uint64_t gap_ns, uint64_t* out_ns);
 // Test hooks: the stamp reduction's wait (0: the default 5 s), and the argument slots left to
 // reductions that timed out (never written again).
 void aql_reduce_timeout(uint64_t ns);

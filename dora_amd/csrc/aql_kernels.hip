@@ -30,7 +30,6 @@ template <int U, int NT = 2>
 __device__ __forceinline__ void pack1(uint8_t* dst, const uint8_t* src, uint64_t len,
                                       uint64_t* flag, uint32_t* done, uint64_t epoch,
                                       uint32_t chunk_bytes, uint32_t grid) {
-  if (len == 0 && !flag && !done) return;  // the no-op arguments of an armed dispatch (aql.cpp)
   const uint64_t nc =
       dora::pack::segment_chunks(reinterpret_cast<uintptr_t>(dst), 0, len, chunk_bytes);
   dora::pack::PackArgsT<1> a;

@@ -127,18 +127,6 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
 
-int dora_gpu_test_cp_hold(int device, int on) { return dora::aql_cp_hold(device, on != 0); }
-int dora_gpu_test_armed(int on) {
-  dora::aql_arm(on != 0);
-  return DORA_OK;
-}
-int dora_gpu_test_arm_stats(int device, uint64_t* out3) {
-  return dora::aql_arm_stats(device, out3, out3 + 1, out3 + 2);
-}
-int dora_gpu_test_arm_probe(int device, int mode, uint32_t n, uint64_t gap_ns, uint64_t* out_ns) {
-  return dora::aql_arm_probe(device, mode, n, gap_ns, out_ns);
-}
-
 int dora_gpu_test_reduce_timeout(uint64_t ns) {
   dora::aql_reduce_timeout(ns);
   return DORA_OK;

@@ -32,16 +32,6 @@ int dora_gpu_test_aql_hold(int device, int hold);
  * (ns; 0 = the default 5 s) — a tiny value makes the wait time out while the packet still runs —
  * and the AQL argument slots left to reductions that timed out (never written again). */
 int dora_gpu_test_reduce_timeout(uint64_t ns);
-/* Experiment: while `on`, one barrier-AND packet waiting on a host signal sits on a queue of its
- * own of `device` (does a pending packet keep the command processor awake?); 0 releases it. */
-int dora_gpu_test_cp_hold(int device, int on);
-/* Armed lone dispatch: on / off for the process; per device the lone packs that
- * went through an armed pair, the pairs released unused, and the pairs written (out3[3]). */
-int dora_gpu_test_armed(int on);
-int dora_gpu_test_arm_stats(int device, uint64_t* out3);
-/* Experiment: release -> completion of `n` no-op dispatches `gap_ns` apart (mode 0 doorbell,
- * 1 a barrier-AND written ahead and released), into out_ns[n]. */
-int dora_gpu_test_arm_probe(int device, int mode, uint32_t n, uint64_t gap_ns, uint64_t* out_ns);
 int dora_gpu_test_abandoned_slots(int device, uint32_t* slots);
 /* Test tool: empty packets the keep-awake thread of `device` has published in this process
  * (dora_gpu_set_keep_awake), and whether it is parked (no send for 100 ms). */

@@ -48,11 +48,6 @@ def spin(us):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=400)
-    ap.add_argument("--cp-hold", action="store_true",
-                    help="during the cases, one barrier-AND packet waiting on a host signal sits "
-                         "on a queue of its own (dora_gpu_test_cp_hold)")
-    ap.add_argument("--armed", action="store_true",
-                    help="lone packs through a dispatch written ahead (dora_gpu_test_armed)")
     ap.add_argument("--keep-awake-us", type=float, default=None,
                     help="dora_gpu_set_keep_awake period (0: off; default: the library's)")
     a = ap.parse_args()
@@ -87,11 +82,6 @@ def main():
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
     seq += 1
-    from dora_amd._lib import call
-    if a.cp_hold:
-        call("dora_gpu_test_cp_hold", 0, 1)
-    if a.armed:
-        call("dora_gpu_test_armed", 1)
     t_case = {}
     for label, z, gap, spun in CASES:
         t0 = time.time_ns()
@@ -106,15 +96,6 @@ def main():
         t_case[label] = (t0, time.time_ns())
     node.send_output("throughput", b"", {"seq": seq, "ack": True})
     node.wait_input("ack", "seq", seq, 60.0)
-    if a.cp_hold:
-        call("dora_gpu_test_cp_hold", 0, 0)
-    arm = None
-    if a.armed:
-        import ctypes
-        v = (ctypes.c_uint64 * 3)()
-        call("dora_gpu_test_arm_stats", 0, v)
-        arm = {"hits": v[0], "misses": v[1], "arms": v[2]}
-        call("dora_gpu_test_armed", 0)
     buf.free()
     stream.close()
     node.close()
@@ -128,7 +109,7 @@ def main():
             ev.setdefault(r["token"], {}).setdefault(int(r["point"]), int(r["t_ns"]))
     for label, z, gap, _ in CASES:
         s = series.get(z, {})
-        row = {"case": label, "cp_hold": a.cp_hold, "armed": arm,
+        row = {"case": label,
                "keep_awake_us": a.keep_awake_us, "bytes": z, "gap_us": gap, "n": s.get("n"),
                "latency_p50_us": s.get("p50_us"), "latency_p99_us": s.get("p99_us"),
                "incl_send_p50_us": s.get("full_p50_us")}
