@@ -867,6 +867,14 @@ void heartbeat_locked(AqlQueue* a) {
 // dispatched since its last wake, publishes one such packet; kWarmWindow after the last dispatch
 // it parks until the next.  dora_gpu_set_keep_awake sets the period (default 25 us; 0: off).
 constexpr auto kWarmWindow = std::chrono::milliseconds(100);
+// A slow periodic sender — its last kSlowSends dispatches each came more than kSlowGap after the
+// one before — would pay kSlowGap / period wake-ups per message for a wake-up of ~5.5 us
+// (a 10 Hz sender never parked): its thread parks kSlowIdle after each dispatch
+// instead (the command processor itself idles after 50-200 us), and one quicker dispatch brings
+// the 100 ms window back.
+constexpr auto kSlowGap = std::chrono::milliseconds(5);
+constexpr auto kSlowIdle = std::chrono::microseconds(200);
+constexpr int kSlowSends = 3;
 std::atomic<int64_t> g_warm_period_ns{25000};
 
 void warm_main(AqlQueue* a) {
@@ -875,6 +883,11 @@ void warm_main(AqlQueue* a) {
   uint64_t seen = a->activity.load(std::memory_order_relaxed);
   auto last_change = clock::now();
   auto next = last_change;
+  int slow = 0;  // consecutive dispatches more than kSlowGap apart
+  auto note_gap = [&](clock::time_point now) {
+    slow = now - last_change > kSlowGap ? std::min(slow + 1, kSlowSends) : 0;
+    last_change = now;
+  };
   while (!a->failed.load(std::memory_order_relaxed) &&
          !a->warm_stop.load(std::memory_order_relaxed)) {
     const auto period = std::chrono::nanoseconds(g_warm_period_ns.load(std::memory_order_relaxed));
@@ -891,10 +904,11 @@ void warm_main(AqlQueue* a) {
     const uint64_t c = a->activity.load(std::memory_order_relaxed);
     if (c != seen) {
       seen = c;
-      last_change = now;
+      note_gap(now);
       continue;
     }
-    if (now - last_change > kWarmWindow) {
+    if (now - last_change > (slow >= kSlowSends ? std::chrono::duration_cast<clock::duration>(kSlowIdle)
+                                                 : std::chrono::duration_cast<clock::duration>(kWarmWindow))) {
       // park; a dispatch wakes it (wake_warm).  The 10 ms bound covers a dispatch that raced
       // the parking.
       std::unique_lock<std::mutex> lk(a->warm_mu);
@@ -905,7 +919,8 @@ void warm_main(AqlQueue* a) {
         a->warm_cv.wait_for(lk, std::chrono::milliseconds(10));
       a->warm_parked.store(false);
       seen = a->activity.load(std::memory_order_relaxed);
-      last_change = next = clock::now();
+      note_gap(clock::now());  // woken by a dispatch (or the stop)
+      next = last_change;
       continue;
     }
     if (a->mu.try_lock()) {  // busy: a send is being dispatched right now

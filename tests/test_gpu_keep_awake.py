@@ -1,6 +1,8 @@
 """The keep-awake thread (aql.cpp warm_main, dora_gpu_set_keep_awake): while a node sends device
 samples it publishes empty AQL packets whenever nothing was dispatched for one period, parks
-100 ms after the last send, wakes with the next one, and stops when the period is set to 0."""
+100 ms after the last send, wakes with the next one, and stops when the period is set to 0.  A
+slow periodic sender (three sends in a row > 5 ms apart) has it park 200 us after each send
+instead, until a quicker send."""
 import ctypes
 import time
 
@@ -69,3 +71,44 @@ def test_keep_awake_beats_while_sending_then_parks(tmp_path):
             assert df.wait(30)["sink"] == 0, df.log("sink")
     finally:
         device.set_keep_awake(25)
+
+
+def test_slow_periodic_sender_parks_after_each_send(tmp_path):
+    from dora_amd import device
+    from dora_amd.dataflow import Dataflow
+    from dora_amd.node import Node
+    desc = {"nodes": [
+        {"id": "node", "path": "dynamic", "outputs": ["latency"], "inputs": {"ack": "sink/ack"}},
+        {"id": "sink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
+         "inputs": {"latency": {"source": "node/latency", "queue_size": 10}},
+         "env": {"DORA_BENCH_RESULT": str(tmp_path / "sink.json")}},
+    ]}
+    device.set_keep_awake(25)
+    with Dataflow(desc) as df:
+        node = Node("node", dataflow=df.shm, device=0)
+        buf = device.DeviceBuffer(4096)
+        seq = 0
+        for _ in range(5):  # 30 ms apart: slow from the fourth on
+            node.send_output_device_bytes("latency", buf.ptr, 4096, {"seq": seq})
+            seq += 1
+            time.sleep(0.03)
+        b0, _ = _stats()
+        node.send_output_device_bytes("latency", buf.ptr, 4096, {"seq": seq})
+        seq += 1
+        time.sleep(0.03)
+        b1, parked = _stats()
+        # 200 us at one packet per 25 us is ~8; a whole 30 ms awake would be ~1200
+        assert parked and b1 - b0 <= 60, (b0, b1, parked)
+        for _ in range(6):  # 1 ms apart: the 100 ms window again
+            node.send_output_device_bytes("latency", buf.ptr, 4096, {"seq": seq})
+            seq += 1
+            time.sleep(0.001)
+        b2, _ = _stats()
+        time.sleep(0.03)
+        b3, parked = _stats()
+        assert b3 - b2 > 50 and not parked, (b2, b3, parked)
+        node.send_output("latency", b"", {"seq": seq, "ack": True})
+        node.wait_input("ack", "seq", seq, 30.0)
+        buf.free()
+        node.close()
+        assert df.wait(30)["sink"] == 0, df.log("sink")
