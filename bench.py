@@ -39,8 +39,10 @@ LADDER_SMALL = [0, 8, 64, 512, 2048]
 # host-resident sources of the latency ladder (output `latency_host`): below 4096 B they travel
 # inline as the reference's DataMessage::Vec (no slot, no GPU), 4096 B is an H2D device sample
 LADDER_HOST = [8, 512, 2048, 4096, 65536, 4 << 20, 6220800, 40960000]
-# device-resident sources delivered to a node without a GPU (`hostsink`, DORA_GPU_DEVICE -1):
-# staged to host memory on receipt, the reference's host ArrowData (event.rs:35-91)
+# device-resident sources delivered to a node without a GPU (`hostsink`, DORA_GPU_DEVICE -1),
+# the reference's host ArrowData (event.rs:35-91): `to_host` has no other receiver, so samples
+# <= 1 MiB are packed by the producer straight into shared memory, larger ones staged to host
+# memory on receipt
 LADDER_D2H = [8, 4096, 65536, 1 << 20, 6220800, 40960000]
 
 
@@ -733,7 +735,7 @@ def main():
          "outputs": ["latency", "latency_host", "throughput", "to_host", "to_host_warm"],
          "inputs": {"ack": "sink/ack", "ack_host": "hostsink/ack"},
          "_unstable_deploy": {"gpu": local_rank}},
-        # a receiver without a GPU: device samples reach it staged in host memory
+        # a receiver without a GPU: device samples reach it in host memory
         {"id": "hostsink", "path": "dora-gpu-bench-sink", "outputs": ["ack"],
          "inputs": {"to_host": {"source": "node/to_host", "queue_size": 10},
                     "to_host_warm": {"source": "node/to_host_warm", "queue_size": 10}},
@@ -1201,7 +1203,8 @@ def main():
                                        "p99_incl_pack_us": s["full_p99_us"], "n": s["n"],
                                        "verified": s["verified"], "mismatches": s["mismatches"]}
     # host paths as rates against this box's PCIe DMA (pinned <-> HBM, box_h2d): host sources
-    # (BAR writes to 2 MiB, HIP's copy above) and device samples staged for a host-only receiver
+    # (BAR writes to 2 MiB, HIP's copy above) and device samples for a host-only receiver
+    # (packed into shared memory to 1 MiB, staged on receipt above)
     host_rates = {}
     for key, z in ([(f"host_{z}", z) for z in LADDER_HOST if z >= 4096] +
                    [(f"d2h_{z}", z) for z in LADDER_D2H if z >= 4096]):

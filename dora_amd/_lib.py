@@ -144,7 +144,7 @@ _SIGS = {
     "dora_node_set_timing_period": (c_int, [c_void_p, c_uint64]),
     "dora_node_fill_paths": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_host_paths": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64),
-                                     POINTER(c_uint64)]),
+                                     POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_plan_cache_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_dataflow_counters": (c_int, [c_void_p, c_char_p, POINTER(c_uint64),
                                             POINTER(c_uint64), POINTER(c_uint64)]),

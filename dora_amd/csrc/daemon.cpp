@@ -438,14 +438,11 @@ class Daemon {
         nodes_[i].subscribed = true;
         region_->hdr()->nodes[i].state.store(1);
         if (ready_sent_) {
-          push_event(i, EV_READY, {});
+          push_event(i, EV_READY, ready_payload(i));
         } else {
           bool all = true;
           for (auto& n : nodes_) all &= n.subscribed || n.done;
-          if (all) {
-            ready_sent_ = true;
-            for (size_t k = 0; k < nodes_.size(); ++k) push_event(static_cast<int>(k), EV_READY, {});
-          }
+          if (all) send_ready();
         }
         break;
       case REQ_SEND_MESSAGE: {
@@ -626,11 +623,40 @@ class Daemon {
     if (!ready_sent_) {  // a node that exits before subscribing must not stall the others
       bool all = true;
       for (auto& n : nodes_) all &= n.subscribed || n.done;
-      if (all) {
-        ready_sent_ = true;
-        for (size_t k = 0; k < nodes_.size(); ++k) push_event(static_cast<int>(k), EV_READY, {});
-      }
+      if (all) send_ready();
     }
+  }
+
+  // AllNodesReady (the reference's PendingNodes, daemon pending.rs): every node has subscribed
+  // (or exited), so every node's GPU is known.
+  void send_ready() {
+    ready_sent_ = true;
+    for (size_t k = 0; k < nodes_.size(); ++k)
+      push_event(static_cast<int>(k), EV_READY, ready_payload(static_cast<int>(k)));
+  }
+
+  // EV_READY's payload for node i: its outputs whose every receiver is a running local node
+  // without a GPU (DORA_GPU_DEVICE < 0) — such samples are wanted in host memory only, so the
+  // producer packs them straight into shared memory (node.cpp pack_and_send) instead of into
+  // an HBM slot each receiver would copy out.  [u32 n][str output] x n.
+  std::vector<uint8_t> ready_payload(int i) {
+    std::vector<const std::string*> outs;
+    for (const auto& kv : outputs_[size_t(i)]) {
+      if (remote_[size_t(i)].count(kv.first)) continue;
+      size_t live = 0;
+      bool host = true;
+      for (const Receiver& rc : kv.second) {
+        if (nodes_[size_t(rc.node)].done) continue;
+        ++live;
+        host &= region_->hdr()->nodes[rc.node].device.load() == -1;
+      }
+      if (live && host) outs.push_back(&kv.first);
+    }
+    if (outs.empty()) return {};
+    WBuf w;
+    w.u32(static_cast<uint32_t>(outs.size()));
+    for (const std::string* o : outs) w.str(*o);
+    return w.take();
   }
 
   void check_liveness() {

@@ -174,6 +174,9 @@ struct Slot {
   // host-only node: a POSIX shared-memory region (DataMessage::SharedMemory) instead of HBM
   bool host = false;
   std::string shm_name;
+  // a device node's shared-memory slot (host_bound_sample): page-locked and mapped for the GPU,
+  // which packs into it
+  bool registered = false;
   // device slot mapped for the CPU through the large BAR (host sources written in place,
   // host_bar_fill): tried once per slot
   bool bar = false, bar_tried = false;
@@ -182,6 +185,7 @@ struct Slot {
 // The memory of a slot no fill can still write (its events, its HBM or shared-memory region).
 void release_slot_memory(Slot* s) {
   if (s->host) {
+    if (s->registered) (void)hipHostUnregister(s->ptr);
     shmem_unmap(s->ptr, s->cap);
     shmem_unlink(s->shm_name);
   } else {
@@ -845,6 +849,10 @@ struct dora_node {
   std::vector<uint32_t> region_cp_used;
   uint64_t aql_packs = 0, hip_packs = 0;  // fills by dispatch path
   uint64_t bar_fills = 0;  // host sources written into their slot by the CPU (host_bar_fill)
+  // outputs whose every receiver has no GPU (the daemon's AllNodesReady): device sources up to
+  // kHostPackMax are packed straight into shared memory for them (host_bound_sample)
+  std::set<std::string, std::less<>> host_bound;
+  uint64_t host_packs = 0;
   bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
@@ -1103,10 +1111,12 @@ uint64_t slot_bytes(uint64_t len) {
 // capacity the oldest returned one, whose last fill has had the longest to complete and whose
 // flag line on_token has prefetched (the reference takes the newest; any fit is equivalent).
 // `need`: the smallest capacity a new slot of `len` would have (an exact fit ends the search).
-int best_fit(dora_node* n, uint64_t len, uint64_t need) {
+// `host`: a shared-memory slot is wanted (a device node caches both kinds).
+int best_fit(dora_node* n, uint64_t len, uint64_t need, bool host) {
   int best = -1;
   for (int i = 0; i < static_cast<int>(n->cache.size()); ++i) {
     Slot* s = n->cache[static_cast<size_t>(i)];
+    if (s->host != host) continue;
     if (s->cap >= len && (best < 0 || s->cap < n->cache[static_cast<size_t>(best)]->cap)) {
       best = i;
       if (s->cap == need) break;  // an exact fit: no later slot fits better
@@ -1116,7 +1126,7 @@ int best_fit(dora_node* n, uint64_t len, uint64_t need) {
 }
 
 int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
-  const int best = best_fit(n, len, slot_bytes(len));
+  const int best = best_fit(n, len, slot_bytes(len), false);
   if (best >= 0) {
     Slot* s = n->cache[static_cast<size_t>(best)];
     n->cache.erase(n->cache.begin() + best);
@@ -1173,7 +1183,7 @@ int allocate_slot(dora_node* n, uint64_t len, Slot** out) {  // mod.rs:321-346
 int allocate_host_slot(dora_node* n, uint64_t len, Slot** out) {
   constexpr uint64_t kPage = 4096;
   const uint64_t need = (std::max<uint64_t>(len, 1) + kPage - 1) / kPage * kPage;
-  const int best = best_fit(n, len, need);
+  const int best = best_fit(n, len, need, true);
   if (best >= 0) {
     *out = n->cache[static_cast<size_t>(best)];
     n->cache.erase(n->cache.begin() + best);
@@ -1985,6 +1995,66 @@ int alloc_sample(dora_node* n, uint64_t len, dora_sample** out, uint64_t ext_len
   return DORA_OK;
 }
 
+// Device-resident samples up to this size for an output whose receivers all lack a GPU are
+// packed by the GPU straight into a shared-memory region (host_bound_sample): one dispatch on
+// the sender's warm queues instead of a slot in HBM that each receiver copies out with a HIP copy
+// of its own (stage_to_host, ~13 us of runtime overhead at any small size).  Larger samples keep
+// that path: the copy engines move them at the box's DMA rate and leave the CUs free, where a
+// pack writing over PCIe would hold its workgroups for the whole transfer.
+constexpr uint64_t kHostPackMax = 1ull << 20;
+
+// A sample for such an output: a shared-memory slot of this node (the reference's
+// DataMessage::SharedMemory, which its receivers map), page-locked and mapped for the GPU once,
+// with a fill flag for the pack to signal.  Null, with no error, when one cannot be made (no
+// free fill flag, registration refused): the caller takes an HBM slot.
+dora_sample* host_bound_sample(dora_node* n, uint64_t len, uint64_t ext_len) {
+  NodeCore* c = n->core.get();
+  if (!c->region_dev || !c->fill_done) return nullptr;
+  handle_finished_drop_tokens(n);
+  const uint64_t t0 = mono_ns();
+  while (n->sent_out.size() >= max_in_flight(len) && mono_ns() - t0 < kSlotWaitNs) {
+    c->drops.wait(1000);
+    handle_finished_drop_tokens(n);
+    if (c->region->hdr()->nodes[c->idx].state.load() == 2) break;
+  }
+  Slot* slot = nullptr;
+  const uint64_t ext = std::max(len, ext_len);
+  if (allocate_host_slot(n, ext, &slot) != DORA_OK) {
+    clear_error();
+    return nullptr;
+  }
+  if (!slot->registered) {
+    DeviceScope ds(c->device);
+    void* dp = nullptr;
+    if (hipHostRegister(slot->ptr, slot->cap, hipHostRegisterMapped | hipHostRegisterPortable) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      release_slot_memory(slot);
+      return nullptr;
+    }
+    slot->registered = true;
+    // the pack writes through the host address (one address space for host and GPU)
+    if (hipHostGetDevicePointer(&dp, slot->ptr, 0) != hipSuccess || dp != slot->ptr) {
+      (void)hipGetLastError();
+      release_slot_memory(slot);
+      return nullptr;
+    }
+  }
+  if (slot->flag < 0) {
+    if (c->free_flags.empty()) {
+      add_to_cache(n, slot);
+      return nullptr;
+    }
+    slot->flag = static_cast<int>(c->free_flags.back());
+    c->free_flags.pop_back();
+  }
+  auto* s = new dora_sample();
+  s->len = len;
+  s->ext_len = ext;
+  s->slot = slot;
+  return s;
+}
+
 // An unsent sample back to the node: its slot to the cache (an inline Vec is just freed).
 void discard_sample(dora_node* n, dora_sample* s) {
   if (!s) return;
@@ -2104,7 +2174,8 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
       }
       s->slot->region_cp_area = area;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
-                   n->region_armed, slot_bytes(s->slot->cap), stamps, sync) == DORA_OK) {
+                   n->region_armed, s->slot->host ? s->slot->cap : slot_bytes(s->slot->cap),
+                   stamps, sync) == DORA_OK) {
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -2121,7 +2192,8 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
   ++n->hip_packs;
   bool signalled = false;
   int rc = launch_pack(segs, nseg, dev, static_cast<uint8_t*>(s->slot->ptr), st, t_start,
-                       t_stop, sp, &signalled, slot_bytes(s->slot->cap));
+                       t_stop, sp, &signalled,
+                       s->slot->host ? s->slot->cap : slot_bytes(s->slot->cap));
   if (rc != DORA_OK) return rc;
   if (signalled) {
     s->epoch = sig.epoch;
@@ -2370,11 +2442,19 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   const uint64_t t0 = mono_ns();
   // a host-resident array below the zero-copy threshold goes inline, as in the reference
   const bool host_src = plan->dev != ARROW_DEVICE_ROCM;
-  int rc = alloc_sample(n, plan->size, &s, plan->fill_size(), host_src);
+  // a device array for receivers that all lack a GPU: packed into shared memory
+  // (host_bound_sample; not inside a timed region, whose stamps live in HBM slots' flags, and
+  // not a plan whose validity bitmaps travel in a tail past the sample: a SharedMemory message
+  // has no room to name one)
+  if (!host_src && plan->size && plan->fill_size() == plan->size && plan->size <= kHostPackMax &&
+      !n->host_bound.empty() &&
+      !n->region_armed && n->host_bound.count(output_id) && !n->bcast_out.count(output_id))
+    s = host_bound_sample(n, plan->size, plan->size);
+  int rc = s ? DORA_OK : alloc_sample(n, plan->size, &s, plan->fill_size(), host_src);
   if (rc != DORA_OK) return rc;
   const uint64_t t1 = mono_ns();
   uint64_t t2 = t1, t3 = t1;
-  if (plan->size && (!s->slot || s->slot->host)) {
+  if (plan->size && (!s->slot || (s->slot->host && !s->slot->registered))) {
     // an inline Vec or a host-only node's shared-memory slot: the host copies the buffers
     // (copy_array_into_sample, arrow_utils.rs:48)
     if (!host_src) {
@@ -2423,6 +2503,21 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     if (n->region_armed && plan->dev != ARROW_DEVICE_CPU) {
       if (s->stamped) s->slot->region_epoch = s->epoch;
       else ++n->region_unstamped;
+    }
+    if (s->slot->host) {
+      // packed into shared memory: its receivers read it on the host when it arrives (the
+      // reference's SharedMemory sample is complete when sent), so the pack completes first
+      SourceWait w;
+      w.kind = s->fill;
+      w.epoch = s->epoch;
+      if (s->fill == FILL_FLAG) w.flag = n->core->flag_host(s->slot->flag);
+      rc = wait_source_read(n, w);
+      if (rc != DORA_OK) {
+        delete s;  // a pack that may still write the region: its slot is not reused
+        return rc;
+      }
+      s->fill = FILL_DONE;
+      ++n->host_packs;
     }
     t2 = t3 = mono_ns();
   }
@@ -2578,7 +2673,14 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     uint32_t kind;
     std::vector<uint8_t> p;
     if (core->ev.try_pop(&kind, &p)) {
-      if (kind == dora::EV_READY) break;
+      if (kind == dora::EV_READY) {
+        // the outputs whose receivers all lack a GPU (daemon.cpp ready_payload)
+        if (device >= 0 && p.size() >= 4) {
+          dora::RBuf r(p);
+          for (uint32_t k = r.u32(); k > 0; --k) n->host_bound.insert(r.str());
+        }
+        break;
+      }
       dora::encode_event(n, kind, p);
       continue;
     }
@@ -3112,9 +3214,10 @@ int dora_node_fill_paths(dora_node* n, uint64_t* aql_packs, uint64_t* hip_packs)
 }
 
 int dora_node_host_paths(dora_node* n, uint64_t* bar_fills, uint64_t* staged,
-                         uint64_t* staged_bytes) {
+                         uint64_t* staged_bytes, uint64_t* host_packs) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (bar_fills) *bar_fills = n->bar_fills;
+  if (host_packs) *host_packs = n->host_packs;
   if (staged) *staged = n->core->host_staged.load();
   if (staged_bytes) *staged_bytes = n->core->host_staged_bytes.load();
   return DORA_OK;

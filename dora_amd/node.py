@@ -391,11 +391,13 @@ class Node:
         return {"aql": a.value, "hip": h.value}
 
     def host_paths(self) -> dict:
-        """Host sources written into their slot by the CPU through the BAR, and device samples
-        this node (without a GPU) staged to host memory (dora_node_host_paths)."""
-        a, b, c = c_uint64(), c_uint64(), c_uint64()
-        call("dora_node_host_paths", self.handle, byref(a), byref(b), byref(c))
-        return {"bar_fills": a.value, "staged": b.value, "staged_bytes": c.value}
+        """Host sources written into their slot by the CPU through the BAR, device samples this
+        node (without a GPU) staged to host memory, and device samples this node packed straight
+        into shared memory for receivers that all lack a GPU (dora_node_host_paths)."""
+        a, b, c, d = c_uint64(), c_uint64(), c_uint64(), c_uint64()
+        call("dora_node_host_paths", self.handle, byref(a), byref(b), byref(c), byref(d))
+        return {"bar_fills": a.value, "staged": b.value, "staged_bytes": c.value,
+                "host_packs": d.value}
 
     def set_timing_period(self, period: int):
         """Stamp every `period`-th pack launch (0: the default, every 8th)."""

@@ -2,8 +2,10 @@
 
 * A receiver without a GPU (DORA_GPU_DEVICE < 0) gets the reference's host ArrowData from a
   device producer (apis/rust/node/src/event_stream/event.rs:35-91; Python: a pyarrow array,
-  apis/python/operator/src/lib.rs:135-144): the sample is staged into pinned host memory on
-  receipt and the producer's token goes back at once.
+  apis/python/operator/src/lib.rs:135-144).  When every receiver of the output lacks a GPU, a
+  sample <= 1 MiB is packed by the producer straight into shared memory and sent as the
+  reference's DataMessage::SharedMemory; otherwise (larger, or a device receiver too) it is
+  staged into pinned host memory on receipt and the producer's token goes back at once.
 * Host-resident sources >= 4096 B from a device node (the reference benchmark's payloads,
   examples/benchmark/node/src/main.rs:38-70 via send_output_raw, mod.rs:180-215): up to 2 MiB the
   CPU writes the slot through the large BAR (no GPU dispatch), above that HIP DMAs them; both
@@ -117,8 +119,10 @@ def test_device_producer_to_host_only_python_receiver(launcher):
             _settle(tx, rx)
             created.append(tx.stats()["slots_created"])
         assert created[1] == created[0], created  # tokens came back: every slot was reused
-        hp = rx.host_paths()
-        assert hp["staged"] >= 2 * len(sizes), hp
+        # the output's only receiver lacks a GPU: samples <= 1 MiB were packed by the producer
+        # straight into shared memory, larger ones staged by the receiver's copy engines
+        assert tx.host_paths()["host_packs"] >= 2 * 3, tx.host_paths()
+        assert rx.host_paths()["staged"] >= 2 * 2, rx.host_paths()
         # the edge's latency (device 4 KB -> host receiver, one process), for the record
         lat = []
         for k in range(200):
@@ -141,36 +145,49 @@ def test_device_producer_to_host_only_python_receiver(launcher):
 
 def test_host_only_receiver_staging_stress(launcher):
     """600 device messages of 8 B .. 1 MiB, each with new bytes (the source is rewritten after
-    every synchronous send), reach a receiver without a GPU byte for byte, each staged by the
-    copy engines into a recycled pinned buffer (a stale or reused buffer would show)."""
+    every synchronous send), reach a receiver without a GPU byte for byte over both host paths:
+    output `x`, whose only receiver lacks a GPU, is packed by the producer straight into recycled
+    shared-memory regions; output `y` also feeds a device receiver, so its sample stays in HBM and
+    the host receiver stages it with the copy engines into a recycled pinned buffer (a stale or
+    reused region or buffer would show)."""
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.device import DeviceBuffer
-    from oracle.checksum_ref import splitmix_bytes
+    from oracle.checksum_ref import csum64, splitmix_bytes
     desc = {"nodes": [
-        {"id": "src", "path": "dynamic", "outputs": ["x"]},
-        {"id": "dst", "path": "dynamic", "inputs": {"x": {"source": "src/x", "queue_size": 10}},
+        {"id": "src", "path": "dynamic", "outputs": ["x", "y"]},
+        {"id": "dst", "path": "dynamic",
+         "inputs": {"x": {"source": "src/x", "queue_size": 10},
+                    "y": {"source": "src/y", "queue_size": 10}},
          "_unstable_deploy": {"gpu": -1}},
+        {"id": "gpu", "path": "dynamic", "inputs": {"y": {"source": "src/y", "queue_size": 10}}},
     ]}
     sizes = [8, 100, 4096, 4097, 65539, (1 << 20) - 1, 1 << 20]
     s = device.Stream()
     buf = DeviceBuffer(1 << 20)
     with Dataflow(desc, launcher=launcher) as df:
-        n = _nodes(df, {"src": 0, "dst": -1})
-        tx, rx = n["src"], n["dst"]
+        n = _nodes(df, {"src": 0, "dst": -1, "gpu": 0})
+        tx, rx, gx = n["src"], n["dst"], n["gpu"]
         for k in range(600):
             z = sizes[k % len(sizes)]
+            out = "x" if k % 2 == 0 else "y"
             device.fill_splitmix(buf.ptr, z, 0xABC000 + k, s)
             s.sync()
-            tx.send_output_device_bytes("x", buf.ptr, z, {"k": k})
+            tx.send_output_device_bytes(out, buf.ptr, z, {"k": k})
+            want = splitmix_bytes(z, 0xABC000 + k)
             ev = rx.next(timeout=60)
-            assert ev["metadata"] == {"k": k} and not ev["on_device"]
-            assert ctypes.string_at(ev["data_ptr"], z) == splitmix_bytes(z, 0xABC000 + k), (k, z)
+            assert ev["id"] == out and ev["metadata"] == {"k": k} and not ev["on_device"]
+            assert ctypes.string_at(ev["data_ptr"], z) == want, (k, z, out)
             del ev
-        hp = rx.host_paths()
-        assert hp["staged"] >= 600, hp
+            if out == "y":
+                ev = gx.next(timeout=60)
+                assert ev["on_device"] and device.csum64(ev["data_ptr"], z, s) == csum64(want)
+                del ev
+        assert tx.host_paths()["host_packs"] >= 300, tx.host_paths()
+        assert rx.host_paths()["staged"] >= 300, rx.host_paths()
         tx.close()
         rx.close()
+        gx.close()
         df.wait(30)
     buf.free()
     s.close()
