@@ -42,6 +42,10 @@ def test_keep_awake_beats_while_sending_then_parks(tmp_path):
         with Dataflow(desc) as df:
             node = Node("node", dataflow=df.shm, device=0)
             buf = device.DeviceBuffer(4096)
+            # the thread is the process's: quick sends first, whatever earlier tests sent
+            for k in range(5):
+                node.send_output_device_bytes("latency", buf.ptr, 4096, {"seq": 100 + k})
+                time.sleep(0.001)
             node.send_output_device_bytes("latency", buf.ptr, 4096, {"seq": 0})
             b0, _ = _stats()
             time.sleep(0.03)
