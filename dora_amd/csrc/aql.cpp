@@ -85,6 +85,7 @@ struct Pending {
   bool profile = false;
   bool cp = false;  // signalled by the command processor (aql_cp_candidate)
   bool lone = false;  // runs alone on the GPU (a synchronous send, or every queue idle)
+  bool read = false;  // read-signalled (dora_aql_pack1r_u4): a synchronous send returns on its read word
   uint64_t* cp_stamps = nullptr;  // CP-signalled: the timed region's stamp area (device), or none
 };
 
@@ -93,16 +94,18 @@ struct Pending {
 constexpr int kMaxQueues = 8;
 
 // The kernels of the embedded code object, in AqlQueue::kobj order.
-constexpr int kKernels = 5;
+constexpr int kKernels = 6;
 constexpr int kMultiKernel = 0;   // multi-segment packs (nested arrays)
 constexpr int kOneKernel = 1;     // single-segment packs behind the acquire fence
 constexpr int kOneCohKernel = 2;  // single-segment packs with agent-coherent loads, no fence
 constexpr int kBatchKernel = 3;
 constexpr int kReduceKernel = 4;
+constexpr int kReadKernel = 5;    // read-signalled synchronous packs (aql_kernels.hip)
 constexpr uint32_t kReduceArgsBytes = 32;  // base, areas, out, n, area_words
+constexpr uint32_t kReadArgsBytes = 64;    // dst, src, len, rflag, done, epoch, stamps, grid, per
 constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4", "dora_aql_pack1_u4",
                                                 "dora_aql_pack1c_u4", "dora_aql_packb_u4",
-                                                "dora_aql_stamp_reduce"};
+                                                "dora_aql_stamp_reduce", "dora_aql_pack1r_u4"};
 
 // Dispatch policy (every figure below was measured against the alternative
 // on MI355X, the alternatives are not built any more):
@@ -356,6 +359,7 @@ AqlQueue* create(int device) {
         ka != (k == kMultiKernel    ? aql_args_size()
                : k == kBatchKernel  ? aql_batch_args_size()
                : k == kReduceKernel ? size_t(kReduceArgsBytes)
+               : k == kReadKernel   ? size_t(kReadArgsBytes)
                                     : size_t(kArgs1Bytes)) ||
         ka > kSlotBytes) {
       delete a;
@@ -549,6 +553,16 @@ namespace {
 // copies saturate HBM: 12.9-13.0 us per pack on three queues vs 13.2 on four,
 // profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
 // the 20-cloud burst, profiles/r04_full_ab.jsonl).
+// Read-signalled packs (dora_aql_pack1r_u4): <= 12 units of 16 B per lane (aql_kernels.hip
+// kReadUnits), <= kMaxSignalWgs workgroups (their done words), so up to 192 MiB; 1024
+// workgroups unless that holds too little.
+constexpr uint64_t kReadLaneUnits = 12;
+constexpr uint64_t kReadMaxUnits = uint64_t(kMaxSignalWgs) * 256 * kReadLaneUnits;
+uint32_t read_grid(uint64_t units) {
+  const uint64_t need = (units + 256 * kReadLaneUnits - 1) / (256 * kReadLaneUnits);
+  const uint64_t fill = std::min<uint64_t>(1024, (units + 255) / 256);
+  return static_cast<uint32_t>(std::max<uint64_t>(std::max(need, fill), 1));
+}
 int big_queues(int nq, uint64_t bytes) {
   return std::min(nq, bytes >= (uint64_t(32) << 20) ? 3 : 4);
 }
@@ -604,7 +618,22 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // completion signal is the flag's CpSignal line (shm.h FillFlag)
   const bool cp = !batch && it0.cp && it0.flag_host;
   int rc;
-  if (batch) {
+  if (it0.read) {
+    // dst, src, len, the flag line's read word, done words, epoch, stamp area, grid, units per
+    // workgroup (read_grid)
+    const uint64_t units = segs[0].len >> 4;
+    grid = read_grid(units);
+    const uint32_t per = static_cast<uint32_t>((units + grid - 1) / grid);
+    const uint64_t w[7] = {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(segs[0].src),
+                           segs[0].len,
+                           reinterpret_cast<uintptr_t>(sig.flag) + offsetof(FillFlag, read_epoch),
+                           reinterpret_cast<uintptr_t>(sig.done), sig.epoch,
+                           reinterpret_cast<uintptr_t>(it0.cp_stamps)};
+    std::memcpy(args, w, sizeof(w));
+    std::memcpy(args + 56, &grid, 4);
+    std::memcpy(args + 60, &per, 4);
+    rc = DORA_OK;
+  } else if (batch) {
     BatchItem bi[kBatchMsgs];
     for (size_t m = 0; m < n; ++m)
       bi[m] = {items[m].segs, items[m].n, items[m].dst, items[m].sig, items[m].dst_cap};
@@ -647,14 +676,17 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // host memory over PCIe — 0.6-0.7 us less from doorbell to completion at any size
   // (aql_pipeline_bench modes 5 vs 7, profiles/r04_lone_dispatch_ab.jsonl).  Pipelined packs keep
   // the host ring: no HDP flush per send.
-  const bool dev_args1 = one && it0.lone;
+  const bool dev_args1 = (one && it0.lone) || it0.read;
   if (one && !dev_args1) {
     // coherent host memory: ordered before the packet header's release store (x86 TSO)
     slot = a->hring + r * kHostSlotBytes;
     std::memcpy(slot, args, kArgs1Bytes);
   } else {
     slot = a->ring + r * kSlotBytes;
-    std::memcpy(slot, args, one ? kArgs1Bytes : batch ? aql_batch_args_size() : aql_args_size());
+    std::memcpy(slot, args, it0.read ? kReadArgsBytes
+                            : one    ? kArgs1Bytes
+                            : batch  ? aql_batch_args_size()
+                                     : aql_args_size());
     // write-combined stores leave the CPU, the HDP flush makes them visible to the GPU; both
     // are posted writes ordered before the doorbell
     __builtin_ia32_sfence();
@@ -693,8 +725,11 @@ int dispatch_locked(AqlQueue* a, size_t qi, const Pending* items, size_t n, bool
   // ever read stale, test_gpu_fence.py rewrites the source between > 512 such packs).  Their
   // arguments come preloaded into SGPRs, or from the device ring behind the HDP flush (lone).
   // Pipelined packs outside the window and multi-segment packs keep the fence.
-  const bool coh = one && ((cp && it0.bytes < kCpHi) || it0.lone);
-  const int k = batch ? kBatchKernel : one ? (coh ? kOneCohKernel : kOneKernel) : kMultiKernel;
+  const bool coh = it0.read || (one && ((cp && it0.bytes < kCpHi) || it0.lone));
+  const int k = it0.read ? kReadKernel
+                : batch  ? kBatchKernel
+                : one    ? (coh ? kOneCohKernel : kOneKernel)
+                         : kMultiKernel;
   p->workgroup_size_x = 256;
   p->workgroup_size_y = 1;
   p->workgroup_size_z = 1;
@@ -986,7 +1021,8 @@ void dispatcher_main(AqlQueue* a) {
 
 int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap,
-             uint64_t* cp_stamps, bool sync) {
+             uint64_t* cp_stamps, bool sync, bool* read_signalled) {
+  if (read_signalled) *read_signalled = false;
   if (!a || a->failed.load()) return fail(DORA_ERR_HIP, "AQL queue unavailable");
   if (n == 0 || n > kMaxItemSegs) return fail(DORA_ERR_INVALID, "AQL pack: %zu segments", n);
   SubSpan sp_all(SP_AQL_PACK);
@@ -1012,6 +1048,13 @@ int aql_pack(AqlQueue* a, const Segment* segs, size_t n, uint8_t* dst, const Fil
   // one skips the idle check, which loads a GPU-written flag line per queue)
   p.lone = sync || (n == 1 && segs[0].dst_off == 0 && queues_idle(a));
   p.cp = (!profile || cp_stamps) && flag_host && aql_cp_candidate(segs, n, sync);
+  // a synchronous CP-signalled single-segment pack of aligned bytes up to what its workgroups
+  // hold in VGPRs: read-signalled (dora_aql_pack1r_u4)
+  p.read = sync && p.cp && n == 1 && segs[0].op == SEG_COPY &&
+           segs[0].dst_off == 0 && sig.done && sig.flag && p.bytes >= kCpLo &&
+           (p.bytes >> 4) <= kReadMaxUnits &&
+           ((reinterpret_cast<uintptr_t>(segs[0].src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  if (read_signalled) *read_signalled = p.read;
   // HBM-bound packs (>= kBarrierBytes) run in order per queue (barrier bit) over at most three
   // (four below 32 MiB) queues, big_queues: more concurrent 40 MB copies only contend (14.1-14.5
   // us per pack without the barrier, 12.9-13.0 with it; profiles/r02_aql_big_ab.jsonl).

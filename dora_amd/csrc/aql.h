@@ -42,10 +42,13 @@ bool aql_usable(const AqlQueue* q);
 // every queue idle, runs alone on the GPU: its arguments go to the device ring and it reads
 // without the acquire fence; a synchronous one is also signalled by the command processor at any
 // size >= 1 MiB, with a grid of up to 3584 workgroups (no done words to poll, so no
-// 1024-workgroup signalling cap).
+// 1024-workgroup signalling cap).  A synchronous one of 1-256 MiB of 16-byte-aligned bytes is
+// read-signalled (*read_signalled): the pack raises the flag line's read word (FillFlag
+// read_epoch) once every source byte is in its workgroups' registers, before its stores drain,
+// and the caller may return then.
 int aql_pack(AqlQueue* q, const Segment* segs, size_t n, uint8_t* dst, const FillSignal& sig,
              const std::atomic<uint64_t>* flag_host, bool profile, uint64_t dst_cap = 0,
-             uint64_t* cp_stamps = nullptr, bool sync = false);
+             uint64_t* cp_stamps = nullptr, bool sync = false, bool* read_signalled = nullptr);
 // Would a pack of these segments be signalled by the command processor: [1 MiB, 32 MiB), or
 // (`lone`: a synchronous send) a single-segment pack of any size from 1 MiB.
 bool aql_cp_candidate(const Segment* segs, size_t n, bool lone = false);

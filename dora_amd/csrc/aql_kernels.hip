@@ -62,6 +62,97 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
   pack1<4, dora::pack::kCoherent>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
 
+// Read-signalled single-segment pack (aql.cpp: a synchronous send of 1-256 MiB, source and slot
+// 16-byte aligned).  The reference's send_output returns once its source has been copied; a pack
+// that loads and stores chunk by chunk has read its last source byte only about when it has
+// written its last sample byte, so a synchronous send waited for the whole pack plus the host
+// round trip (0.47 of HBM per 40.96 MB message).  Here every workgroup first loads
+// its whole share of the source into VGPRs (<= kReadUnits 16-B units per lane), publishes that in
+// its done word once all its loads have returned, and only then stores; workgroup 0 waits for
+// every done word and raises the flag line's read word — the send returns there, and the next
+// send's loads overlap this pack's stores.  The fill itself is the dispatch's completion signal
+// (every wave waits for its own stores), as for the other lone packs; stamps as pack_body's CP
+// branch.
+constexpr int kReadUnits = 12;  // aql.cpp kReadLaneUnits
+extern "C" __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8)))
+void dora_aql_pack1r_u4(
+    uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* rflag, uint32_t* done,
+    uint64_t epoch, uint64_t* stamps, uint32_t grid, uint32_t per) {
+  using namespace dora;
+  using namespace dora::pack;
+  const uint32_t blk = __builtin_amdgcn_workgroup_id_x(), t = threadIdx.x;
+  const uint64_t t_start = blk == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+  // lane t holds units u0 + t + 256 k, k < nk: one VGPR offset, the stride in SGPR offsets
+  // (few VGPRs, so every workgroup of the grid is resident at once)
+  const uint32_t units = static_cast<uint32_t>(len >> 4);
+  const uint32_t u0 = blk * per;
+  const uint32_t u1 = u0 + per < units ? u0 + per : units;
+  const uint32_t mine = u0 + t < u1 ? (u1 - u0 - t + kThreads - 1) / kThreads : 0;
+  const uint32_t off = 16 * (u0 + t);
+  const __amdgpu_buffer_rsrc_t rs = src_rsrc(src), rd = src_rsrc(dst);
+  u32x4 v[kReadUnits];
+#pragma unroll
+  for (int k = 0; k < kReadUnits; ++k)
+    if (uint32_t(k) < mine)
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * kThreads * k, kCoherentPolicy);
+  const uint32_t tail = static_cast<uint32_t>(len & 15);
+  const bool tail_lane = blk == grid - 1 && t < tail;
+  uint8_t tb = 0;
+  if (tail_lane) tb = ld1<kCoherent>(src + 16 * uint64_t(units) + t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every load of this workgroup has returned
+  __syncthreads();
+  const uint32_t e = static_cast<uint32_t>(epoch);
+  if (t == 0) __hip_atomic_store(done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blk == 0) {
+    // as signal_fill: every done word at once per round, bounded (a lost workgroup leaves the
+    // read word unset; the send then waits for the fill instead)
+    constexpr int kPer = kMaxSignalWgs / kThreads;
+    __shared__ uint32_t missing;
+    for (uint32_t round = 0; round < (1u << 22); ++round) {
+      if (t == 0) missing = 0;
+      __syncthreads();
+      // four loads in flight per lane at a time: this workgroup's source bytes stay in VGPRs
+      // meanwhile, and few registers keep every workgroup of the grid resident
+      bool all_mine = true;
+#pragma unroll 1
+      for (int k0 = 0; k0 < kPer; k0 += 4) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t i = t + (k0 + j) * kThreads;
+          w[j] = i < grid ? __hip_atomic_load(done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : e;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) all_mine &= w[j] == e;
+      }
+      if (!all_mine) missing = 1;
+      __syncthreads();
+      const bool all = missing == 0;
+      __syncthreads();
+      if (all) {
+        if (t == 0) __hip_atomic_store(rflag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  // write-through to device scope, as st16<kCoherent> (sc1 nt)
+#pragma unroll
+  for (int k = 0; k < kReadUnits; ++k)
+    if (uint32_t(k) < mine)
+      __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, off, 16 * kThreads * k, kCoherentPolicy);
+  if (tail_lane) st1<kCoherent>(dst + 16 * uint64_t(units) + t, tb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fill: complete before the waves end
+  if (stamps) {
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_fetch_max(stamps + 1 + (blk % kCpStampWgs), __builtin_amdgcn_s_memrealtime(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (blk == 0) __hip_atomic_store(stamps, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // Region-end reduction of CP-signalled packs' stamp areas (aql.cpp aql_stamp_reduce, node.cpp
 // dora_node_region_end): workgroup i reads area `areas[i]` of `base` (area_words words: [0] the
 // first workgroup's start, then the end stamps of pack_body's CP branch) and writes (start,

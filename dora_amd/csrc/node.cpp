@@ -761,6 +761,7 @@ struct dora_sample {
   uint8_t fill = dora::FILL_DONE;  // how the receiver learns the fill completed
   uint64_t epoch = 0;
   bool stamped = false;  // the pack kernel stamps its start / signal time into the flag line
+  bool read_signalled = false;  // its pack raises the flag line's read word (aql.h aql_pack)
 };
 
 namespace dora {
@@ -852,7 +853,9 @@ struct dora_node {
   // outputs whose every receiver has no GPU (the daemon's AllNodesReady): device sources up to
   // kHostPackMax are packed straight into shared memory for them (host_bound_sample)
   std::set<std::string, std::less<>> host_bound;
-  uint64_t host_packs = 0;
+  // samples put straight into shared memory for such outputs: device arrays packed there by the
+  // GPU (host_bound_sample), host sources copied there by the CPU
+  uint64_t host_packs = 0, host_copies = 0;
   bool aql_ready = false;  // the process's AQL queues were set up (first non-empty sample)
   hipEvent_t region_start = nullptr;
   std::vector<hipEvent_t> region_stop;
@@ -2173,9 +2176,11 @@ int fill_sample(dora_node* n, dora_sample* s, const Segment* segs, size_t nseg,
         stamps = n->region_cp_stamps + size_t(area) * kCpAreaWords;
       }
       s->slot->region_cp_area = area;
+      bool read = false;
       if (aql_pack(q, segs, nseg, static_cast<uint8_t*>(s->slot->ptr), sig, fh,
                    n->region_armed, s->slot->host ? s->slot->cap : slot_bytes(s->slot->cap),
-                   stamps, sync) == DORA_OK) {
+                   stamps, sync, &read) == DORA_OK) {
+        s->read_signalled = read;
         n->core->note_aql_fill(fh, sig.epoch);
         if (n->region_armed) ++n->region_aql;
         ++n->aql_packs;
@@ -2360,6 +2365,7 @@ void form_bcast_groups(dora_node* n) {
 // What a synchronous send of a device source waits for: the pack has read the whole source.
 struct SourceWait {
   uint8_t kind = FILL_DONE;  // FILL_FLAG: flag >= epoch; FILL_EVENT: event; FILL_BCAST: stream
+  bool read = false;  // FILL_FLAG of a read-signalled pack: its read word >= epoch suffices
   hipStream_t stream = nullptr;  // FILL_BCAST: the output's broadcast stream
   const std::atomic<uint64_t>* flag = nullptr;
   uint64_t epoch = 0;
@@ -2375,7 +2381,9 @@ int wait_source_read(dora_node* n, const SourceWait& w) {
   if (w.kind == FILL_FLAG && w.flag) {
     const uint64_t t0 = mono_ns();
     uint32_t spins = 0;
-    while (!fill_reached(w.flag, w.epoch)) {
+    const auto* ff = reinterpret_cast<const FillFlag*>(w.flag);
+    while (!(w.read && ff->read_epoch.load(std::memory_order_acquire) >= w.epoch) &&
+           !fill_reached(w.flag, w.epoch)) {
       if (++spins < 4096) {
         __builtin_ia32_pause();
         continue;
@@ -2446,15 +2454,30 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
   // (host_bound_sample; not inside a timed region, whose stamps live in HBM slots' flags, and
   // not a plan whose validity bitmaps travel in a tail past the sample: a SharedMemory message
   // has no room to name one)
-  if (!host_src && plan->size && plan->fill_size() == plan->size && plan->size <= kHostPackMax &&
-      !n->host_bound.empty() &&
-      !n->region_armed && n->host_bound.count(output_id) && !n->bcast_out.count(output_id))
+  const bool host_bound = plan->size && plan->fill_size() == plan->size && !n->host_bound.empty() &&
+                          !n->region_armed && n->core->device >= 0 &&
+                          n->host_bound.count(output_id) && !n->bcast_out.count(output_id);
+  if (host_bound && !host_src && plan->size <= kHostPackMax) {
     s = host_bound_sample(n, plan->size, plan->size);
+  } else if (host_bound && host_src && plan->size >= kZeroCopyThreshold) {
+    // a host source for them: the CPU copies it into shared memory, as a node without a GPU
+    // does (the reference's copy_array_into_sample) — no HBM slot for each receiver to copy out
+    handle_finished_drop_tokens(n);
+    Slot* slot = nullptr;
+    if (allocate_host_slot(n, plan->size, &slot) == DORA_OK) {
+      s = new dora_sample();
+      s->len = plan->size;
+      s->slot = slot;
+      ++n->host_copies;
+    } else {
+      clear_error();
+    }
+  }
   int rc = s ? DORA_OK : alloc_sample(n, plan->size, &s, plan->fill_size(), host_src);
   if (rc != DORA_OK) return rc;
   const uint64_t t1 = mono_ns();
   uint64_t t2 = t1, t3 = t1;
-  if (plan->size && (!s->slot || (s->slot->host && !s->slot->registered))) {
+  if (plan->size && (!s->slot || (s->slot->host && (host_src || !s->slot->registered)))) {
     // an inline Vec or a host-only node's shared-memory slot: the host copies the buffers
     // (copy_array_into_sample, arrow_utils.rs:48)
     if (!host_src) {
@@ -2538,6 +2561,7 @@ int pack_and_send(dora_node* n, const char* output_id, const dora_plan* plan, co
     wait.kind = bo != n->bcast_out.end() ? uint8_t(FILL_BCAST) : s->fill;
     if (bo != n->bcast_out.end()) wait.stream = bo->second.stream;
     wait.epoch = s->epoch;
+    wait.read = s->read_signalled;
     if (s->fill == FILL_FLAG) wait.flag = n->core->flag_host(s->slot->flag);
     if (s->fill == FILL_EVENT) wait.event = s->slot->done;
   }
@@ -3217,7 +3241,7 @@ int dora_node_host_paths(dora_node* n, uint64_t* bar_fills, uint64_t* staged,
                          uint64_t* staged_bytes, uint64_t* host_packs) {
   if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
   if (bar_fills) *bar_fills = n->bar_fills;
-  if (host_packs) *host_packs = n->host_packs;
+  if (host_packs) *host_packs = n->host_packs + n->host_copies;
   if (staged) *staged = n->core->host_staged.load();
   if (staged_bytes) *staged_bytes = n->core->host_staged_bytes.load();
   return DORA_OK;

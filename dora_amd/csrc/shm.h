@@ -66,7 +66,10 @@ struct FillFlag {
   alignas(64) std::atomic<uint64_t> epoch;
   uint64_t t_start, t_end;
   std::atomic<uint64_t> cp_epoch;  // epoch of the CP-signalled fill `cp` reports
-  uint64_t pad_[4];
+  // the latest fill whose every source byte has been read (a read-signalled pack, aql.h): its
+  // synchronous send may return while the pack's stores drain
+  std::atomic<uint64_t> read_epoch;
+  uint64_t pad_[3];
   CpSignal cp;
 };
 static_assert(offsetof(FillFlag, cp) == 64 && sizeof(FillFlag) == 128, "FillFlag layout");

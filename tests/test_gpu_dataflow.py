@@ -866,20 +866,25 @@ def test_rewritten_source_each_send_bit_exact(launcher, tmp_path, writer, size):
     assert paths["aql"] >= n_msgs, paths
 
 
-@pytest.mark.parametrize("mode", ["sync", "async"])
-def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_path, mode):
+@pytest.mark.parametrize("mode,size,n_msgs", [("sync", 1 << 20, 200), ("async", 1 << 20, 200),
+                                               ("sync", (3 << 20) + 5, 100),
+                                               ("sync", 40960000, 60)])
+def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_path, mode, size,
+                                                                n_msgs):
     """The reference copies inside send_output (arrow_utils.rs:48, node/mod.rs:206-209): the
     caller may rewrite its buffer as soon as the call returns.  Here the source is rewritten by
     a kernel on a stream the library knows nothing about, right after every send returns, with
-    no synchronisation.  The default (synchronous) send must deliver every sample bit-exact;
-    DORA_SEND_ASYNC makes no such promise (its contract: rewrite only via dora_node_stream or
-    after dora_node_sync), and its count of corrupted samples is only reported."""
+    no synchronisation.  The default (synchronous) send must deliver every sample bit-exact —
+    it returns when its read-signalled pack has every source byte in registers, while the
+    stores still drain (aql_kernels.hip dora_aql_pack1r_u4; 1 MiB, a ragged 3 MiB + 5 B and the
+    40.96 MB headline size); DORA_SEND_ASYNC makes no such promise (its contract: rewrite only
+    via dora_node_stream or after dora_node_sync), and its count of corrupted samples is only
+    reported."""
     from dora_amd import device
     from dora_amd.dataflow import Dataflow
     from dora_amd.node import Node
     from dora_amd.verify import to_i64
     res = str(tmp_path / "sink.json")
-    n_msgs, size = 200, 1 << 20
     s = device.Stream()
     scratch = device.DeviceBuffer(size)
     sums = []
@@ -893,6 +898,7 @@ def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_pa
     other.sync()
     with Dataflow(_bench_desc(res), launcher=launcher) as df:
         node = Node("node", dataflow=df.shm, device=0)
+        read0 = device.aql_dispatch_counts(0).get("dora_aql_pack1r_u4", 0)
         for k in range(n_msgs):
             # the rewrite launched after the previous send has finished before this send: a
             # source must be complete when it is sent (only what follows a send is under test)
@@ -902,6 +908,7 @@ def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_pa
                                           asynchronous=mode == "async")
             device.fill_splitmix(src.ptr, size, 0xFACE00 + k + 1, other)  # no sync
         other.sync()
+        reads = device.aql_dispatch_counts(0).get("dora_aql_pack1r_u4", 0) - read0
         node.close()
         codes = df.wait(60)
         log = df.log("sink")
@@ -912,9 +919,11 @@ def test_device_source_rewritten_on_unrelated_stream_after_send(launcher, tmp_pa
     out = json.load(open(res))
     bad = sum(x["mismatches"] for x in out["series"])
     assert sum(x["verified"] for x in out["series"]) == n_msgs
-    print(f"{mode}: {bad} of {n_msgs} samples corrupted by the rewrite")
+    print(f"{mode} {size} B: {bad} of {n_msgs} samples corrupted by the rewrite; "
+          f"{reads} read-signalled packs")
     if mode == "sync":
         assert bad == 0, out
+        assert reads == n_msgs, reads
 
 
 def test_device_array_send_waits_for_its_source(launcher):

@@ -193,6 +193,38 @@ def test_host_only_receiver_staging_stress(launcher):
     s.close()
 
 
+def test_host_source_to_host_only_receiver_copied_into_shared_memory(launcher):
+    """A device node's host-resident bytes (>= 4096 B) on an output read only on the host are
+    copied by the CPU into shared memory, as a node without a GPU sends them (the reference's
+    copy_array_into_sample): no BAR write into an HBM slot, nothing staged at the receiver."""
+    from dora_amd.dataflow import Dataflow
+    from oracle.checksum_ref import splitmix_bytes
+    desc = {"nodes": [
+        {"id": "src", "path": "dynamic", "outputs": ["x"]},
+        {"id": "dst", "path": "dynamic", "inputs": {"x": {"source": "src/x", "queue_size": 10}},
+         "_unstable_deploy": {"gpu": -1}},
+    ]}
+    sizes = [100, 4096, 65539, 3 << 20]
+    with Dataflow(desc, launcher=launcher) as df:
+        n = _nodes(df, {"src": 0, "dst": -1})
+        tx, rx = n["src"], n["dst"]
+        t0, r0 = tx.host_paths(), rx.host_paths()
+        for k in range(40):
+            z = sizes[k % len(sizes)]
+            want = splitmix_bytes(z, 0x5EED00 + k)
+            tx.send_output("x", want, {"k": k})
+            ev = rx.next(timeout=60)
+            assert ev["metadata"] == {"k": k} and not ev["on_device"]
+            assert ctypes.string_at(ev["data_ptr"], ev["data_len"]) == want, (k, z)
+            del ev
+        t1, r1 = tx.host_paths(), rx.host_paths()
+        assert t1["host_packs"] - t0["host_packs"] == 30, t1  # the 30 sends >= 4096 B
+        assert t1["bar_fills"] == t0["bar_fills"] and r1["staged"] == r0["staged"], (t1, r1)
+        tx.close()
+        rx.close()
+        df.wait(30)
+
+
 def test_host_sources_bar_and_dma_paths_bit_exact(launcher):
     """Host bytes of 4096, 4097, 1 MiB + 3, 2 MiB, 2 MiB + 1 and 40.96 MB, and multi-buffer host
     pyarrow arrays (a 20k-point cloud on the BAR path, the 1M-point C3 cloud on the DMA path),
