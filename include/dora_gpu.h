@@ -379,9 +379,10 @@ int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_pac
  * device node wrote into its slot with the CPU through the large BAR (the reference's memcpy
  * into its shared-memory sample, arrow_utils.rs:48: no GPU dispatch), and device samples a node
  * without a GPU (DORA_GPU_DEVICE < 0) staged into host memory on receipt (count, bytes): such a
- * receiver gets the reference's host ArrowData (event.rs:35-91); and device samples <= 1 MiB this
- * node packed straight into shared memory because every receiver of the output lacks a GPU
- * (sent as the reference's DataMessage::SharedMemory).  Any pointer may be NULL. */
+ * receiver gets the reference's host ArrowData (event.rs:35-91); and samples this node put
+ * straight into shared memory because every receiver of the output lacks a GPU (sent as the
+ * reference's DataMessage::SharedMemory): device arrays <= 1 MiB packed there by the GPU, host
+ * sources >= 4096 B copied there by the CPU.  Any pointer may be NULL. */
 int dora_node_host_paths(dora_node* node, uint64_t* bar_fills, uint64_t* staged,
                          uint64_t* staged_bytes, uint64_t* host_packs);
 /* dora_node_send_output of device arrays keeps the plans of recent sends that read no array
