@@ -241,11 +241,11 @@ size_t max_in_flight(uint64_t len) {
 
 
 // Streams the HIP-launched fills of a node rotate over (host sources, compacting transforms,
-// relays; device-source packs go to the AQL queues, aql.h).  A pack ends in a drain tail (its
-// last workgroups, the fill signal) and starts with a ramp; on one stream consecutive fills
-// serialise those, on three hardware queues the next fill streams through them (r01 probe,
-// profiles/r01_stream_probe.jsonl: 40.96 MB 17.1 -> 13.2 us per message, 16 MB 9.8 -> 6.0).
-constexpr size_t kFillStreams = 3;
+// relays; device-source packs go to the AQL queues, aql.h).  Three (r01: HIP-launched device
+// packs overlapped their ramps and tails over three hardware queues, 40.96 MB 17.1 -> 13.2 us per
+// message, profiles/r01_stream_probe.jsonl) until r06: device packs have left for the AQL
+// queues, and every HIP stream costs one of the GPU's 24 compute queues.
+constexpr size_t kFillStreams = 1;
 
 // DORA_GPU_PIN=0: leave the node's CPU affinity alone (shm.cpp pin_to_numa)
 bool numa_pinning() {
