@@ -555,12 +555,15 @@ namespace {
 // the 20-cloud burst, profiles/r04_full_ab.jsonl).
 // Read-signalled packs (dora_aql_pack1r_u4): <= 12 units of 16 B per lane (aql_kernels.hip
 // kReadUnits), <= kMaxSignalWgs workgroups (their done words), so up to 192 MiB; 1024
-// workgroups unless that holds too little.
-constexpr uint64_t kReadLaneUnits = 12;
+// workgroups unless that holds too little, and no more than give every lane 4 units: a
+// synchronous 4 MiB send 8.4-8.7 -> 7.2-7.5 us against one unit per lane, 40.96 MB unchanged
+// (profiles/r06_read_grid_ab.jsonl; 8 units per lane 7.2-7.4).
+constexpr uint64_t kReadLaneUnits = 12, kReadLaneMin = 4;
 constexpr uint64_t kReadMaxUnits = uint64_t(kMaxSignalWgs) * 256 * kReadLaneUnits;
 uint32_t read_grid(uint64_t units) {
   const uint64_t need = (units + 256 * kReadLaneUnits - 1) / (256 * kReadLaneUnits);
-  const uint64_t fill = std::min<uint64_t>(1024, (units + 255) / 256);
+  const uint64_t fill =
+      std::min<uint64_t>(1024, (units + 256 * kReadLaneMin - 1) / (256 * kReadLaneMin));
   return static_cast<uint32_t>(std::max<uint64_t>(std::max(need, fill), 1));
 }
 int big_queues(int nq, uint64_t bytes) {
