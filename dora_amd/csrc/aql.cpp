@@ -553,12 +553,12 @@ namespace {
 // copies saturate HBM: 12.9-13.0 us per pack on three queues vs 13.2 on four,
 // profiles/r02_aql_big_ab.jsonl), four below (C3's 13 MB clouds: 0.71-0.72 -> 0.75 of HBM over
 // the 20-cloud burst, profiles/r04_full_ab.jsonl).
-// Read-signalled packs (dora_aql_pack1r_u4): <= 12 units of 16 B per lane (aql_kernels.hip
-// kReadUnits), <= kMaxSignalWgs workgroups (their done words), so up to 192 MiB; 1024
+// Read-signalled packs (dora_aql_pack1r_u4): <= kReadLaneUnits (12) units of 16 B per lane
+// (plan.h), <= kMaxSignalWgs workgroups (their done words), so up to 192 MiB; 1024
 // workgroups unless that holds too little, and no more than give every lane 4 units: a
 // synchronous 4 MiB send 8.4-8.7 -> 7.2-7.5 us against one unit per lane, 40.96 MB unchanged
 // (profiles/r06_read_grid_ab.jsonl; 8 units per lane 7.2-7.4).
-constexpr uint64_t kReadLaneUnits = 12, kReadLaneMin = 4;
+constexpr uint64_t kReadLaneMin = 4;
 constexpr uint64_t kReadMaxUnits = uint64_t(kMaxSignalWgs) * 256 * kReadLaneUnits;
 uint32_t read_grid(uint64_t units) {
   const uint64_t need = (units + 256 * kReadLaneUnits - 1) / (256 * kReadLaneUnits);

@@ -62,18 +62,17 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
   pack1<4, dora::pack::kCoherent>(dst, src, len, flag, done, epoch, chunk_bytes, grid);
 }
 
-// Read-signalled single-segment pack (aql.cpp: a synchronous send of 1-256 MiB, source and slot
+// Read-signalled single-segment pack (aql.cpp: a synchronous send of 1-192 MiB, source and slot
 // 16-byte aligned).  The reference's send_output returns once its source has been copied; a pack
 // that loads and stores chunk by chunk has read its last source byte only about when it has
 // written its last sample byte, so a synchronous send waited for the whole pack plus the host
 // round trip (0.47 of HBM per 40.96 MB message).  Here every workgroup first loads
-// its whole share of the source into VGPRs (<= kReadUnits 16-B units per lane), publishes that in
-// its done word once all its loads have returned, and only then stores; workgroup 0 waits for
-// every done word and raises the flag line's read word — the send returns there, and the next
-// send's loads overlap this pack's stores.  The fill itself is the dispatch's completion signal
-// (every wave waits for its own stores), as for the other lone packs; stamps as pack_body's CP
-// branch.
-constexpr int kReadUnits = 12;  // aql.cpp kReadLaneUnits
+// its whole share of the source into VGPRs (<= kReadLaneUnits 16-B units per lane, plan.h),
+// publishes that in its done word once all its loads have returned, and only then stores;
+// workgroup 0 waits for every done word and raises the flag line's read word — the send returns
+// there, and the next send's loads overlap this pack's stores.  The fill itself is the
+// dispatch's completion signal (every wave waits for its own stores), as for the other lone
+// packs; stamps as pack_body's CP branch.
 extern "C" __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8)))
 void dora_aql_pack1r_u4(
     uint8_t* dst, const uint8_t* src, uint64_t len, uint64_t* rflag, uint32_t* done,
@@ -90,9 +89,9 @@ void dora_aql_pack1r_u4(
   const uint32_t mine = u0 + t < u1 ? (u1 - u0 - t + kThreads - 1) / kThreads : 0;
   const uint32_t off = 16 * (u0 + t);
   const __amdgpu_buffer_rsrc_t rs = src_rsrc(src), rd = src_rsrc(dst);
-  u32x4 v[kReadUnits];
+  u32x4 v[kReadLaneUnits];
 #pragma unroll
-  for (int k = 0; k < kReadUnits; ++k)
+  for (int k = 0; k < int(kReadLaneUnits); ++k)
     if (uint32_t(k) < mine)
       v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * kThreads * k, kCoherentPolicy);
   const uint32_t tail = static_cast<uint32_t>(len & 15);
@@ -138,7 +137,7 @@ void dora_aql_pack1r_u4(
   }
   // write-through to device scope, as st16<kCoherent> (sc1 nt)
 #pragma unroll
-  for (int k = 0; k < kReadUnits; ++k)
+  for (int k = 0; k < int(kReadLaneUnits); ++k)
     if (uint32_t(k) < mine)
       __builtin_amdgcn_raw_buffer_store_b128(v[k], rd, off, 16 * kThreads * k, kCoherentPolicy);
   if (tail_lane) st1<kCoherent>(dst + 16 * uint64_t(units) + t, tb);

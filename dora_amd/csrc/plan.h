@@ -91,6 +91,9 @@ constexpr uint32_t kMaxSignalWgs = 4096;
 // The host does not read the words through the BAR (8 KiB of uncached reads per pack, ~57 ms
 // for a 200-send region, r04 trace): one AQL dispatch reduces them (aql_stamp_reduce).
 constexpr uint32_t kCpStampWgs = 1024;
+// Read-signalled packs (aql_kernels.hip dora_aql_pack1r_u4): 16-byte units of the source each
+// lane holds in VGPRs at most (62 VGPRs at 12: every workgroup of two 40.96 MB packs resident).
+constexpr uint32_t kReadLaneUnits = 12;
 
 // One message of a batch pack (aql.cpp): its copy segments, slot, fill signal, writable bytes.
 struct BatchItem {
