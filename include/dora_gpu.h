@@ -284,7 +284,12 @@ int dora_node_send_output_sample(dora_node* node, const char* output_id, const u
  * which copies the array inside the call
  * (arrow_utils.rs:48), the call returns once the sample no longer needs the source: for a
  * device source it waits (after the descriptor has left) until the pack kernel has read it, so
- * the caller may rewrite or free the source on any stream right away. */
+ * the caller may rewrite or free the source on any stream right away.  (A single-segment
+ * sample of 1-192 MiB from a 16-byte-aligned source is packed read-first: the call returns
+ * when every source byte is in the pack's registers, before its stores have drained.)  When
+ * every receiver of the output runs without a GPU, a device sample <= 1 MiB is packed into
+ * shared memory and a host sample >= 4096 B copied there by the CPU (DataMessage::SharedMemory,
+ * complete when the call returns). */
 int dora_node_send_output(dora_node* node, const char* output_id, const struct ArrowArray* array,
                           const struct ArrowSchema* schema, ArrowDeviceType device_type,
                           const uint8_t* params, size_t params_len);
