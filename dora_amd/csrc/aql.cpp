@@ -1233,6 +1233,59 @@ int aql_batch_stats(int device, uint64_t* batches, uint64_t* batched_msgs, uint6
   return DORA_OK;
 }
 
+namespace {
+hsa_status_t first_cpu_agent(hsa_agent_t a, void* p) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS &&
+      t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(p) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+}  // namespace
+
+int hsa_copy_to_host(void* dst, const void* src, uint64_t n) {
+  static hsa_agent_t cpu{};
+  static const bool ok = [] {
+    return hsa_init() == HSA_STATUS_SUCCESS &&
+           hsa_iterate_agents(first_cpu_agent, &cpu) == HSA_STATUS_INFO_BREAK;
+  }();
+  if (!ok) return fail(DORA_ERR_UNSUPPORTED, "no HSA CPU agent");
+  hsa_amd_pointer_info_t pi{};
+  pi.size = sizeof(pi);
+  hsa_device_type_t t{};
+  if (hsa_amd_pointer_info(const_cast<void*>(src), &pi, nullptr, nullptr, nullptr) !=
+          HSA_STATUS_SUCCESS ||
+      (pi.type != HSA_EXT_POINTER_TYPE_HSA && pi.type != HSA_EXT_POINTER_TYPE_IPC) ||
+      !pi.agentOwner.handle ||
+      hsa_agent_get_info(pi.agentOwner, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS ||
+      t != HSA_DEVICE_TYPE_GPU)
+    return fail(DORA_ERR_UNSUPPORTED, "source not device memory the runtime knows");
+  thread_local hsa_signal_t sig{0};
+  if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
+    sig.handle = 0;
+    return fail(DORA_ERR_UNSUPPORTED, "hsa_signal_create");
+  }
+  hsa_signal_store_relaxed(sig, 1);
+  if (hsa_amd_memory_async_copy(dst, cpu, src, pi.agentOwner, n, 0, nullptr, sig) !=
+      HSA_STATUS_SUCCESS)
+    return fail(DORA_ERR_UNSUPPORTED, "hsa_amd_memory_async_copy refused the copy");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0; hsa_signal_load_scacquire(sig) != 0; ++spin) {
+    __builtin_ia32_pause();
+    if ((spin & 1023) == 1023) {
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt > std::chrono::seconds(10)) {
+        sig.handle = 0;  // the copy may still complete: its signal is not reused
+        return fail(DORA_ERR_TIMEOUT, "copy engine did not complete in 10 s");
+      }
+      if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
+    }
+  }
+  return DORA_OK;
+}
+
 uint64_t aql_cp_signalled(int device) {
   if (device < 0 || device >= 64) return 0;
   AqlQueue* a;

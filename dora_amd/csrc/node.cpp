@@ -1420,10 +1420,15 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
 // producer GPU's copy engines into pinned host memory the input owns (recycled, host_pool), then
 // the producer's token goes back at once and the input is a host input like a shared-memory one
 // (the reference's receivers always get host ArrowData, event_stream/event.rs:35-91; a Python
-// receiver a pyarrow array, apis/python/operator/src/lib.rs:135-144).  4 KB: ~12.7 us, 40.96 MB:
-// 56 GB/s on an MI355X box (profiles/r06_host_path_probe.jsonl, d2h_pinned).  The pack kernel
-// writing pinned host memory from one raw AQL packet instead was slower at every size tried,
-// 23 / 27 / 30 us against 18 / 16 / 20 at 4 KB / 64 KB / 256 KB (profiles/r06_d2h_stage_ab.jsonl).
+// receiver a pyarrow array, apis/python/operator/src/lib.rs:135-144).  The copy is issued to the
+// copy engines through HSA and its signal polled (aql.h hsa_copy_to_host): 4 KB in 6.9 us where
+// hipMemcpyAsync + hipStreamSynchronize took 17 (scripts/d2h_copy_probe.py,
+// profiles/r06_d2h_copy_probe.jsonl); a 4 KB message to such a receiver beside a device one,
+// send call to receipt, 15.5-16.5 us p50 / 19-21 p99 against 20.9-21.9 / 37-38 with HIP's copy
+// (profiles/r06_stage_copy_ab.txt, five interleaved rounds); HIP's copy stays the fallback.  40.96 MB: 56 GB/s on an
+// MI355X box (profiles/r06_host_path_probe.jsonl, d2h_pinned).  The pack kernel writing pinned
+// host memory from one raw AQL packet of the receiver was slower at every size tried, 23 / 27 /
+// 30 us against 18 / 16 / 20 at 4 KB / 64 KB / 256 KB (profiles/r06_d2h_stage_ab.jsonl).
 int stage_to_host(InputData* in, int src_device) {
   NodeCore* c = in->core.get();
   if (in->ext_len) {
@@ -1433,10 +1438,19 @@ int stage_to_host(InputData* in, int src_device) {
     if (!h)
       return fail(DORA_ERR_HIP, "pinned staging buffer of %llu bytes",
                   (unsigned long long)in->ext_len);
-    hipStream_t st = c->stage_stream(src_device);
-    hipError_t e = st ? hipMemcpyAsync(h, in->ptr, in->ext_len, hipMemcpyDeviceToHost, st)
-                      : hipErrorInvalidResourceHandle;
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipError_t e = hipSuccess;
+    const int hrc = hsa_copy_to_host(h, in->ptr, in->ext_len);
+    if (hrc == DORA_ERR_TIMEOUT) return hrc;  // the buffer is not reused: the copy may still land
+    if (hrc != DORA_OK) {
+      static std::atomic<bool> noted{false};
+      if (std::getenv("DORA_GPU_TRACE") && !noted.exchange(true))
+        std::fprintf(stderr, "dora-gpu: staging through HIP's copy: %s\n", dora_gpu_last_error());
+      clear_error();
+      hipStream_t st = c->stage_stream(src_device);
+      e = st ? hipMemcpyAsync(h, in->ptr, in->ext_len, hipMemcpyDeviceToHost, st)
+             : hipErrorInvalidResourceHandle;
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+    }
     if (e != hipSuccess) {
       (void)hipGetLastError();
       c->host_pool_put(h, cap);

@@ -4,6 +4,8 @@
 // tests/ and scripts/ only.  Each hook calls into the library's internals (aql.cpp, kernels.hip,
 // bincode.cpp, bcast.cpp, shm.h).
 #include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <sys/prctl.h>
 
@@ -126,6 +128,77 @@ int dora_gpu_test_cp_arm(void* flag, uint64_t epoch) {
 
 
 int dora_gpu_test_aql_hold(int device, int hold) { return dora::aql_hold(device, hold != 0); }
+
+namespace {
+hsa_status_t find_cpu_agent(hsa_agent_t a, void* p) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS &&
+      t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(p) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+}  // namespace
+
+int dora_gpu_test_d2h_copy_probe(int device, int mode, uint64_t bytes, uint32_t n,
+                                 uint64_t gap_ns, uint64_t* out_ns) {
+  if (!out_ns || !n || !bytes) return dora::fail(DORA_ERR_INVALID, "copy probe: arguments");
+  DORA_HIP(hipSetDevice(device));
+  void* src = nullptr;
+  void* dst = nullptr;
+  hipStream_t st = nullptr;
+  DORA_HIP(hipMalloc(&src, bytes));
+  DORA_HIP(hipMemset(src, 0x5a, bytes));
+  DORA_HIP(hipHostMalloc(&dst, bytes, 0));
+  DORA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  DORA_HIP(hipDeviceSynchronize());
+  hsa_agent_t gpu{}, cpu{};
+  hsa_signal_t sig{0};
+  if (mode == 1) {
+    hsa_amd_pointer_info_t pi{};
+    pi.size = sizeof(pi);
+    if (hsa_init() != HSA_STATUS_SUCCESS ||
+        hsa_amd_pointer_info(src, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        hsa_iterate_agents(find_cpu_agent, &cpu) != HSA_STATUS_INFO_BREAK ||
+        hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+      return dora::fail(DORA_ERR_HIP, "copy probe: HSA setup");
+    gpu = pi.agentOwner;
+  }
+  using clock = std::chrono::steady_clock;
+  int rc = DORA_OK;
+  for (uint32_t i = 0; i < n && rc == DORA_OK; ++i) {
+    const auto until = clock::now() + std::chrono::nanoseconds(gap_ns);
+    while (clock::now() < until) std::this_thread::yield();
+    const auto t0 = clock::now();
+    if (mode == 1) {
+      hsa_signal_store_relaxed(sig, 1);
+      if (hsa_amd_memory_async_copy(dst, cpu, src, gpu, bytes, 0, nullptr, sig) !=
+          HSA_STATUS_SUCCESS) {
+        rc = dora::fail(DORA_ERR_HIP, "hsa_amd_memory_async_copy");
+        break;
+      }
+      while (hsa_signal_load_scacquire(sig) != 0) {
+        __builtin_ia32_pause();
+        if (clock::now() - t0 > std::chrono::seconds(2)) {
+          rc = dora::fail(DORA_ERR_TIMEOUT, "copy probe: no completion");
+          break;
+        }
+      }
+    } else if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipStreamSynchronize(st) != hipSuccess) {
+      rc = dora::fail(DORA_ERR_HIP, "hipMemcpyAsync");
+    }
+    out_ns[i] = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(clock::now() - t0).count());
+  }
+  if (rc == DORA_OK && static_cast<const uint8_t*>(dst)[bytes - 1] != 0x5a)
+    rc = dora::fail(DORA_ERR_INVALID, "copy probe: wrong bytes");
+  if (sig.handle && rc == DORA_OK) hsa_signal_destroy(sig);
+  (void)hipStreamDestroy(st);
+  (void)hipHostFree(dst);
+  (void)hipFree(src);
+  return rc;
+}
 
 int dora_gpu_test_reduce_timeout(uint64_t ns) {
   dora::aql_reduce_timeout(ns);

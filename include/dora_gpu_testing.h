@@ -32,6 +32,11 @@ int dora_gpu_test_aql_hold(int device, int hold);
  * (ns; 0 = the default 5 s) — a tiny value makes the wait time out while the packet still runs —
  * and the AQL argument slots left to reductions that timed out (never written again). */
 int dora_gpu_test_reduce_timeout(uint64_t ns);
+/* Experiment: `n` D2H copies of `bytes` from HBM into pinned host memory, `gap_ns` apart, each
+ * timed call -> complete into out_ns[n]: mode 0 hipMemcpyAsync + hipStreamSynchronize on a
+ * stream of its own, mode 1 hsa_amd_memory_async_copy + a busy wait on its signal. */
+int dora_gpu_test_d2h_copy_probe(int device, int mode, uint64_t bytes, uint32_t n,
+                                 uint64_t gap_ns, uint64_t* out_ns);
 int dora_gpu_test_abandoned_slots(int device, uint32_t* slots);
 /* Test tool: empty packets the keep-awake thread of `device` has published in this process
  * (dora_gpu_set_keep_awake), and whether it is parked (no send for 100 ms). */

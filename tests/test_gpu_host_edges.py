@@ -185,6 +185,20 @@ def test_host_only_receiver_staging_stress(launcher):
                 del ev
         assert tx.host_paths()["host_packs"] >= 300, tx.host_paths()
         assert rx.host_paths()["staged"] >= 300, rx.host_paths()
+        # the staging edge's latency (device 4 KB -> host-only receiver beside a device one), for
+        # the record
+        lat = []
+        for k in range(200):
+            t0 = time.perf_counter()
+            tx.send_output_device_bytes("y", buf.ptr, 4096, {"k": k})
+            ev = rx.next(timeout=30)
+            lat.append((time.perf_counter() - t0) * 1e6)
+            del ev
+            ev = gx.next(timeout=30)  # the device receiver's copy of the same message
+            del ev
+        lat.sort()
+        print(f"device 4 KB -> host-only receiver, staged: p50 {lat[100]:.2f} us, "
+              f"p99 {lat[198]:.2f} us")
         tx.close()
         rx.close()
         gx.close()
