@@ -1245,31 +1245,42 @@ hsa_status_t first_cpu_agent(hsa_agent_t a, void* p) {
 }
 }  // namespace
 
-int hsa_copy_to_host(void* dst, const void* src, uint64_t n) {
+namespace {
+// The GPU agent owning device memory `p` (this process's or IPC-imported), or none.
+bool gpu_owner(const void* p, hsa_agent_t* out) {
+  hsa_amd_pointer_info_t pi{};
+  pi.size = sizeof(pi);
+  hsa_device_type_t t{};
+  if (hsa_amd_pointer_info(const_cast<void*>(p), &pi, nullptr, nullptr, nullptr) !=
+          HSA_STATUS_SUCCESS ||
+      (pi.type != HSA_EXT_POINTER_TYPE_HSA && pi.type != HSA_EXT_POINTER_TYPE_IPC) ||
+      !pi.agentOwner.handle ||
+      hsa_agent_get_info(pi.agentOwner, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS ||
+      t != HSA_DEVICE_TYPE_GPU)
+    return false;
+  *out = pi.agentOwner;
+  return true;
+}
+}  // namespace
+
+int hsa_copy_host(void* dst, const void* src, uint64_t n, bool to_host) {
   static hsa_agent_t cpu{};
   static const bool ok = [] {
     return hsa_init() == HSA_STATUS_SUCCESS &&
            hsa_iterate_agents(first_cpu_agent, &cpu) == HSA_STATUS_INFO_BREAK;
   }();
   if (!ok) return fail(DORA_ERR_UNSUPPORTED, "no HSA CPU agent");
-  hsa_amd_pointer_info_t pi{};
-  pi.size = sizeof(pi);
-  hsa_device_type_t t{};
-  if (hsa_amd_pointer_info(const_cast<void*>(src), &pi, nullptr, nullptr, nullptr) !=
-          HSA_STATUS_SUCCESS ||
-      (pi.type != HSA_EXT_POINTER_TYPE_HSA && pi.type != HSA_EXT_POINTER_TYPE_IPC) ||
-      !pi.agentOwner.handle ||
-      hsa_agent_get_info(pi.agentOwner, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS ||
-      t != HSA_DEVICE_TYPE_GPU)
-    return fail(DORA_ERR_UNSUPPORTED, "source not device memory the runtime knows");
+  hsa_agent_t gpu{};
+  if (!gpu_owner(to_host ? src : dst, &gpu))
+    return fail(DORA_ERR_UNSUPPORTED, "not device memory the runtime knows");
   thread_local hsa_signal_t sig{0};
   if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
     sig.handle = 0;
     return fail(DORA_ERR_UNSUPPORTED, "hsa_signal_create");
   }
   hsa_signal_store_relaxed(sig, 1);
-  if (hsa_amd_memory_async_copy(dst, cpu, src, pi.agentOwner, n, 0, nullptr, sig) !=
-      HSA_STATUS_SUCCESS)
+  if (hsa_amd_memory_async_copy(dst, to_host ? cpu : gpu, src, to_host ? gpu : cpu, n, 0, nullptr,
+                                sig) != HSA_STATUS_SUCCESS)
     return fail(DORA_ERR_UNSUPPORTED, "hsa_amd_memory_async_copy refused the copy");
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0; hsa_signal_load_scacquire(sig) != 0; ++spin) {

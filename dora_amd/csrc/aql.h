@@ -109,12 +109,13 @@ void bar_publish(AqlQueue* q, const void* last);
 int aql_stamp_reduce(int device, const uint64_t* base, uint32_t area_words,
                      const uint32_t* areas, uint32_t n, uint64_t* out);
 
-// One copy-engine copy of `n` bytes from device memory `src` (this process's or IPC-imported)
-// into host memory `dst` every agent can reach (pinned), waited for by polling its signal: a 4 KB
-// sample in 6.9 us against 17 for hipMemcpyAsync + hipStreamSynchronize, equal from ~64 KB
-// (scripts/d2h_copy_probe.py, profiles/r06_d2h_copy_probe.jsonl).  DORA_ERR_UNSUPPORTED when the
-// runtime cannot take it (the caller uses HIP's copy); DORA_ERR_TIMEOUT after 10 s.
-int hsa_copy_to_host(void* dst, const void* src, uint64_t n);
+// One copy-engine copy of `n` bytes between device memory (this process's or IPC-imported) and
+// pinned host memory — `to_host`: `src` is the device side, else `dst` — waited for by polling its
+// signal: a 4 KB sample to the host in 6.9 us against 17 for hipMemcpyAsync +
+// hipStreamSynchronize, equal from ~64 KB (scripts/d2h_copy_probe.py,
+// profiles/r06_d2h_copy_probe.jsonl).  DORA_ERR_UNSUPPORTED when the runtime cannot take it (the
+// caller uses HIP's copy); DORA_ERR_TIMEOUT after 10 s.
+int hsa_copy_host(void* dst, const void* src, uint64_t n, bool to_host);
 // Test hooks: the stamp reduction's wait (0: the default 5 s), and the argument slots left to
 // reductions that timed out (never written again).
 void aql_reduce_timeout(uint64_t ns);

@@ -1421,7 +1421,7 @@ void encode_event(dora_node* n, uint32_t kind, const std::vector<uint8_t>& p) {
 // the producer's token goes back at once and the input is a host input like a shared-memory one
 // (the reference's receivers always get host ArrowData, event_stream/event.rs:35-91; a Python
 // receiver a pyarrow array, apis/python/operator/src/lib.rs:135-144).  The copy is issued to the
-// copy engines through HSA and its signal polled (aql.h hsa_copy_to_host): 4 KB in 6.9 us where
+// copy engines through HSA and its signal polled (aql.h hsa_copy_host): 4 KB in 6.9 us where
 // hipMemcpyAsync + hipStreamSynchronize took 17 (scripts/d2h_copy_probe.py,
 // profiles/r06_d2h_copy_probe.jsonl); a 4 KB message to such a receiver beside a device one,
 // send call to receipt, 15.5-16.5 us p50 / 19-21 p99 against 20.9-21.9 / 37-38 with HIP's copy
@@ -1439,7 +1439,7 @@ int stage_to_host(InputData* in, int src_device) {
       return fail(DORA_ERR_HIP, "pinned staging buffer of %llu bytes",
                   (unsigned long long)in->ext_len);
     hipError_t e = hipSuccess;
-    const int hrc = hsa_copy_to_host(h, in->ptr, in->ext_len);
+    const int hrc = hsa_copy_host(h, in->ptr, in->ext_len, true);
     if (hrc == DORA_ERR_TIMEOUT) return hrc;  // the buffer is not reused: the copy may still land
     if (hrc != DORA_OK) {
       static std::atomic<bool> noted{false};
@@ -1653,9 +1653,19 @@ int ensure_local(InputData* in) {
         (void)hipGetLastError();
       }
     }
-    hipError_t e = hipMemcpyAsync(local, in->ptr, in->ext_len, hipMemcpyHostToDevice, ps);
-    if (e == hipSuccess) e = hipStreamSynchronize(ps);
-    if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "shared-memory pull: %s", hipGetErrorString(e));
+    // the copy engines through HSA, its signal polled (as stage_to_host), once the region is
+    // pinned; else HIP's copy.  Host-only 4 KB to a device receiver, send call to receipt:
+    // 10.8-14.3 us p50 / 23-32 p99 against 17.5-20.3 / 45-58 (profiles/r06_pull_copy_ab.txt)
+    rc = in->shm->registered ? hsa_copy_host(local, in->ptr, in->ext_len, false)
+                             : int(DORA_ERR_UNSUPPORTED);
+    if (rc == DORA_ERR_TIMEOUT) return rc;  // the receive slot is not reused: the copy may land
+    if (rc != DORA_OK) {
+      clear_error();
+      rc = DORA_OK;
+      hipError_t e = hipMemcpyAsync(local, in->ptr, in->ext_len, hipMemcpyHostToDevice, ps);
+      if (e == hipSuccess) e = hipStreamSynchronize(ps);
+      if (e != hipSuccess) rc = fail(DORA_ERR_HIP, "shared-memory pull: %s", hipGetErrorString(e));
+    }
   } else if (peer_copy_mode() == PEER_SDMA) {
     rc = ensure_peer_access(c, in->remote_device);
     if (rc == DORA_OK) {

@@ -158,6 +158,17 @@ def test_host_only_node_shared_memory_to_device_receiver(launcher):
         # one region per size of the first round; 4099 B takes the best-fitting larger region,
         # and the second round creates none
         assert st["slots_created"] == 3 and st["cache_hits"] >= 5, st
+        # the edge's latency (host-only 4 KB -> device receiver, pulled on receipt), for the record
+        lat = []
+        for k in range(200):
+            t0 = time.perf_counter()
+            tx.send_output("x", payloads[4096], {"k": k})
+            ev = rx.next(timeout=30)
+            lat.append((time.perf_counter() - t0) * 1e6)
+            del ev
+        lat.sort()
+        print(f"host-only 4 KB -> device receiver, pulled: p50 {lat[100]:.2f} us, "
+              f"p99 {lat[198]:.2f} us")
         tx.close()
         rx.close()
         df.wait(30)
