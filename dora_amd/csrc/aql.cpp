@@ -111,6 +111,8 @@ constexpr const char* kKernelNames[kKernels] = {"dora_aql_pack_u4", "dora_aql_pa
 // on MI355X, the alternatives are not built any more):
 // * four HSA queues per process: 4 MB 2.4 -> 2.1 us per message, C3 2.09 -> 2.41 TB/s against
 //   two (profiles/r01_aql_queues_ab.jsonl);
+//   Three instead (one compute queue fewer per sending process): C3 0.74-0.75 ->
+//   0.65-0.66, native 4 MB 1.35-1.41 -> 1.91 us per message (profiles/r06_queues_ab.jsonl);
 constexpr int kQueues = 4;
 // * packs of [1 MiB, 32 MiB) are signalled by the command processor (the packet's completion
 //   signal, every wave waiting for its own stores), so consecutive packets of a queue overlap:
