@@ -1245,9 +1245,7 @@ hsa_status_t first_cpu_agent(hsa_agent_t a, void* p) {
   }
   return HSA_STATUS_SUCCESS;
 }
-}  // namespace
 
-namespace {
 // The GPU agent owning device memory `p` (this process's or IPC-imported), or none.
 bool gpu_owner(const void* p, hsa_agent_t* out) {
   hsa_amd_pointer_info_t pi{};
