@@ -143,6 +143,7 @@ _SIGS = {
     "dora_node_set_profiling": (c_int, [c_void_p, c_int]),
     "dora_node_set_timing_period": (c_int, [c_void_p, c_uint64]),
     "dora_node_fill_paths": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "dora_node_host_bound_outputs": (c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
     "dora_node_host_paths": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64),
                                      POINTER(c_uint64), POINTER(c_uint64)]),
     "dora_node_plan_cache_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),

@@ -2722,8 +2722,9 @@ int dora_node_init(const char* shm_name, const char* node_id, int device, dora_n
     std::vector<uint8_t> p;
     if (core->ev.try_pop(&kind, &p)) {
       if (kind == dora::EV_READY) {
-        // the outputs whose receivers all lack a GPU (daemon.cpp ready_payload)
-        if (device >= 0 && p.size() >= 4) {
+        // the outputs whose receivers all lack a GPU (daemon.cpp ready_payload); kept on a
+        // host-only node too, for dora_node_host_bound_outputs, though only a device node packs
+        if (p.size() >= 4) {
           dora::RBuf r(p);
           for (uint32_t k = r.u32(); k > 0; --k) n->host_bound.insert(r.str());
         }
@@ -3268,6 +3269,17 @@ int dora_node_host_paths(dora_node* n, uint64_t* bar_fills, uint64_t* staged,
   if (host_packs) *host_packs = n->host_packs + n->host_copies;
   if (staged) *staged = n->core->host_staged.load();
   if (staged_bytes) *staged_bytes = n->core->host_staged_bytes.load();
+  return DORA_OK;
+}
+
+int dora_node_host_bound_outputs(dora_node* n, char* buf, uint64_t cap, uint64_t* len) {
+  if (!n) return dora::fail(DORA_ERR_INVALID, "NULL node");
+  std::string all;
+  for (const auto& o : n->host_bound) all += o + "\n";
+  if (len) *len = all.size();
+  if (!buf) return DORA_OK;
+  if (cap < all.size() + 1) return dora::fail(DORA_ERR_INVALID, "buffer too small");
+  std::memcpy(buf, all.c_str(), all.size() + 1);
   return DORA_OK;
 }
 

@@ -399,6 +399,15 @@ class Node:
         return {"bar_fills": a.value, "staged": b.value, "staged_bytes": c.value,
                 "host_packs": d.value}
 
+    def host_bound_outputs(self) -> list:
+        """The outputs the daemon named host-bound in AllNodesReady: all receivers lack a GPU
+        (dora_node_host_bound_outputs)."""
+        n = c_uint64()
+        call("dora_node_host_bound_outputs", self.handle, None, 0, byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        call("dora_node_host_bound_outputs", self.handle, buf, n.value + 1, byref(n))
+        return buf.value.decode().split("\n")[:-1] if n.value else []
+
     def set_timing_period(self, period: int):
         """Stamp every `period`-th pack launch (0: the default, every 8th)."""
         call("dora_node_set_timing_period", self.handle, int(period))

@@ -390,6 +390,12 @@ int dora_node_fill_paths(dora_node* node, uint64_t* aql_packs, uint64_t* hip_pac
  * sources >= 4096 B copied there by the CPU.  Any pointer may be NULL. */
 int dora_node_host_paths(dora_node* node, uint64_t* bar_fills, uint64_t* staged,
                          uint64_t* staged_bytes, uint64_t* host_packs);
+/* The outputs of this node the daemon named host-bound in AllNodesReady (new; diagnostics):
+ * every receiver is a running local node without a GPU and none is on another machine, so a
+ * device node packs them into shared memory (above).  Newline-terminated names, sorted, NUL
+ * after the last; *len (if not NULL) = their bytes without the NUL.  buf NULL: only *len;
+ * cap < *len + 1: DORA_ERR_INVALID. */
+int dora_node_host_bound_outputs(dora_node* node, char* buf, uint64_t cap, uint64_t* len);
 /* dora_node_send_output of device arrays keeps the plans of recent sends that read no array
  * bytes (fixed-width and nested arrays with known null counts), keyed by everything such a plan
  * depends on (schema strings and flags, lengths, offsets, null counts, buffer addresses): a

@@ -233,6 +233,29 @@ def test_zero_length_sample_and_ordering():
     d.join()
 
 
+def test_all_nodes_ready_names_host_bound_outputs():
+    """AllNodesReady carries, for each node, the outputs whose every receiver is a running local
+    node without a GPU (daemon.cpp ready_payload): a device producer packs those into shared
+    memory instead of HBM.  An output nobody reads is not named; the consumer's own outputs go
+    nowhere.  (Device receivers and receivers on another machine exclude an output: the first is
+    covered by tests/test_gpu_host_edges.py, the second by tests/test_interdaemon.py.)"""
+    d = InProcessDaemon({"nodes": [
+        {"id": "a", "outputs": ["to_b", "unread", "to_both"]},
+        {"id": "b", "inputs": {"x": "a/to_b", "y": "a/to_both"}, "outputs": ["back"]},
+        {"id": "c", "inputs": {"y": "a/to_both", "z": "b/back"}}]})
+    nodes = _start_nodes(d.shm, ["a", "b", "c"])
+    assert nodes["a"].host_bound_outputs() == ["to_b", "to_both"]
+    assert nodes["b"].host_bound_outputs() == ["back"]
+    assert nodes["c"].host_bound_outputs() == []
+    nodes["a"].close()
+    for k in ("b", "c"):
+        while nodes[k].next(timeout=5) is not None:
+            pass
+        nodes[k].close()
+    d.join()
+    assert d.rc == 0
+
+
 def test_host_only_shared_memory_samples_recycle():
     """A host-only node sends samples >= 4096 B as DataMessage::SharedMemory (the reference's
     allocate_shared_memory, apis/rust/node/src/node/mod.rs:321-346): the receiver reads the

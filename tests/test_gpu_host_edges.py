@@ -168,6 +168,8 @@ def test_host_only_receiver_staging_stress(launcher):
     with Dataflow(desc, launcher=launcher) as df:
         n = _nodes(df, {"src": 0, "dst": -1, "gpu": 0})
         tx, rx, gx = n["src"], n["dst"], n["gpu"]
+        # AllNodesReady names x only: y also has a receiver with a GPU
+        assert tx.host_bound_outputs() == ["x"]
         for k in range(600):
             z = sizes[k % len(sizes)]
             out = "x" if k % 2 == 0 else "y"

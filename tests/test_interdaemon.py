@@ -82,6 +82,9 @@ def test_two_daemons_deliver_in_order_and_close(tmp_path):
         lt.start()
         src = _open(a, "src")
         lt.join(30)
+        # receivers on another machine keep an output off the host-bound list of AllNodesReady
+        # (daemon.cpp ready_payload): "side" also has a local host-only receiver
+        assert src.host_bound_outputs() == []
         sent = []
         for i in range(100):
             # every tenth message >= 4096 B: a shared-memory sample on A (read by the
