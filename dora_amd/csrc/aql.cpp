@@ -1273,27 +1273,43 @@ int hsa_copy_host(void* dst, const void* src, uint64_t n, bool to_host) {
   hsa_agent_t gpu{};
   if (!gpu_owner(to_host ? src : dst, &gpu))
     return fail(DORA_ERR_UNSUPPORTED, "not device memory the runtime knows");
-  thread_local hsa_signal_t sig{0};
-  if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
-    sig.handle = 0;
-    return fail(DORA_ERR_UNSUPPORTED, "hsa_signal_create");
+  // completion signals are pooled process-wide (any thread may stage or pull; a signal per
+  // thread would leak with every short-lived one), and never destroyed: the pool is as large as
+  // the most copies ever in flight at once
+  // (never freed either: a thread still copying during exit finds them)
+  static auto* pool_mu = new std::mutex;
+  static auto* pool = new std::vector<hsa_signal_t>;
+  hsa_signal_t sig{0};
+  {
+    std::lock_guard<std::mutex> g(*pool_mu);
+    if (!pool->empty()) {
+      sig = pool->back();
+      pool->pop_back();
+    }
   }
+  if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+    return fail(DORA_ERR_UNSUPPORTED, "hsa_signal_create");
+  auto give_back = [&] {
+    std::lock_guard<std::mutex> g(*pool_mu);
+    pool->push_back(sig);
+  };
   hsa_signal_store_relaxed(sig, 1);
   if (hsa_amd_memory_async_copy(dst, to_host ? cpu : gpu, src, to_host ? gpu : cpu, n, 0, nullptr,
-                                sig) != HSA_STATUS_SUCCESS)
+                                sig) != HSA_STATUS_SUCCESS) {
+    give_back();
     return fail(DORA_ERR_UNSUPPORTED, "hsa_amd_memory_async_copy refused the copy");
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0; hsa_signal_load_scacquire(sig) != 0; ++spin) {
     __builtin_ia32_pause();
     if ((spin & 1023) == 1023) {
       const auto dt = std::chrono::steady_clock::now() - t0;
-      if (dt > std::chrono::seconds(10)) {
-        sig.handle = 0;  // the copy may still complete: its signal is not reused
+      if (dt > std::chrono::seconds(10))  // the copy may still complete: its signal is dropped
         return fail(DORA_ERR_TIMEOUT, "copy engine did not complete in 10 s");
-      }
       if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
     }
   }
+  give_back();
   return DORA_OK;
 }
 
