@@ -198,6 +198,7 @@ _TEST_SIGS = {
     "dora_gpu_test_aql_hold": (c_int, [c_int, c_int]),
     "dora_gpu_test_reduce_timeout": (c_int, [c_uint64]),
     "dora_gpu_test_d2h_copy_probe": (c_int, [c_int, c_int, c_uint64, c_uint32, c_uint64, c_void_p]),
+    "dora_gpu_test_stream_order_probe": (c_int, [c_int, c_int, c_uint64, c_uint32, c_void_p]),
     "dora_gpu_test_abandoned_slots": (c_int, [c_int, POINTER(c_uint32)]),
     "dora_gpu_test_keep_awake_stats": (c_int, [c_int, POINTER(c_uint64), POINTER(c_int)]),
     "dora_gpu_test_aql_ring_wc": (c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),

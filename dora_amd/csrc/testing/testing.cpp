@@ -200,6 +200,50 @@ int dora_gpu_test_d2h_copy_probe(int device, int mode, uint64_t bytes, uint32_t 
   return rc;
 }
 
+// Experiment: what ordering a sample written on the node stream costs per message
+// (dora_node_send_output_sample -> order_fill): `n` kernels writing `bytes` on one stream, each
+// followed by nothing (mode 0), hipStreamWriteValue64 into pinned host memory like a fill flag
+// (1), or a second 8-byte kernel (2).  out_ns[0] = host enqueue ns per message, out_ns[1] =
+// enqueue + drain ns per message.
+int dora_gpu_test_stream_order_probe(int device, int mode, uint64_t bytes, uint32_t n,
+                                     uint64_t* out_ns) {
+  if (!out_ns || !n || !bytes || mode < 0 || mode > 2)
+    return dora::fail(DORA_ERR_INVALID, "stream order probe: arguments");
+  DORA_HIP(hipSetDevice(device));
+  void* buf = nullptr;
+  void* tiny = nullptr;
+  uint64_t* word = nullptr;
+  hipStream_t st = nullptr;
+  DORA_HIP(hipMalloc(&buf, bytes));
+  DORA_HIP(hipMalloc(&tiny, 64));
+  DORA_HIP(hipHostMalloc(reinterpret_cast<void**>(&word), 64, hipHostMallocMapped));
+  DORA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  DORA_HIP(hipDeviceSynchronize());
+  int rc = DORA_OK;
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  for (uint32_t i = 0; i < n && rc == DORA_OK; ++i) {
+    rc = dora_gpu_fill_splitmix(buf, bytes, i, st);
+    if (rc != DORA_OK) break;
+    if (mode == 1 && hipStreamWriteValue64(st, word, i + 1, 0) != hipSuccess)
+      rc = dora::fail(DORA_ERR_HIP, "hipStreamWriteValue64");
+    if (mode == 2) rc = dora_gpu_fill_splitmix(tiny, 8, i, st);
+  }
+  const auto t1 = clock::now();
+  if (hipStreamSynchronize(st) != hipSuccess && rc == DORA_OK)
+    rc = dora::fail(DORA_ERR_HIP, "hipStreamSynchronize");
+  const auto t2 = clock::now();
+  out_ns[0] = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count()) / n;
+  out_ns[1] = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t0).count()) / n;
+  if (rc == DORA_OK && mode == 1 && *reinterpret_cast<volatile uint64_t*>(word) != n)
+    rc = dora::fail(DORA_ERR_INVALID, "stream order probe: flag %llu", (unsigned long long)*word);
+  (void)hipStreamDestroy(st);
+  (void)hipHostFree(word);
+  (void)hipFree(tiny);
+  (void)hipFree(buf);
+  return rc;
+}
+
 int dora_gpu_test_reduce_timeout(uint64_t ns) {
   dora::aql_reduce_timeout(ns);
   return DORA_OK;

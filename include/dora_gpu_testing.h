@@ -37,6 +37,11 @@ int dora_gpu_test_reduce_timeout(uint64_t ns);
  * stream of its own, mode 1 hsa_amd_memory_async_copy + a busy wait on its signal. */
 int dora_gpu_test_d2h_copy_probe(int device, int mode, uint64_t bytes, uint32_t n,
                                  uint64_t gap_ns, uint64_t* out_ns);
+/* Experiment: per-message cost of ordering a sample written on a stream — `n` kernels writing
+ * `bytes`, each followed by nothing (mode 0), hipStreamWriteValue64 into pinned host memory (1)
+ * or an 8-byte kernel (2); out_ns[0] host enqueue, out_ns[1] enqueue + drain, ns per message. */
+int dora_gpu_test_stream_order_probe(int device, int mode, uint64_t bytes, uint32_t n,
+                                     uint64_t* out_ns);
 int dora_gpu_test_abandoned_slots(int device, uint32_t* slots);
 /* Test tool: empty packets the keep-awake thread of `device` has published in this process
  * (dora_gpu_set_keep_awake), and whether it is parked (no send for 100 ms). */
