@@ -70,7 +70,10 @@ extern "C" __global__ __launch_bounds__(kThreads) void dora_aql_pack1c_u4(
 // its whole share of the source into VGPRs (<= kReadLaneUnits 16-B units per lane, plan.h),
 // publishes that in its done word once all its loads have returned, and only then stores;
 // workgroup 0 waits for every done word and raises the flag line's read word — the send returns
-// there, and the next send's loads overlap this pack's stores.  The fill itself is the
+// there, and the next send's loads overlap this pack's stores.  The other workgroups hold their
+// stores until workgroup 0 raises a go word with it (≤ 20 us): early stores slowed the loads
+// the read word waits for (40.96 MB synchronous sends 18.3-18.9 -> 16.8-17.3 us per message,
+// profiles/r06_gate_ab.jsonl).  The fill itself is the
 // dispatch's completion signal (every wave waits for its own stores), as for the other lone
 // packs; stamps as pack_body's CP branch.
 extern "C" __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8)))
@@ -102,6 +105,8 @@ void dora_aql_pack1r_u4(
   __syncthreads();
   const uint32_t e = static_cast<uint32_t>(epoch);
   if (t == 0) __hip_atomic_store(done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the flag's last done word, when the grid leaves it free: workgroup 0's go for the stores
+  uint32_t* const go = grid < kMaxSignalWgs ? done + (kMaxSignalWgs - 1) : nullptr;
   if (blk == 0) {
     // as signal_fill: every done word at once per round, bounded (a lost workgroup leaves the
     // read word unset; the send then waits for the fill instead)
@@ -129,11 +134,29 @@ void dora_aql_pack1r_u4(
       const bool all = missing == 0;
       __syncthreads();
       if (all) {
-        if (t == 0) __hip_atomic_store(rflag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t == 0) {
+          __hip_atomic_store(rflag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (go) __hip_atomic_store(go, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
+  } else if (go) {
+    // the stores wait for every workgroup's loads (the go word, raised with the read word), so
+    // the loads run alone at the read rate and the send returns sooner; bounded (a workgroup
+    // that is not resident yet cannot hold the others past kGoWaitTicks)
+    constexpr uint64_t kGoWaitTicks = 2000;  // 20 us at 100 MHz
+    __shared__ uint32_t gone;
+    if (t == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e &&
+             __builtin_amdgcn_s_memrealtime() - t0 < kGoWaitTicks)
+        __builtin_amdgcn_s_sleep(1);
+      gone = 1;
+    }
+    __syncthreads();
+    (void)gone;
   }
   // write-through to device scope, as st16<kCoherent> (sc1 nt)
 #pragma unroll
