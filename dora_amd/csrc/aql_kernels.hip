@@ -147,16 +147,13 @@ void dora_aql_pack1r_u4(
     // the loads run alone at the read rate and the send returns sooner; bounded (a workgroup
     // that is not resident yet cannot hold the others past kGoWaitTicks)
     constexpr uint64_t kGoWaitTicks = 2000;  // 20 us at 100 MHz
-    __shared__ uint32_t gone;
     if (t == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != e &&
              __builtin_amdgcn_s_memrealtime() - t0 < kGoWaitTicks)
         __builtin_amdgcn_s_sleep(1);
-      gone = 1;
     }
     __syncthreads();
-    (void)gone;
   }
   // write-through to device scope, as st16<kCoherent> (sc1 nt)
 #pragma unroll
