@@ -105,8 +105,10 @@ void dora_aql_pack1r_u4(
   __syncthreads();
   const uint32_t e = static_cast<uint32_t>(epoch);
   if (t == 0) __hip_atomic_store(done + blk, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the flag's last done word, when the grid leaves it free: workgroup 0's go for the stores
-  uint32_t* const go = grid < kMaxSignalWgs ? done + (kMaxSignalWgs - 1) : nullptr;
+  // workgroup 0's go for the stores: the flag's last done word, free below kMaxSignalWgs.  Only
+  // for grids an idle GPU holds at once (<= 1024 of these 63-VGPR workgroups, a 50 MB pack): a
+  // larger one would hold its resident workgroups for the whole bound while the rest wait
+  uint32_t* const go = grid <= 1024 ? done + (kMaxSignalWgs - 1) : nullptr;
   if (blk == 0) {
     // as signal_fill: every done word at once per round, bounded (a lost workgroup leaves the
     // read word unset; the send then waits for the fill instead)
