@@ -1398,6 +1398,9 @@ def compact_line(line, detail_path):
     if sh:
         out["sync_send"] = _pick(sh, "us_per_msg", "hbm_frac_2S", "pack_own_us", "pack_own_frac",
                                  "gap_us_median")
+        # read-first packs hold their stores until every workgroup's loads are in:
+        # own time counts that wait and the next pack starts before this one ends
+        out["sync_send"]["note"] = "own incl. held-store wait; gap<0: packs overlap"
     if line.get("sync_send_4mb"):
         out["sync_send_4mb"] = _pick(line["sync_send_4mb"], "us_per_msg", "hbm_frac_2S")
     mid = {}
